@@ -1,0 +1,337 @@
+// Python bindings for the MI355X kernels and the native checkpoint engine.
+//
+// Kernels live in lean .hip translation units exposing extern "C" launchers (raw pointers +
+// hipStream_t); this file is the only one that includes the torch headers.  Every launcher
+// runs on the caller's current HIP stream so ops compose with torch stream semantics and
+// hipGraph capture.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <pybind11/stl.h>
+
+#include "kernels/args.h"
+#include "runtime/ckpt_engine.cpp"
+
+using torch::Tensor;
+namespace py = pybind11;
+
+extern "C" {
+int rtdc_gemm_bf16(const rtdc::GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
+                   hipStream_t stream);
+int rtdc_gemm_f32(const rtdc::GemmF32Args* args, hipStream_t st);
+int rtdc_layernorm_fwd(const void* x, const void* g, const void* b, void* y, float* mean, float* rstd,
+                       int M, int D, float eps, hipStream_t st);
+int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rstd, int M, int D, float eps,
+                     hipStream_t st);
+int rtdc_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean, const float* rstd,
+                       const void* dres, void* dx, float* ws, float* dg, float* db, int M, int D,
+                       int nwaves, int accumulate, hipStream_t st);
+int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, const float* rstd, const void* dres,
+                     void* dx, float* ws, float* dg, int M, int D, int nwaves, int accumulate,
+                     hipStream_t st);
+int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out, int accumulate,
+                int is_bf16, hipStream_t st);
+int rtdc_xent(const void* logits, void* dlogits, const int64_t* target, float* loss, float* lse,
+              int64_t* argmax, int M, int V, int ld, float grad_scale, int ignore_index, int is_bf16,
+              hipStream_t st);
+int rtdc_adamw(const void* chunks, int nchunks, float* p, const float* g, float* m, float* v, void* shadow,
+               float lr, float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt,
+               float grad_scale, hipStream_t st);
+int rtdc_sgd(const void* chunks, int nchunks, float* p, const float* g, float* buf, void* shadow, float lr,
+             float momentum, float dampening, float wd, int nesterov, int first, float grad_scale,
+             hipStream_t st);
+int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st);
+int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float* partial, hipStream_t st);
+int rtdc_softmax_fwd(const void* S, void* P, float* lse, long long rows, int T, int causal, hipStream_t st);
+int rtdc_softmax_bwd(const void* P, const void* dP, void* dS, long long rows, int T, int causal,
+                     hipStream_t st);
+int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int ntok, int T, int D,
+                   hipStream_t st);
+int rtdc_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int B, int T, int D,
+                   int accumulate_wpe, hipStream_t st);
+int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
+                 unsigned long long offset, int is_bf16, hipStream_t st);
+int rtdc_relu_dropout(const void* h, void* y, const void* dy, void* dx, long long n, float p,
+                      unsigned long long seed, unsigned long long offset, int backward, int is_bf16,
+                      hipStream_t st);
+}
+
+static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+static void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed (rc=", rc, rc == 1 ? ": unsupported shape" : ": launch error", ")");
+}
+
+static void* ptr_or_null(const c10::optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+static void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+}
+
+// ---------------------------------------------------------------------------------- GEMMs
+static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c10::optional<Tensor> bias,
+                      c10::optional<Tensor> aux_in, c10::optional<Tensor> aux_out, int64_t M, int64_t N,
+                      int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool a_kmajor, bool b_kmajor,
+                      int64_t batch, int64_t batch_inner, int64_t sA0, int64_t sA1, int64_t sB0, int64_t sB1,
+                      int64_t sC0, int64_t sC1, double alpha, double beta, int64_t act, int64_t causal) {
+  check_dev(A, "A");
+  check_dev(B, "B");
+  check_dev(C, "C");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "A/B must be bf16");
+  TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "C must be bf16/fp32");
+  TORCH_CHECK(K % 64 == 0 && M % 8 == 0 && N % 8 == 0, "gemm_bf16: need K%64==0, M%8==0, N%8==0");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0, "gemm_bf16: leading dims must be 16-B multiples");
+  rtdc::GemmArgs a{};
+  a.A = (const uint16_t*)A.data_ptr();
+  a.B = (const uint16_t*)B.data_ptr();
+  a.C = C.data_ptr();
+  a.Cin = ptr_or_null(Cin);
+  a.bias = ptr_or_null(bias);
+  a.bias_type = bias.has_value() ? (bias->scalar_type() == at::kFloat ? 2 : 1) : 0;
+  a.aux_in = (const uint16_t*)ptr_or_null(aux_in);
+  a.aux_out = (uint16_t*)ptr_or_null(aux_out);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.lda = (int)lda; a.ldb = (int)ldb; a.ldc = (int)ldc;
+  a.sA0 = sA0; a.sA1 = sA1; a.sB0 = sB0; a.sB1 = sB1; a.sC0 = sC0; a.sC1 = sC1;
+  a.batch_inner = (int)std::max<int64_t>(1, batch_inner);
+  a.alpha = (float)alpha; a.beta = (float)beta;
+  a.act = (int)act; a.causal = (int)causal;
+  TORCH_CHECK(!(act == 2) || a.aux_out, "gelu forward needs aux_out");
+  TORCH_CHECK(!(act == 3 || act == 4) || a.aux_in, "activation backward needs aux_in");
+  check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream()),
+           "gemm_bf16");
+}
+
+static void gemm_f32(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c10::optional<Tensor> bias,
+                     c10::optional<Tensor> aux_in, c10::optional<Tensor> aux_out, int64_t M, int64_t N,
+                     int64_t K, int64_t sam, int64_t sak, int64_t sbk, int64_t sbn, int64_t ldc, double alpha,
+                     double beta, int64_t act) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm_f32 needs GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kFloat && B.scalar_type() == at::kFloat && C.scalar_type() == at::kFloat,
+              "gemm_f32: fp32 only");
+  rtdc::GemmF32Args a{};
+  a.A = A.data_ptr<float>();
+  a.B = B.data_ptr<float>();
+  a.C = C.data_ptr<float>();
+  a.Cin = (const float*)ptr_or_null(Cin);
+  a.bias = (const float*)ptr_or_null(bias);
+  a.aux_in = (const float*)ptr_or_null(aux_in);
+  a.aux_out = (float*)ptr_or_null(aux_out);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.sam = sam; a.sak = sak; a.sbk = sbk; a.sbn = sbn;
+  a.ldc = (int)ldc;
+  a.alpha = (float)alpha; a.beta = (float)beta; a.act = (int)act;
+  check_rc(rtdc_gemm_f32(&a, cur_stream()), "gemm_f32");
+}
+
+// ---------------------------------------------------------------------------------- norms
+static void layernorm_fwd(Tensor x, Tensor g, Tensor b, Tensor y, Tensor mean, Tensor rstd, double eps) {
+  check_dev(x, "x");
+  const int D = (int)x.size(-1), M = (int)(x.numel() / D);
+  check_rc(rtdc_layernorm_fwd(x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
+                              rstd.data_ptr<float>(), M, D, (float)eps, cur_stream()),
+           "layernorm_fwd");
+}
+static void rmsnorm_fwd(Tensor x, Tensor g, Tensor y, Tensor rstd, double eps) {
+  check_dev(x, "x");
+  const int D = (int)x.size(-1), M = (int)(x.numel() / D);
+  check_rc(rtdc_rmsnorm_fwd(x.data_ptr(), g.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), M, D, (float)eps,
+                            cur_stream()),
+           "rmsnorm_fwd");
+}
+static void layernorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
+                          Tensor dx, Tensor ws, Tensor dg, Tensor db, int64_t nwaves, bool accumulate) {
+  const int D = (int)x.size(-1), M = (int)(x.numel() / D);
+  TORCH_CHECK(ws.numel() >= 2 * nwaves * D, "layernorm_bwd workspace too small");
+  check_rc(rtdc_layernorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr<float>(),
+                              rstd.data_ptr<float>(), ptr_or_null(dres), dx.data_ptr(), ws.data_ptr<float>(),
+                              dg.data_ptr<float>(), db.data_ptr<float>(), M, D, (int)nwaves, accumulate,
+                              cur_stream()),
+           "layernorm_bwd");
+}
+static void rmsnorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor rstd, c10::optional<Tensor> dres, Tensor dx,
+                        Tensor ws, Tensor dg, int64_t nwaves, bool accumulate) {
+  const int D = (int)x.size(-1), M = (int)(x.numel() / D);
+  TORCH_CHECK(ws.numel() >= nwaves * D, "rmsnorm_bwd workspace too small");
+  check_rc(rtdc_rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), rstd.data_ptr<float>(), ptr_or_null(dres),
+                            dx.data_ptr(), ws.data_ptr<float>(), dg.data_ptr<float>(), M, D, (int)nwaves,
+                            accumulate, cur_stream()),
+           "rmsnorm_bwd");
+}
+static void colsum(Tensor X, int64_t M, int64_t N, int64_t ld, Tensor ws, int64_t nblk, Tensor out,
+                   bool accumulate) {
+  TORCH_CHECK(ws.numel() >= nblk * N, "colsum workspace too small");
+  check_rc(rtdc_colsum(X.data_ptr(), (int)M, (int)N, (int)ld, ws.data_ptr<float>(), (int)nblk,
+                       out.data_ptr<float>(), accumulate, X.scalar_type() == at::kBFloat16, cur_stream()),
+           "colsum");
+}
+
+// ---------------------------------------------------------------------------------- xent
+static void xent(Tensor logits, c10::optional<Tensor> dlogits, c10::optional<Tensor> target,
+                 c10::optional<Tensor> loss, c10::optional<Tensor> lse, c10::optional<Tensor> argmax, int64_t M,
+                 int64_t V, int64_t ld, double grad_scale, int64_t ignore_index) {
+  TORCH_CHECK(logits.is_cuda(), "xent: GPU tensor expected");
+  check_rc(rtdc_xent(logits.data_ptr(), ptr_or_null(dlogits), (const int64_t*)ptr_or_null(target),
+                     (float*)ptr_or_null(loss), (float*)ptr_or_null(lse), (int64_t*)ptr_or_null(argmax), (int)M,
+                     (int)V, (int)ld, (float)grad_scale, (int)ignore_index,
+                     logits.scalar_type() == at::kBFloat16, cur_stream()),
+           "xent");
+}
+
+// ---------------------------------------------------------------------------------- optim
+static void adamw(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, Tensor m, Tensor v,
+                  c10::optional<Tensor> shadow, double lr, double b1, double b2, double eps, double wd, double bc1,
+                  double bc2_sqrt, double grad_scale) {
+  check_rc(rtdc_adamw(chunks.data_ptr(), (int)nchunks, p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                      v.data_ptr<float>(), ptr_or_null(shadow), (float)lr, (float)b1, (float)b2, (float)eps,
+                      (float)wd, (float)bc1, (float)bc2_sqrt, (float)grad_scale, cur_stream()),
+           "adamw");
+}
+static void sgd(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, c10::optional<Tensor> buf,
+                c10::optional<Tensor> shadow, double lr, double momentum, double dampening, double wd,
+                bool nesterov, bool first, double grad_scale) {
+  check_rc(rtdc_sgd(chunks.data_ptr(), (int)nchunks, p.data_ptr<float>(), g.data_ptr<float>(),
+                    (float*)ptr_or_null(buf), ptr_or_null(shadow), (float)lr, (float)momentum, (float)dampening,
+                    (float)wd, nesterov, first, (float)grad_scale, cur_stream()),
+           "sgd");
+}
+static void f32_to_bf16(Tensor x, Tensor y) {
+  check_rc(rtdc_f32_to_bf16(x.data_ptr<float>(), y.data_ptr(), (long long)x.numel(), cur_stream()), "f32_to_bf16");
+}
+static void sumsq(Tensor chunks, int64_t nchunks, Tensor g, Tensor partial) {
+  check_rc(rtdc_sumsq(chunks.data_ptr(), (int)nchunks, g.data_ptr<float>(), partial.data_ptr<float>(), cur_stream()),
+           "sumsq");
+}
+
+// ---------------------------------------------------------------------------------- attention softmax
+static void softmax_fwd(Tensor S, Tensor P, c10::optional<Tensor> lse, int64_t rows, int64_t T, bool causal) {
+  check_rc(rtdc_softmax_fwd(S.data_ptr(), P.data_ptr(), (float*)ptr_or_null(lse), rows, (int)T, causal, cur_stream()),
+           "softmax_fwd");
+}
+static void softmax_bwd(Tensor P, Tensor dP, Tensor dS, int64_t rows, int64_t T, bool causal) {
+  check_rc(rtdc_softmax_bwd(P.data_ptr(), dP.data_ptr(), dS.data_ptr(), rows, (int)T, causal, cur_stream()),
+           "softmax_bwd");
+}
+
+// ---------------------------------------------------------------------------------- embedding / dropout
+static void embed_fwd(Tensor idx, Tensor wte, c10::optional<Tensor> wpe, Tensor out, int64_t T) {
+  const int D = (int)wte.size(1);
+  check_rc(rtdc_embed_fwd(idx.data_ptr<int64_t>(), wte.data_ptr(), ptr_or_null(wpe), out.data_ptr(),
+                          (int)idx.numel(), (int)T, D, cur_stream()),
+           "embed_fwd");
+}
+static void embed_bwd(Tensor idx, Tensor dout, Tensor dwte, c10::optional<Tensor> dwpe, int64_t B, int64_t T,
+                      bool accumulate_wpe) {
+  const int D = (int)dwte.size(1);
+  check_rc(rtdc_embed_bwd(idx.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
+                          (float*)ptr_or_null(dwpe), (int)B, (int)T, D, accumulate_wpe, cur_stream()),
+           "embed_bwd");
+}
+static void dropout(Tensor x, Tensor y, double p, uint64_t seed, uint64_t offset) {
+  check_rc(rtdc_dropout(x.data_ptr(), y.data_ptr(), (long long)x.numel(), (float)p, seed, offset,
+                        x.scalar_type() == at::kBFloat16, cur_stream()),
+           "dropout");
+}
+static void relu_dropout(Tensor h, c10::optional<Tensor> y, c10::optional<Tensor> dy, c10::optional<Tensor> dx,
+                         double p, uint64_t seed, uint64_t offset, bool backward) {
+  check_rc(rtdc_relu_dropout(h.data_ptr(), ptr_or_null(y), ptr_or_null(dy), ptr_or_null(dx), (long long)h.numel(),
+                             (float)p, seed, offset, backward, h.scalar_type() == at::kBFloat16, cur_stream()),
+           "relu_dropout");
+}
+
+// ---------------------------------------------------------------------------------- checkpoint engine
+using rtdc_ckpt::Engine;
+using rtdc_ckpt::FileJob;
+using rtdc_ckpt::Record;
+
+// record tuple: (name, data: bytes|None, ptr: int, nbytes: int, on_device: bool)
+static std::vector<Record> to_records(const py::list& recs) {
+  std::vector<Record> out;
+  for (auto item : recs) {
+    auto t = item.cast<py::tuple>();
+    Record r;
+    r.name = t[0].cast<std::string>();
+    if (!t[1].is_none()) {
+      r.inline_data = t[1].cast<std::string>();
+    } else {
+      r.src = reinterpret_cast<const char*>(t[2].cast<uintptr_t>());
+      r.nbytes = t[3].cast<uint64_t>();
+      r.on_device = t[4].cast<bool>();
+    }
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+
+static py::tuple plan_layout(const py::list& recs) {
+  auto r = to_records(recs);
+  uint64_t total = 0;
+  auto lay = rtdc_ckpt::plan_layout(r, &total);
+  return py::make_tuple(lay, total);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) kernels and native checkpoint engine";
+  m.def("gemm_bf16", &gemm_bf16);
+  m.def("gemm_f32", &gemm_f32);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("colsum", &colsum);
+  m.def("xent", &xent);
+  m.def("adamw", &adamw);
+  m.def("sgd", &sgd);
+  m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("sumsq", &sumsq);
+  m.def("softmax_fwd", &softmax_fwd);
+  m.def("softmax_bwd", &softmax_bwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("dropout", &dropout);
+  m.def("relu_dropout", &relu_dropout);
+
+  m.def("have_gpu", &rtdc_ckpt::g_have_gpu);
+  m.def("plan_layout", &plan_layout, "zip layout: ([(data_offset, size)], total_bytes)");
+  m.def("crc32", [](py::bytes b) {
+    std::string s = b;
+    return (uint32_t)crc32(0L, (const Bytef*)s.data(), (uInt)s.size());
+  });
+  m.def(
+      "read_ranges",
+      [](const std::string& path, std::vector<uint64_t> offs, std::vector<uint64_t> lens, std::vector<uintptr_t> dsts,
+         int nthreads) {
+        py::gil_scoped_release nogil;
+        rtdc_ckpt::read_ranges(path, offs, lens, dsts, nthreads);
+      },
+      "parallel pread of (offset, len) ranges into raw destination pointers");
+
+  py::class_<Engine>(m, "CkptEngine")
+      .def(py::init<size_t, size_t, int, int>(), py::arg("nslots"), py::arg("slot_bytes"), py::arg("nwriters"),
+           py::arg("device"))
+      .def(
+          "submit",
+          [](Engine& e, const py::list& files, uintptr_t ready_event) {
+            std::vector<std::shared_ptr<FileJob>> fj;
+            for (auto item : files) {
+              auto t = item.cast<py::tuple>();
+              auto f = std::make_shared<FileJob>();
+              f->path = t[0].cast<std::string>();
+              f->fsync_on = t[1].cast<bool>();
+              f->crc_on = t[2].cast<bool>();
+              f->recs = to_records(t[3].cast<py::list>());
+              fj.push_back(f);
+            }
+            return e.submit(std::move(fj), reinterpret_cast<hipEvent_t>(ready_event));
+          },
+          py::arg("files"), py::arg("ready_event") = 0)
+      .def("poll", &Engine::poll)
+      .def(
+          "wait",
+          [](Engine& e, int id) {
+            py::gil_scoped_release nogil;
+            return e.wait(id);
+          })
+      .def_property_readonly("slot_bytes", &Engine::slot_bytes)
+      .def_property_readonly("pinned", &Engine::pinned);
+}

@@ -1,0 +1,42 @@
+// Launch-argument structs shared by the HIP kernels and the host bindings.
+#pragma once
+#include <stdint.h>
+
+namespace rtdc {
+
+// bf16 MFMA GEMM (gemm_bf16.hip)
+struct GemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const void* Cin;        // added as beta*Cin (same dtype as C); may alias C
+  const void* bias;       // [N], bf16 or fp32
+  const uint16_t* aux_in; // act-backward input (pre-activation), ld = ldc
+  uint16_t* aux_out;      // act-forward pre-activation output, ld = ldc
+  int M, N, K;
+  int lda, ldb, ldc;
+  long long sA0, sA1, sB0, sB1, sC0, sC1;
+  int batch_inner;
+  float alpha, beta;
+  int act;        // 0 none, 1 relu, 2 gelu_tanh, 3 *gelu'(aux_in), 4 *relu'(aux_in)
+  int causal;     // 0 none, 1 skip tiles with n0 > m_last, 2 k < m0+BM, 3 k >= m0
+  int bias_type;  // 0 none, 1 bf16, 2 fp32
+};
+
+// fp32 MFMA GEMM (gemm_f32.hip)
+struct GemmF32Args {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* Cin;
+  const float* bias;
+  const float* aux_in;
+  float* aux_out;
+  int M, N, K;
+  long long sam, sak, sbk, sbn;  // A(m,k) = A[m*sam + k*sak]; B(k,n) = B[k*sbk + n*sbn]
+  int ldc;
+  float alpha, beta;
+  int act;  // 0 none, 1 relu (aux_out gets pre-activation if set), 4 relu-backward via aux_in
+};
+
+}  // namespace rtdc

@@ -1,0 +1,278 @@
+// LayerNorm / RMSNorm forward + backward for bf16 activations (gfx950).
+//
+// One wave64 per row; each lane owns CPL 16-B chunks (8 bf16) of the row, so the row lives in
+// registers between the statistics pass and the normalisation pass (one HBM read, one write).
+// Backward fuses the residual-gradient add (dx = dres + LN'(dy)) and writes per-wave partial
+// dgamma/dbeta rows to a workspace that a second kernel reduces in a fixed order, so the
+// parameter gradients are bitwise reproducible (no float atomics, MI355X_MICROARCH.md §Global
+// float atomics).
+#include "common.h"
+
+namespace rtdc {
+
+__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
+  uint4 x = *(const uint4*)p;
+  uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float* v) {
+  uint4 x = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]),
+                       pack_bf2(v[6], v[7]));
+  *(uint4*)p = x;
+}
+
+template <int CPL, bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ g,
+                                                      const bf16_t* __restrict__ b,
+                                                      bf16_t* __restrict__ y, float* __restrict__ mean_out,
+                                                      float* __restrict__ rstd_out, int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = D >> 3;
+  const bf16_t* xr = x + (long long)row * D;
+  float v[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      ld8(xr + c * 8, v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[i][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float d = v[i][e] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+  bf16_t* yr = y + (long long)row * D;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float gg[8], bb[8], o[8];
+      ld8(g + c * 8, gg);
+      if (!RMS) ld8(b + c * 8, bb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * gg[e] + (RMS ? 0.f : bb[e]);
+      st8(yr + c * 8, o);
+    }
+  }
+}
+
+// dxhat = dy*g ; dx = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat*xhat))   (LayerNorm)
+// dx = rstd * (dxhat - xhat * mean(dxhat*xhat))                                  (RMSNorm)
+template <int CPL, bool RMS>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ ws_dg,
+    float* __restrict__ ws_db, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int nch = D >> 3;
+  float adg[CPL][8], adb[CPL][8];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) adg[i][e] = adb[i][e] = 0.f;
+
+  float gg[CPL][8];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) ld8(g + c * 8, gg[i]);
+  }
+
+  for (int row = gw; row < M; row += nw) {
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    const bf16_t* xr = x + (long long)row * D;
+    const bf16_t* dyr = dy + (long long)row * D;
+    float xh[CPL][8], dxh[CPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float xv[8], dv[8];
+        ld8(xr + c * 8, xv);
+        ld8(dyr + c * 8, dv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[i][e] = (xv[e] - mean) * rstd;
+          dxh[i][e] = dv[e] * gg[i][e];
+          s1 += dxh[i][e];
+          s2 += dxh[i][e] * xh[i][e];
+          adg[i][e] += dv[e] * xh[i][e];
+          adb[i][e] += dv[e];
+        }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / D;
+    const float m2 = wave_sum(s2) / D;
+    bf16_t* dxr = dx + (long long)row * D;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[8], r[8];
+        if (dres) ld8(dres + (long long)row * D + c * 8, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = rstd * (dxh[i][e] - m1 - xh[i][e] * m2);
+          if (dres) o[e] += r[e];
+        }
+        st8(dxr + c * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float* pg = ws_dg + (long long)gw * D + c * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pg[e] = adg[i][e];
+      if (!RMS) {
+        float* pb = ws_db + (long long)gw * D + c * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pb[e] = adb[i][e];
+      }
+    }
+  }
+}
+
+// out[d] (+)= sum_w ws[w][d], fixed summation order.
+__global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                       int W, int D, int accumulate) {
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.f;
+  for (int w = 0; w < W; ++w) s += ws[(long long)w * D + d];
+  out[d] = accumulate ? out[d] + s : s;
+}
+
+// Column sums of a bf16 matrix [M][N] (bias gradient): stage 1 per-block partials over a row
+// range, stage 2 = colsum_ws_kernel.  Thread t of block owns columns (blockIdx.y*256+t).
+__device__ __forceinline__ float as_f(bf16_t v) { return bf2f(v); }
+__device__ __forceinline__ float as_f(float v) { return v; }
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ X, int M, int N,
+                                                            int ld, int rows_per_block,
+                                                            float* __restrict__ ws) {
+  const int n = blockIdx.y * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += as_f(X[(long long)r * ld + n]);
+  ws[(long long)blockIdx.x * N + n] = s;
+}
+
+}  // namespace rtdc
+
+using namespace rtdc;
+
+template <bool RMS>
+static int launch_norm_fwd(const void* x, const void* g, const void* b, void* y, float* mean,
+                           float* rstd, int M, int D, float eps, hipStream_t st) {
+  if (D % 8 != 0) return 1;
+  const int cpl = (D / 8 + 63) / 64;
+  dim3 grid((M + 3) / 4), block(256);
+#define L(C)                                                                                  \
+  hipLaunchKernelGGL((norm_fwd_kernel<C, RMS>), grid, block, 0, st, (const bf16_t*)x,         \
+                     (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, mean, rstd, M, D, eps)
+  if (cpl <= 1) L(1);
+  else if (cpl <= 2) L(2);
+  else if (cpl <= 4) L(4);
+  else if (cpl <= 8) L(8);
+  else if (cpl <= 16) L(16);
+  else return 1;
+#undef L
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+template <bool RMS>
+static int launch_norm_bwd(const void* dy, const void* x, const void* g, const float* mean,
+                           const float* rstd, const void* dres, void* dx, float* ws, float* dg,
+                           float* db, int M, int D, int nwaves, int accumulate, hipStream_t st) {
+  if (D % 8 != 0 || nwaves % 4 != 0) return 1;
+  const int cpl = (D / 8 + 63) / 64;
+  dim3 grid(nwaves / 4), block(256);
+  float* ws_dg = ws;
+  float* ws_db = ws + (long long)nwaves * D;
+#define L(C)                                                                                  \
+  hipLaunchKernelGGL((norm_bwd_kernel<C, RMS>), grid, block, 0, st, (const bf16_t*)dy,        \
+                     (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \
+                     (bf16_t*)dx, ws_dg, ws_db, M, D)
+  if (cpl <= 1) L(1);
+  else if (cpl <= 2) L(2);
+  else if (cpl <= 4) L(4);
+  else if (cpl <= 8) L(8);
+  else return 1;
+#undef L
+  dim3 g2((D + 255) / 256);
+  hipLaunchKernelGGL(colsum_ws_kernel, g2, block, 0, st, ws_dg, dg, nwaves, D, accumulate);
+  if (!RMS) hipLaunchKernelGGL(colsum_ws_kernel, g2, block, 0, st, ws_db, db, nwaves, D, accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_layernorm_fwd(const void* x, const void* g, const void* b, void* y, float* mean,
+                                  float* rstd, int M, int D, float eps, hipStream_t st) {
+  return launch_norm_fwd<false>(x, g, b, y, mean, rstd, M, D, eps, st);
+}
+extern "C" int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rstd, int M, int D,
+                                float eps, hipStream_t st) {
+  return launch_norm_fwd<true>(x, g, nullptr, y, nullptr, rstd, M, D, eps, st);
+}
+extern "C" int rtdc_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean,
+                                  const float* rstd, const void* dres, void* dx, float* ws,
+                                  float* dg, float* db, int M, int D, int nwaves, int accumulate,
+                                  hipStream_t st) {
+  return launch_norm_bwd<false>(dy, x, g, mean, rstd, dres, dx, ws, dg, db, M, D, nwaves,
+                                accumulate, st);
+}
+extern "C" int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, const float* rstd,
+                                const void* dres, void* dx, float* ws, float* dg, int M, int D,
+                                int nwaves, int accumulate, hipStream_t st) {
+  return launch_norm_bwd<true>(dy, x, g, nullptr, rstd, dres, dx, ws, dg, nullptr, M, D, nwaves,
+                               accumulate, st);
+}
+extern "C" int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out,
+                           int accumulate, int is_bf16, hipStream_t st) {
+  const int rpb = (M + nblk - 1) / nblk;
+  dim3 grid(nblk, (N + 255) / 256), block(256);
+  if (is_bf16)
+    hipLaunchKernelGGL((colsum_partial_kernel<bf16_t>), grid, block, 0, st, (const bf16_t*)X, M, N, ld, rpb, ws);
+  else
+    hipLaunchKernelGGL((colsum_partial_kernel<float>), grid, block, 0, st, (const float*)X, M, N, ld, rpb, ws);
+  hipLaunchKernelGGL(colsum_ws_kernel, dim3((N + 255) / 256), block, 0, st, (const float*)ws, out, nblk, N,
+                     accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -1,0 +1,162 @@
+// Fused optimizers over FLAT parameter/state buffers (gfx950).
+//
+// The framework keeps every parameter, gradient and optimizer state of a model in one
+// contiguous buffer per kind (FlatParamSpace), so an optimizer step is ONE launch over a
+// chunk table instead of ATen's multi-tensor-apply foreach chain (reference: SGD(momentum=0.9)
+// at R/my_ray_module.py:142,160 -> torch/optim/sgd.py _multi_tensor_sgd).  A chunk is a slice
+// of one parameter (never crossing parameters) carrying that parameter's weight-decay flag;
+// segments are 64-element aligned so every lane moves 16 B per load.
+//
+// AdamW: fp32 master + m + v, optional bf16 shadow written in the same pass (the copy the
+// bf16 MFMA kernels read).  grad_scale folds the DDP 1/world pre-divide into the step.
+// Semantics follow torch.optim.AdamW / SGD (decoupled weight decay; SGD first-step clone).
+#include "common.h"
+
+namespace rtdc {
+
+struct Chunk {
+  long long start;
+  int len;
+  int decay;
+};
+
+__global__ __launch_bounds__(256) void adamw_kernel(const Chunk* __restrict__ chunks, int nchunks,
+                                                   float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16_t* __restrict__ shadow, float lr, float b1,
+                                                   float b2, float eps, float wd, float bc1,
+                                                   float bc2_sqrt, float grad_scale) {
+  const float step_size = lr / bc1;
+  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    const Chunk c = chunks[ci];
+    const float decay = c.decay ? (1.f - lr * wd) : 1.f;
+    for (int i = threadIdx.x * 4; i < c.len; i += 256 * 4) {
+      const long long o = c.start + i;
+      if (i + 4 <= c.len) {
+        f32x4 pp = *(f32x4*)(p + o), gg = *(const f32x4*)(g + o);
+        f32x4 mm = *(f32x4*)(m + o), vv = *(f32x4*)(v + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gr = gg[e] * grad_scale;
+          float pe = pp[e] * decay;
+          mm[e] = b1 * mm[e] + (1.f - b1) * gr;
+          vv[e] = b2 * vv[e] + (1.f - b2) * gr * gr;
+          const float denom = sqrtf(vv[e]) / bc2_sqrt + eps;
+          pe -= step_size * mm[e] / denom;
+          pp[e] = pe;
+        }
+        *(f32x4*)(p + o) = pp;
+        *(f32x4*)(m + o) = mm;
+        *(f32x4*)(v + o) = vv;
+        if (shadow) *(uint2*)(shadow + o) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+      } else {
+        for (int e = 0; e < 4 && i + e < c.len; ++e) {
+          const long long oe = o + e;
+          const float gr = g[oe] * grad_scale;
+          float pe = p[oe] * decay;
+          m[oe] = b1 * m[oe] + (1.f - b1) * gr;
+          v[oe] = b2 * v[oe] + (1.f - b2) * gr * gr;
+          const float denom = sqrtf(v[oe]) / bc2_sqrt + eps;
+          pe -= step_size * m[oe] / denom;
+          p[oe] = pe;
+          if (shadow) shadow[oe] = f2bf(pe);
+        }
+      }
+    }
+  }
+}
+
+// torch SGD: d = g*s + wd*p ; buf = first ? d : mom*buf + (1-damp)*d ; d = nesterov ? d + mom*buf : buf
+// p -= lr*d
+__global__ __launch_bounds__(256) void sgd_kernel(const Chunk* __restrict__ chunks, int nchunks,
+                                                 float* __restrict__ p, const float* __restrict__ g,
+                                                 float* __restrict__ buf, bf16_t* __restrict__ shadow,
+                                                 float lr, float momentum, float dampening, float wd,
+                                                 int nesterov, int first, float grad_scale) {
+  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    const Chunk c = chunks[ci];
+    const float w = c.decay ? wd : 0.f;
+    for (int i = threadIdx.x; i < c.len; i += 256) {
+      const long long o = c.start + i;
+      float d = g[o] * grad_scale;
+      float pe = p[o];
+      d += w * pe;
+      if (momentum != 0.f) {
+        float b = first ? d : momentum * buf[o] + (1.f - dampening) * d;
+        buf[o] = b;
+        d = nesterov ? d + momentum * b : b;
+      }
+      pe -= lr * d;
+      p[o] = pe;
+      if (shadow) shadow[o] = f2bf(pe);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                         long long n) {
+  for (long long i = (blockIdx.x * 256LL + threadIdx.x) * 4; i < n; i += gridDim.x * 256LL * 4) {
+    if (i + 4 <= n) {
+      f32x4 v = *(const f32x4*)(x + i);
+      *(uint2*)(y + i) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    } else {
+      for (long long e = i; e < n; ++e) y[e] = f2bf(x[e]);
+    }
+  }
+}
+
+// sum of squares per chunk -> partial[ci] (for grad-norm clipping); deterministic
+__global__ __launch_bounds__(256) void sumsq_kernel(const Chunk* __restrict__ chunks, int nchunks,
+                                                   const float* __restrict__ g, float* __restrict__ partial) {
+  __shared__ float red[4];
+  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    const Chunk c = chunks[ci];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < c.len; i += 256) {
+      const float x = g[c.start + i];
+      s += x * x;
+    }
+    s = block_sum<256>(s, red);
+    if (threadIdx.x == 0) partial[ci] = s;
+  }
+}
+
+}  // namespace rtdc
+
+using namespace rtdc;
+
+static inline int grid_for(int nchunks) { return nchunks < 4096 ? nchunks : 4096; }
+
+extern "C" int rtdc_adamw(const void* chunks, int nchunks, float* p, const float* g, float* m,
+                          float* v, void* shadow, float lr, float b1, float b2, float eps, float wd,
+                          float bc1, float bc2_sqrt, float grad_scale, hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
+                     nchunks, p, g, m, v, (bf16_t*)shadow, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_sgd(const void* chunks, int nchunks, float* p, const float* g, float* buf,
+                        void* shadow, float lr, float momentum, float dampening, float wd,
+                        int nesterov, int first, float grad_scale, hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
+                     nchunks, p, g, buf, (bf16_t*)shadow, lr, momentum, dampening, wd, nesterov, first,
+                     grad_scale);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st) {
+  long long blocks = (n / 4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, (bf16_t*)y, n);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float* partial, hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
+                     nchunks, g, partial);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -1,0 +1,43 @@
+"""Token + position embedding (gather) and its backward (fp32 scatter-add) on native kernels."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import gpu_ext
+from .shadow import shadow_of
+
+
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe):
+        B, T = idx.shape
+        D = wte.shape[1]
+        idx_c = idx.contiguous()
+        out = torch.empty((B, T, D), dtype=torch.bfloat16, device=idx.device)
+        gpu_ext().embed_fwd(idx_c, shadow_of(wte), shadow_of(wpe) if wpe is not None else None, out, T)
+        ctx.save_for_backward(idx_c)
+        ctx.shapes = (wte.shape, None if wpe is None else wpe.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx,) = ctx.saved_tensors
+        B, T = idx.shape
+        wte_shape, wpe_shape = ctx.shapes
+        dwte = torch.zeros(wte_shape, dtype=torch.float32, device=idx.device)
+        dwpe = None
+        if wpe_shape is not None:
+            dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device)
+        gpu_ext().embed_bwd(idx, dout.contiguous(), dwte, dwpe, B, T, False)
+        return None, dwte, dwpe
+
+
+def embedding(idx: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor | None = None,
+              dtype=torch.bfloat16) -> torch.Tensor:
+    if not idx.is_cuda:
+        x = F.embedding(idx, wte)
+        if wpe is not None:
+            x = x + wpe[: idx.shape[1]].unsqueeze(0)
+        return x
+    return _Embedding.apply(idx, wte, wpe)

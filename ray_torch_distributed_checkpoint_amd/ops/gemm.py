@@ -1,0 +1,86 @@
+"""GEMM entry points over the hand-written gfx950 MFMA kernels.
+
+`gemm_bf16` is the raw launcher (layouts, batch strides, causal modes, fused epilogues);
+`linear_fwd / linear_dgrad / linear_wgrad` are the three nn.Linear products expressed on it
+(see csrc/kernels/gemm_bf16.hip for the operand-layout table).  `gemm_f32` is the exact-f32
+MFMA path used by fp32 models (the reference toy MLP, R/my_ray_module.py:94-112).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import gpu_ext
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
+CAUSAL_NONE, CAUSAL_SKIP_UPPER, CAUSAL_K_UPTO_M, CAUSAL_K_FROM_M = 0, 1, 2, 3
+
+_COLSUM_BLOCKS = 128
+_ws_cache: dict = {}
+
+
+def workspace(device, numel: int, tag: str = "ws") -> torch.Tensor:
+    """Per-device reusable fp32 scratch buffer (grown on demand, never shrunk)."""
+    key = (str(device), tag)
+    t = _ws_cache.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
+        _ws_cache[key] = t
+    return t
+
+
+def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, Cin=None, bias=None,
+              aux_in=None, aux_out=None, alpha=1.0, beta=0.0, act=ACT_NONE, causal=CAUSAL_NONE,
+              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0)):
+    sA0, sA1, sB0, sB1, sC0, sC1 = strides
+    gpu_ext().gemm_bf16(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
+                        batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act, causal)
+    return C
+
+
+def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None, aux_out=None,
+               out_dtype=torch.bfloat16):
+    """y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual)."""
+    M, K = x2d.shape
+    N = w.shape[0]
+    y = torch.empty((M, N), dtype=out_dtype, device=x2d.device)
+    gemm_bf16(x2d, w, y, M, N, K, K, K, N, True, True, Cin=residual, bias=bias, aux_out=aux_out,
+              beta=1.0 if residual is not None else 0.0, act=act)
+    return y
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0):
+    """dx[M,K] = dy[M,N] @ w[N,K]  (optionally * act'(aux_in))."""
+    M, N = dy.shape
+    K = w.shape[1]
+    dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
+    gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha)
+    return dx
+
+
+def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0):
+    """dw[N,K] (fp32) = dy[M,N]^T @ x[M,K]."""
+    M, N = dy.shape
+    K = x2d.shape[1]
+    if out is None:
+        out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    gemm_bf16(dy, x2d, out, N, K, M, N, K, K, False, False, Cin=out if accumulate else None,
+              beta=1.0 if accumulate else 0.0, alpha=alpha)
+    return out
+
+
+def colsum(x2d: torch.Tensor, out=None, accumulate=False):
+    """fp32 column sums of a [M,N] matrix (bias gradient), deterministic two-stage reduce."""
+    M, N = x2d.shape
+    if out is None:
+        out = torch.empty((N,), dtype=torch.float32, device=x2d.device)
+    nblk = min(_COLSUM_BLOCKS, max(1, M // 16))
+    ws = workspace(x2d.device, nblk * N, "colsum")
+    gpu_ext().colsum(x2d, M, N, x2d.stride(0), ws, nblk, out, accumulate)
+    return out
+
+
+def gemm_f32(A, B, C, M, N, K, sam, sak, sbk, sbn, ldc, *, Cin=None, bias=None, aux_in=None, aux_out=None,
+             alpha=1.0, beta=0.0, act=ACT_NONE):
+    gpu_ext().gemm_f32(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, sam, sak, sbk, sbn, ldc, float(alpha),
+                       float(beta), act)
+    return C

@@ -1,0 +1,156 @@
+"""Linear layers on the native MFMA GEMMs, with fused epilogues.
+
+* `linear(x, w, b, act, residual)` - bf16 activations (fp32 master params, bf16 shadows):
+  forward = one GEMM with bias/ReLU/residual fused in the epilogue; backward = dgrad + wgrad
+  GEMMs (fp32 weight gradient) + a deterministic bias-gradient column reduce.
+* `fused_mlp(x, w_fc, b_fc, w_proj, b_proj, residual)` - the transformer MLP: the c_fc GEMM
+  writes both the GELU output and its pre-activation, and in backward the c_proj dgrad GEMM
+  applies GELU' in its epilogue (no separate GELU kernels in either direction).
+* fp32 activations take the exact-f32 MFMA path (`gemm_f32`): the reference toy MLP.
+
+On CPU every op is its PyTorch reference implementation (same math, autograd by torch).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import gemm as G
+from ._ext import gpu_ext
+from .shadow import shadow_of
+
+
+def _relu_mask_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """dx = dy * (y > 0) on the native elementwise kernel."""
+    dx = torch.empty_like(dy)
+    gpu_ext().relu_dropout(y, None, dy, dx, 0.0, 0, 0, True)
+    return dx
+
+
+class _LinearBF16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, residual, relu: bool):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        ws = shadow_of(w)
+        res2 = residual.reshape(-1, w.shape[0]) if residual is not None else None
+        y = G.linear_fwd(x2, ws, bias=b, act=G.ACT_RELU if relu else G.ACT_NONE, residual=res2)
+        ctx.save_for_backward(x2, ws, y if relu else None)
+        ctx.relu = relu
+        ctx.has_b = b is not None
+        ctx.has_res = residual is not None
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, ws, y = ctx.saved_tensors
+        N = ws.shape[0]
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dpre = _relu_mask_bwd(dy2, y) if ctx.relu else dy2
+        dx = G.linear_dgrad(dpre, ws).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dw = G.linear_wgrad(dpre, x2) if ctx.needs_input_grad[1] else None
+        db = G.colsum(dpre) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dres = dy if ctx.has_res else None
+        return dx, dw, db, dres, None
+
+
+class _LinearF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu: bool):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K).contiguous()
+        M, N = x2.shape[0], w.shape[0]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        G.gemm_f32(x2, w, y, M, N, K, K, 1, 1, K, N, bias=b, act=G.ACT_RELU if relu else G.ACT_NONE)
+        ctx.save_for_backward(x2, w, y if relu else None)
+        ctx.relu = relu
+        ctx.has_b = b is not None
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        N, K = w.shape
+        M = x2.shape[0]
+        dy2 = dy.reshape(-1, N).contiguous()
+        dpre = _relu_mask_bwd(dy2, y) if ctx.relu else dy2
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
+            G.gemm_f32(dpre, w, dx, M, K, N, N, 1, K, 1, K)
+            dx = dx.view(ctx.in_shape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+            G.gemm_f32(dpre, x2, dw, N, K, M, 1, N, K, 1, K)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = G.colsum(dpre)
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, relu: bool = False,
+           residual: torch.Tensor | None = None) -> torch.Tensor:
+    if not x.is_cuda:
+        y = F.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
+        if relu:
+            y = torch.relu(y)
+        if residual is not None:
+            y = y + residual
+        return y
+    if x.dtype == torch.float32:
+        if residual is not None:
+            return _LinearF32.apply(x, w, b, relu) + residual
+        return _LinearF32.apply(x, w, b, relu)
+    return _LinearBF16.apply(x, w, b, residual, relu)
+
+
+class _FusedMLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w_fc, b_fc, w_proj, b_proj, residual):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M = x2.shape[0]
+        H = w_fc.shape[0]
+        wfs, wps = shadow_of(w_fc), shadow_of(w_proj)
+        pre = torch.empty((M, H), dtype=torch.bfloat16, device=x.device)
+        g = G.linear_fwd(x2, wfs, bias=b_fc, act=G.ACT_GELU, aux_out=pre)
+        res2 = residual.reshape(-1, C) if residual is not None else None
+        y = G.linear_fwd(g, wps, bias=b_proj, residual=res2)
+        ctx.save_for_backward(x2, wfs, wps, pre, g)
+        ctx.has_res = residual is not None
+        ctx.in_shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wfs, wps, pre, g = ctx.saved_tensors
+        C = x2.shape[1]
+        dy2 = dy.reshape(-1, C)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dw_proj = G.linear_wgrad(dy2, g)
+        db_proj = G.colsum(dy2)
+        dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_GELU_BWD, aux_in=pre)
+        dw_fc = G.linear_wgrad(dpre, x2)
+        db_fc = G.colsum(dpre)
+        dx = G.linear_dgrad(dpre, wfs).view(ctx.in_shape)
+        return dx, dw_fc, db_fc, dw_proj, db_proj, (dy if ctx.has_res else None)
+
+
+def gelu_tanh_ref(x):
+    return F.gelu(x, approximate="tanh")
+
+
+def fused_mlp(x, w_fc, b_fc, w_proj, b_proj, residual=None):
+    if not x.is_cuda:
+        h = gelu_tanh_ref(F.linear(x, w_fc.to(x.dtype), b_fc.to(x.dtype)))
+        y = F.linear(h, w_proj.to(x.dtype), b_proj.to(x.dtype))
+        return y + residual if residual is not None else y
+    return _FusedMLP.apply(x, w_fc, b_fc, w_proj, b_proj, residual)

@@ -1,0 +1,2 @@
+from .flat import FlatParamSpace, space_of  # noqa: F401
+from .fused import FusedAdamW, FusedSGD  # noqa: F401

@@ -1,0 +1,139 @@
+"""FlatParamSpace: one contiguous buffer per kind (params, grads, bf16 shadows, optimizer state).
+
+The MI355X-first memory layout for data-parallel training: every parameter of a model is a
+view into one flat fp32 buffer, every gradient a view into one flat fp32 buffer (the DDP
+buckets are contiguous slices of it, so gradients are all-reduced in place - torch's
+`gradient_as_bucket_view` without the copy-in/copy-out of reducer.hpp:329,499), and the
+fused optimizers update the whole model in one launch over a chunk table.  Checkpoint
+snapshots are a handful of large device-to-device copies instead of one copy per tensor.
+
+Segments are 64-element aligned (16-B vector access for fp32/bf16) and laid out in the
+order given (the DDP wrapper passes reverse registration order = approximate backward order).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from ..ops.shadow import bind_shadow
+
+ALIGN = 64
+CHUNK = 16384  # elements per optimizer work item
+
+
+@dataclass
+class Segment:
+    index: int
+    offset: int
+    numel: int
+    shape: tuple
+
+
+class FlatParamSpace:
+    def __init__(self, params, device=None, shadow_dtype=torch.bfloat16, grads=True):
+        params = list(params)
+        assert params, "no parameters"
+        seen = set()
+        uniq = []
+        for p in params:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        self.params = uniq
+        self.device = torch.device(device) if device is not None else uniq[0].device
+        self.segments: list[Segment] = []
+        off = 0
+        for i, p in enumerate(uniq):
+            assert p.dtype == torch.float32, "FlatParamSpace holds fp32 master parameters"
+            self.segments.append(Segment(i, off, p.numel(), tuple(p.shape)))
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=self.device)
+        with torch.no_grad():
+            for p, s in zip(uniq, self.segments):
+                self.data[s.offset:s.offset + s.numel].copy_(p.detach().reshape(-1))
+                p.data = self.view(self.data, s)
+                p._rtdc_space = self
+        self.grad = None
+        if grads:
+            self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
+            for p, s in zip(uniq, self.segments):
+                p.grad = self.view(self.grad, s)
+        self.shadow = None
+        if shadow_dtype is not None and self.device.type == "cuda":
+            self.shadow = torch.empty(off, dtype=shadow_dtype, device=self.device)
+            self.refresh_shadows()
+        self.grad_scale = 1.0
+        self._chunk_cache: dict = {}
+
+    @staticmethod
+    def view(buf: torch.Tensor, s: Segment) -> torch.Tensor:
+        return buf[s.offset:s.offset + s.numel].view(s.shape)
+
+    def segment_of(self, p) -> Segment:
+        for q, s in zip(self.params, self.segments):
+            if q is p:
+                return s
+        raise KeyError("parameter not in this space")
+
+    def refresh_shadows(self):
+        if self.shadow is None:
+            return
+        from ..ops._ext import gpu_ext
+
+        gpu_ext().f32_to_bf16(self.data, self.shadow)
+        for p, s in zip(self.params, self.segments):
+            bind_shadow(p, self.view(self.shadow, s))
+
+    def zero_grad(self):
+        if self.grad is not None:
+            self.grad.zero_()
+            for p, s in zip(self.params, self.segments):
+                v = self.view(self.grad, s)
+                if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                    p.grad = v
+
+    def ensure_grad_views(self):
+        """Re-attach grads that were replaced (e.g. zero_grad(set_to_none=True))."""
+        if self.grad is None:
+            return
+        for p, s in zip(self.params, self.segments):
+            v = self.view(self.grad, s)
+            g = p.grad
+            if g is None:
+                v.zero_()
+                p.grad = v
+            elif g.data_ptr() != v.data_ptr():
+                v.copy_(g)
+                p.grad = v
+
+    def chunk_table(self, params_subset, decay_flags) -> tuple[torch.Tensor, int]:
+        """int64 [nchunks, 2] rows of (start, len | decay<<32) for the native optimizer kernels."""
+        key = (tuple(id(p) for p in params_subset), tuple(decay_flags))
+        hit = self._chunk_cache.get(key)
+        if hit is not None:
+            return hit
+        rows = []
+        for p, d in zip(params_subset, decay_flags):
+            s = self.segment_of(p)
+            for st in range(0, s.numel, CHUNK):
+                ln = min(CHUNK, s.numel - st)
+                rows.append((s.offset + st, ln | (int(bool(d)) << 32)))
+        t = torch.tensor(rows if rows else [(0, 0)], dtype=torch.int64).to(self.device)
+        out = (t, len(rows))
+        self._chunk_cache[key] = out
+        return out
+
+
+def space_of(params) -> FlatParamSpace | None:
+    sp = None
+    for p in params:
+        s = getattr(p, "_rtdc_space", None)
+        if s is None:
+            return None
+        if sp is None:
+            sp = s
+        elif sp is not s:
+            return None
+    return sp

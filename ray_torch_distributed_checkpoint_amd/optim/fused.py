@@ -1,0 +1,212 @@
+"""Fused AdamW / SGD: one native launch per param group over the model's flat buffers.
+
+API and `state_dict()` format match `torch.optim.AdamW` / `torch.optim.SGD` (state keys
+`step`, `exp_avg`, `exp_avg_sq` / `momentum_buffer`), so checkpoints interoperate with stock
+torch.  On the GPU the state tensors are views into flat fp32 buffers and the step is the
+chunk-table kernel in csrc/kernels/optim.hip, which also refreshes the bf16 compute shadows.
+On the CPU the same math runs per tensor with torch ops (reference path).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops._ext import gpu_ext
+from .flat import FlatParamSpace, space_of
+
+
+class _FlatOptimizer(torch.optim.Optimizer):
+    _state_keys: tuple = ()
+
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self._space: FlatParamSpace | None = None
+        self._bufs: dict[str, torch.Tensor] = {}
+
+    # -- flat setup ------------------------------------------------------------------------
+    def _all_params(self):
+        return [p for g in self.param_groups for p in g["params"]]
+
+    def _ensure_space(self):
+        if self._space is not None:
+            return self._space
+        params = self._all_params()
+        sp = space_of(params)
+        if sp is None or any(p not in set(sp.params) for p in params):
+            saved = [p.grad.detach().clone() if p.grad is not None else None for p in params]
+            sp = FlatParamSpace(params)
+            for p, g in zip(params, saved):
+                if g is not None:
+                    p.grad.copy_(g)
+        self._space = sp
+        for k in self._state_keys:
+            self._bufs[k] = torch.zeros(sp.numel, dtype=torch.float32, device=sp.device)
+        # adopt any state that already exists (e.g. loaded before the first step)
+        for p in params:
+            st = self.state.get(p)
+            seg = sp.segment_of(p)
+            if st is None:
+                continue
+            for k in self._state_keys:
+                if k in st and torch.is_tensor(st[k]):
+                    v = FlatParamSpace.view(self._bufs[k], seg)
+                    v.copy_(st[k].to(v.device, v.dtype))
+                    st[k] = v
+        return sp
+
+    def _bind_state(self, p):
+        st = self.state[p]
+        seg = self._space.segment_of(p)
+        for k in self._state_keys:
+            if k not in st:
+                st[k] = FlatParamSpace.view(self._bufs[k], seg)
+        return st
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self._space is not None and self._space.grad is not None:
+            self._space.zero_grad()
+        else:
+            super().zero_grad(set_to_none=set_to_none)
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self._space is not None:
+            for p in self._all_params():
+                st = self.state.get(p)
+                if not st:
+                    continue
+                seg = self._space.segment_of(p)
+                for k in self._state_keys:
+                    if k in st and torch.is_tensor(st[k]):
+                        v = FlatParamSpace.view(self._bufs[k], seg)
+                        if st[k].data_ptr() != v.data_ptr():
+                            v.copy_(st[k].to(v.device, v.dtype))
+                            st[k] = v
+
+    def _use_native(self):
+        ps = self._all_params()
+        return bool(ps) and ps[0].is_cuda
+
+    @property
+    def flat_space(self):
+        return self._space
+
+
+class FusedAdamW(_FlatOptimizer):
+    _state_keys = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
+                 maximize=False):
+        if amsgrad or maximize:
+            raise NotImplementedError("amsgrad/maximize are not supported by the fused kernel")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                                      maximize=False, foreach=None, capturable=False, differentiable=False,
+                                      fused=None))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if self._use_native():
+            sp = self._ensure_space()
+            sp.ensure_grad_views()
+            ext = gpu_ext()
+            for group in self.param_groups:
+                ps = group["params"]
+                if not ps:
+                    continue
+                step = None
+                for p in ps:
+                    st = self._bind_state(p)
+                    if "step" not in st:
+                        st["step"] = torch.tensor(0.0)
+                    st["step"] += 1
+                    step = float(st["step"])
+                b1, b2 = group["betas"]
+                wd = group["weight_decay"]
+                chunks, n = sp.chunk_table(ps, [wd != 0.0] * len(ps))
+                ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"], sp.shadow,
+                          group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step, math.sqrt(1 - b2 ** step),
+                          sp.grad_scale)
+            return loss
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if "step" not in st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+                t = float(st["step"])
+                g = p.grad
+                p.mul_(1 - group["lr"] * group["weight_decay"])
+                st["exp_avg"].lerp_(g, 1 - b1)
+                st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+                denom = (st["exp_avg_sq"].sqrt() / math.sqrt(1 - b2 ** t)).add_(group["eps"])
+                p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / (1 - b1 ** t))
+        return loss
+
+
+class FusedSGD(_FlatOptimizer):
+    _state_keys = ("momentum_buffer",)
+
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
+                 maximize=False):
+        if maximize:
+            raise NotImplementedError("maximize is not supported by the fused kernel")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov, maximize=False, foreach=None, differentiable=False,
+                                      fused=None))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if self._use_native():
+            sp = self._ensure_space()
+            sp.ensure_grad_views()
+            ext = gpu_ext()
+            for group in self.param_groups:
+                ps = group["params"]
+                if not ps:
+                    continue
+                mom = group["momentum"]
+                first = False
+                if mom != 0.0:
+                    for p in ps:
+                        st = self.state[p]
+                        if "momentum_buffer" not in st:
+                            first = True
+                        self._bind_state(p)
+                wd = group["weight_decay"]
+                chunks, n = sp.chunk_table(ps, [wd != 0.0] * len(ps))
+                ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None, sp.shadow,
+                        group["lr"], mom, group["dampening"], wd, group["nesterov"], first, sp.grad_scale)
+            return loss
+        for group in self.param_groups:
+            mom = group["momentum"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                d = p.grad
+                if group["weight_decay"] != 0:
+                    d = d.add(p, alpha=group["weight_decay"])
+                if mom != 0:
+                    st = self.state[p]
+                    buf = st.get("momentum_buffer")
+                    if buf is None:
+                        buf = torch.clone(d).detach()
+                        st["momentum_buffer"] = buf
+                    else:
+                        buf.mul_(mom).add_(d, alpha=1 - group["dampening"])
+                    d = d.add(buf, alpha=mom) if group["nesterov"] else buf
+                p.add_(d, alpha=-group["lr"])
+        return loss

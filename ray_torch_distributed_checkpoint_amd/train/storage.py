@@ -1,0 +1,179 @@
+"""On-disk layout, checkpoint commit and retention (Ray 2.39 layout):
+
+    <storage_path>/                                   RunConfig(storage_path)  (R/my_ray_module.py:237)
+      <experiment>/            TorchTrainer_<YYYY-MM-DD_HH-MM-SS>  (RunConfig.name unset)
+        experiment_state.json
+        <trial>/               TorchTrainer_<trialid>_00000_0_<date>  == Result.path
+          params.json  result.json  progress.csv
+          checkpoint_000000/   <- committed checkpoints (num_to_keep newest / best survive)
+          checkpoint_000001/
+
+A checkpoint is visible only after commit: files are gathered in `checkpoint_NNNNNN.tmp/`
+and rank 0 renames the directory atomically (then fsyncs the trial dir), so a crash never
+leaves a half-written `checkpoint_NNNNNN/` (the reference's per-rank same-name overwrite
+race, SURVEY §5.2, cannot occur: rank 0's copy of a shared file name wins deterministically).
+"""
+from __future__ import annotations
+
+import csv
+import json
+import math
+import os
+import random
+import shutil
+import string
+import time
+from datetime import datetime
+
+CKPT_FMT = "checkpoint_{:06d}"
+
+
+def new_experiment_name(prefix: str = "TorchTrainer") -> str:
+    return f"{prefix}_{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}"
+
+
+def new_trial_dirname(prefix: str = "TorchTrainer") -> str:
+    tid = "".join(random.choice("0123456789abcdef") for _ in range(5))
+    return f"{prefix}_{tid}_00000_0_{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}"
+
+
+def fsync_dir(path: str) -> None:
+    try:
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+        finally:
+            os.close(fd)
+    except OSError:
+        pass
+
+
+def staging_dir(trial_dir: str, index: int) -> str:
+    return os.path.join(trial_dir, CKPT_FMT.format(index) + ".tmp")
+
+
+def final_dir(trial_dir: str, index: int) -> str:
+    return os.path.join(trial_dir, CKPT_FMT.format(index))
+
+
+def merge_into(src: str, dst: str, overwrite: bool) -> None:
+    """Copy files of a worker's checkpoint dir into the staging dir (atomic per file)."""
+    os.makedirs(dst, exist_ok=True)
+    if os.path.abspath(src) == os.path.abspath(dst):
+        return
+    for root, dirs, files in os.walk(src):
+        rel = os.path.relpath(root, src)
+        tdir = os.path.join(dst, rel) if rel != "." else dst
+        os.makedirs(tdir, exist_ok=True)
+        for name in files:
+            s = os.path.join(root, name)
+            d = os.path.join(tdir, name)
+            if os.path.exists(d) and not overwrite:
+                continue
+            tmp = d + f".part{os.getpid()}"
+            shutil.copyfile(s, tmp)
+            os.replace(tmp, d)
+
+
+def commit(trial_dir: str, index: int) -> str:
+    src, dst = staging_dir(trial_dir, index), final_dir(trial_dir, index)
+    if os.path.exists(dst):
+        shutil.rmtree(dst)
+    os.replace(src, dst)
+    fsync_dir(trial_dir)
+    return dst
+
+
+def list_committed(trial_dir: str) -> list[tuple[int, str]]:
+    out = []
+    if not os.path.isdir(trial_dir):
+        return out
+    for name in os.listdir(trial_dir):
+        if name.startswith("checkpoint_") and not name.endswith(".tmp") and name[11:].isdigit():
+            out.append((int(name[11:]), os.path.join(trial_dir, name)))
+    return sorted(out)
+
+
+def latest_committed(trial_dir: str) -> str | None:
+    c = list_committed(trial_dir)
+    return c[-1][1] if c else None
+
+
+class TrialLogger:
+    """result.json (JSON lines) + progress.csv + checkpoint registry with retention (rank 0)."""
+
+    def __init__(self, trial_dir: str, num_to_keep=None, score_attr=None, score_order="max"):
+        self.trial_dir = trial_dir
+        self.num_to_keep = num_to_keep
+        self.score_attr = score_attr
+        self.score_order = score_order
+        self.t0 = time.time()
+        self.iteration = 0
+        self.kept: list[tuple[int, str, dict]] = []  # (index, path, metrics)
+        self._csv_fields = None
+        reg = os.path.join(trial_dir, ".checkpoints.json")
+        if os.path.exists(reg):
+            with open(reg) as f:
+                self.kept = [tuple(x) for x in json.load(f)]
+            self.iteration = max([m.get("training_iteration", 0) for _, _, m in self.kept] + [0])
+
+    def log(self, metrics: dict, checkpoint_index: int | None) -> dict:
+        self.iteration += 1
+        now = time.time()
+        row = dict(metrics)
+        row.update({
+            "timestamp": int(now),
+            "checkpoint_dir_name": CKPT_FMT.format(checkpoint_index) if checkpoint_index is not None else None,
+            "done": False,
+            "training_iteration": self.iteration,
+            "time_total_s": now - self.t0,
+            "date": datetime.now().strftime("%Y-%m-%d_%H-%M-%S"),
+            "pid": os.getpid(),
+        })
+        with open(os.path.join(self.trial_dir, "result.json"), "a") as f:
+            f.write(json.dumps(row, default=str) + "\n")
+        csv_path = os.path.join(self.trial_dir, "progress.csv")
+        flat = {k: v for k, v in row.items() if not isinstance(v, (dict, list))}
+        new = not os.path.exists(csv_path)
+        if self._csv_fields is None:
+            self._csv_fields = list(flat.keys())
+        with open(csv_path, "a", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=self._csv_fields, extrasaction="ignore")
+            if new:
+                w.writeheader()
+            w.writerow(flat)
+        return row
+
+    def _score(self, m: dict):
+        v = m.get(self.score_attr)
+        if v is None or (isinstance(v, float) and math.isnan(v)):
+            return -math.inf if self.score_order == "max" else math.inf
+        return v
+
+    def register(self, index: int, path: str, metrics: dict) -> list[str]:
+        """Record a committed checkpoint; delete what retention drops.  Returns deleted paths."""
+        self.kept.append((index, path, metrics))
+        deleted = []
+        if self.num_to_keep is not None and len(self.kept) > self.num_to_keep:
+            if self.score_attr:
+                rev = self.score_order == "max"
+                ranked = sorted(self.kept, key=lambda x: self._score(x[2]), reverse=rev)
+                keep = ranked[: self.num_to_keep]
+                # never delete the most recent checkpoint (needed for fault-tolerant resume)
+                latest = max(self.kept, key=lambda x: x[0])
+                if latest not in keep:
+                    keep = keep[:-1] + [latest]
+            else:
+                keep = sorted(self.kept, key=lambda x: x[0])[-self.num_to_keep:]
+            keep_idx = {k[0] for k in keep}
+            for k in self.kept:
+                if k[0] not in keep_idx:
+                    shutil.rmtree(k[1], ignore_errors=True)
+                    deleted.append(k[1])
+            self.kept = sorted(keep, key=lambda x: x[0])
+        with open(os.path.join(self.trial_dir, ".checkpoints.json"), "w") as f:
+            json.dump([list(k) for k in self.kept], f, default=str)
+        return deleted
+
+    def best_checkpoints(self):
+        return list(self.kept)

@@ -1,0 +1,353 @@
+"""Numerics of every hand-written HIP kernel against a plain PyTorch fp32 reference (GPU only).
+
+Operands are random (never zero/identity, cdna_hip_programming.md §5.4 rule 25-26); the
+asymmetric layouts catch transposed C writes.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ext():
+    from ray_torch_distributed_checkpoint_amd.ops import _ext
+
+    return _ext.ext()
+
+
+def _bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+def _close(out, ref, rel):
+    err = (out.float() - ref.float()).abs().max().item()
+    mag = ref.float().abs().max().item() + 1e-6
+    assert err <= rel * mag, f"max err {err} vs {rel}*{mag}"
+
+
+def test_native_loaded():
+    m = _ext()
+    assert hasattr(m, "gemm_bf16")
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 192), (384, 640, 512)])
+def test_gemm_bf16_layouts(a_k, b_k, M, N, K):
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(M + N + K)
+    A = _bf(M, K) if a_k else _bf(K, M)
+    B = _bf(N, K) if b_k else _bf(K, N)
+    Af = A.float() if a_k else A.float().t()
+    Bf = B.float().t() if b_k else B.float()
+    ref = Af @ Bf
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k)
+    _close(C, ref, 1e-5)
+    Cb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, Cb, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k)
+    _close(Cb, ref, 1e-2)
+
+
+def test_gemm_bf16_epilogues():
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(1)
+    M, N, K = 256, 384, 256
+    A, B = _bf(M, K), _bf(N, K)
+    bias = torch.randn(N, device=DEV)
+    base = A.float() @ B.float().t()
+    # bias + relu
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, K, K, N, bias=bias, act=G.ACT_RELU)
+    _close(C, torch.relu(base + bias), 1e-5)
+    # alpha + residual accumulate (fp32)
+    R = torch.randn(M, N, device=DEV)
+    C2 = R.clone()
+    G.gemm_bf16(A, B, C2, M, N, K, K, K, N, Cin=C2, beta=1.0, alpha=0.5)
+    _close(C2, 0.5 * base + R, 1e-5)
+    # gelu with pre-activation output (bf16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    Cg = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, Cg, M, N, K, K, K, N, bias=bias, act=G.ACT_GELU, aux_out=pre)
+    _close(pre, base + bias, 1e-2)
+    _close(Cg, F.gelu(base + bias, approximate="tanh"), 1e-2)
+    # gelu backward epilogue
+    h = _bf(M, N)
+    Cb = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, Cb, M, N, K, K, K, N, act=G.ACT_GELU_BWD, aux_in=h)
+    hf = h.float().requires_grad_(True)
+    y = F.gelu(hf, approximate="tanh")
+    (gd,) = torch.autograd.grad(y.sum(), hf)
+    _close(Cb, base * gd, 1e-4)
+
+
+def test_gemm_bf16_batched_strided():
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(2)
+    Bn, H, T, Dh = 2, 3, 256, 64
+    x = _bf(Bn, T, H * Dh)
+    y = _bf(Bn, T, H * Dh)
+    out = torch.empty(Bn, H, T, T, device=DEV, dtype=torch.float32)
+    C = H * Dh
+    G.gemm_bf16(x, y, out, T, T, Dh, C, C, T, True, True, batch=Bn * H, batch_inner=H,
+                strides=(T * C, Dh, T * C, Dh, H * T * T, T * T))
+    xr = x.float().view(Bn, T, H, Dh).transpose(1, 2)
+    yr = y.float().view(Bn, T, H, Dh).transpose(1, 2)
+    _close(out, xr @ yr.transpose(-1, -2), 1e-5)
+
+
+def test_linear_bf16_autograd():
+    from ray_torch_distributed_checkpoint_amd.ops import linear
+
+    torch.manual_seed(3)
+    M, K, N = 512, 384, 256
+    x = _bf(M, K).requires_grad_(True)
+    w = (torch.randn(N, K, device=DEV) * 0.05).requires_grad_(True)
+    b = torch.randn(N, device=DEV).requires_grad_(True)
+    res = _bf(M, N).requires_grad_(True)
+    y = linear(x, w, b, relu=False, residual=res)
+    g = _bf(M, N)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    rr = res.detach().float().requires_grad_(True)
+    yr = F.linear(xr, wr, br) + rr
+    yr.backward(g.float())
+    _close(y, yr, 1e-2)
+    _close(x.grad, xr.grad, 1e-2)
+    _close(w.grad, wr.grad, 1e-4)
+    _close(b.grad, br.grad, 1e-4)
+    _close(res.grad, rr.grad, 1e-6)
+    # relu variant
+    x.grad = None
+    w.grad = None
+    y2 = linear(x, w, b, relu=True)
+    y2.backward(g)
+    xr.grad = None
+    wr.grad = None
+    yr2 = torch.relu(F.linear(xr, wr, br.detach()))
+    yr2.backward(g.float())
+    _close(x.grad, xr.grad, 2e-2)
+    _close(w.grad, wr.grad, 1e-3)
+
+
+def test_fused_mlp():
+    from ray_torch_distributed_checkpoint_amd.ops import fused_mlp
+
+    torch.manual_seed(4)
+    M, C = 256, 128
+    x = _bf(M, C).requires_grad_(True)
+    wf = (torch.randn(4 * C, C, device=DEV) * 0.05).requires_grad_(True)
+    bfc = (torch.randn(4 * C, device=DEV) * 0.1).requires_grad_(True)
+    wp = (torch.randn(C, 4 * C, device=DEV) * 0.05).requires_grad_(True)
+    bp = (torch.randn(C, device=DEV) * 0.1).requires_grad_(True)
+    y = fused_mlp(x, wf, bfc, wp, bp, residual=x)
+    g = _bf(M, C)
+    y.backward(g)
+    ps = [x.detach().float(), wf.detach().bfloat16().float(), bfc.detach(), wp.detach().bfloat16().float(), bp.detach()]
+    ps = [p.clone().requires_grad_(True) for p in ps]
+    h = F.gelu(F.linear(ps[0], ps[1], ps[2]), approximate="tanh")
+    yr = F.linear(h, ps[3], ps[4]) + ps[0]
+    yr.backward(g.float())
+    _close(y, yr, 2e-2)
+    _close(x.grad, ps[0].grad, 3e-2)
+    _close(wf.grad, ps[1].grad, 2e-2)
+    _close(wp.grad, ps[3].grad, 2e-2)
+    _close(bfc.grad, ps[2].grad, 2e-2)
+    _close(bp.grad, ps[4].grad, 1e-4)
+
+
+@pytest.mark.parametrize("H,Hkv", [(4, 4), (4, 2)])
+def test_causal_attention(H, Hkv):
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref
+
+    torch.manual_seed(5)
+    Bn, T, Dh = 2, 256, 64
+    W = (H + 2 * Hkv) * Dh
+    qkv = _bf(Bn, T, W).requires_grad_(True)
+    out = causal_attention(qkv, H, Hkv)
+    g = _bf(Bn, T, H * Dh)
+    out.backward(g)
+    qr = qkv.detach().float().requires_grad_(True)
+    ref = causal_attention_ref(qr, Bn, T, H, Hkv, Dh)
+    ref.backward(g.float())
+    _close(out, ref, 2e-2)
+    _close(qkv.grad, qr.grad, 3e-2)
+
+
+def test_layernorm_rmsnorm():
+    from ray_torch_distributed_checkpoint_amd.ops import layer_norm, rms_norm
+
+    torch.manual_seed(6)
+    for D in (768, 4096, 200):
+        M = 64
+        x = _bf(M, D, scale=2.0).requires_grad_(True)
+        w = (1 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+        b = (0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+        g = _bf(M, D)
+        y = layer_norm(x, w, b)
+        y.backward(g)
+        xr = x.detach().float().requires_grad_(True)
+        wr = w.detach().bfloat16().float().requires_grad_(True)
+        br = b.detach().bfloat16().float().requires_grad_(True)
+        yr = F.layer_norm(xr, (D,), wr, br, 1e-5)
+        yr.backward(g.float())
+        _close(y, yr, 2e-2)
+        _close(x.grad, xr.grad, 2e-2)
+        _close(w.grad, wr.grad, 1e-3)
+        _close(b.grad, br.grad, 1e-3)
+        x.grad = None
+        w.grad = None
+        y2 = rms_norm(x, w)
+        y2.backward(g)
+        xr2 = x.detach().float().requires_grad_(True)
+        wr2 = w.detach().bfloat16().float().requires_grad_(True)
+        yr2 = xr2 * torch.rsqrt(xr2.pow(2).mean(-1, keepdim=True) + 1e-5) * wr2
+        yr2.backward(g.float())
+        _close(y2, yr2, 2e-2)
+        _close(x.grad, xr2.grad, 2e-2)
+        _close(w.grad, wr2.grad, 1e-3)
+
+
+@pytest.mark.parametrize("dtype,V,ld", [(torch.float32, 10, 10), (torch.bfloat16, 1000, 1024), (torch.float32, 333, 333)])
+def test_cross_entropy(dtype, V, ld):
+    from ray_torch_distributed_checkpoint_amd.ops import cross_entropy, xent_metrics
+
+    torch.manual_seed(7)
+    M = 64
+    logits = (torch.randn(M, V, device=DEV) * 3).to(dtype).requires_grad_(True)
+    tgt = torch.randint(0, V, (M,), device=DEV)
+    loss = cross_entropy(logits, tgt)
+    loss.backward()
+    lr_ = logits.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(lr_, tgt)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    _close(logits.grad, lr_.grad, 2e-2 if dtype == torch.bfloat16 else 1e-4)
+    ls, nc = xent_metrics(logits.detach(), tgt)
+    assert abs(ls.item() - ref.item() * M) < 1e-2 * M
+    assert nc.item() == (lr_.detach().argmax(1) == tgt).sum().item()
+
+
+def test_lm_head_cross_entropy_padded_vocab():
+    from ray_torch_distributed_checkpoint_amd.ops import lm_head_cross_entropy
+
+    torch.manual_seed(8)
+    M, C, V, Vp = 128, 128, 1000, 1024
+    x = _bf(M, C).requires_grad_(True)
+    w = (torch.randn(Vp, C, device=DEV) * 0.1).requires_grad_(True)
+    tgt = torch.randint(0, V, (M,), device=DEV)
+    loss = lm_head_cross_entropy(x, w, tgt, V)
+    loss.backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    ref = F.cross_entropy(F.linear(xr, wr)[:, :V], tgt)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-2
+    _close(x.grad, xr.grad, 3e-2)
+    _close(w.grad, wr.grad, 3e-2)
+    assert w.grad[V:].abs().max().item() == 0.0
+
+
+def test_embedding():
+    from ray_torch_distributed_checkpoint_amd.ops import embedding
+
+    torch.manual_seed(9)
+    Bn, T, D, V = 4, 64, 128, 500
+    idx = torch.randint(0, V, (Bn, T), device=DEV)
+    wte = torch.randn(V, D, device=DEV).requires_grad_(True)
+    wpe = torch.randn(128, D, device=DEV).requires_grad_(True)
+    y = embedding(idx, wte, wpe)
+    g = _bf(Bn, T, D)
+    y.backward(g)
+    wr = wte.detach().bfloat16().float().requires_grad_(True)
+    pr = wpe.detach().bfloat16().float().requires_grad_(True)
+    yr = F.embedding(idx, wr) + pr[:T]
+    yr.backward(g.float())
+    _close(y, yr, 1e-2)
+    _close(wte.grad, wr.grad, 1e-4)
+    _close(wpe.grad, pr.grad, 1e-4)
+
+
+def test_dropout_mask_consistency():
+    from ray_torch_distributed_checkpoint_amd.ops import dropout
+
+    torch.manual_seed(10)
+    x = torch.randn(100_003, device=DEV).requires_grad_(True)
+    y = dropout(x, 0.25, True)
+    keep = y.detach() != 0
+    frac = keep.float().mean().item()
+    assert 0.73 < frac < 0.77
+    _close(y[keep], x.detach()[keep] / 0.75, 1e-6)
+    y.backward(torch.ones_like(y))
+    assert torch.equal(x.grad != 0, keep)
+
+
+def test_linear_f32():
+    from ray_torch_distributed_checkpoint_amd.ops import linear
+
+    torch.manual_seed(11)
+    for (M, K, N) in [(16, 784, 512), (16, 512, 10), (37, 100, 70)]:
+        x = torch.randn(M, K, device=DEV).requires_grad_(True)
+        w = (torch.randn(N, K, device=DEV) * 0.05).requires_grad_(True)
+        b = torch.randn(N, device=DEV).requires_grad_(True)
+        y = linear(x, w, b, relu=True)
+        g = torch.randn(M, N, device=DEV)
+        y.backward(g)
+        xr, wr, br = [t.detach().clone().double().requires_grad_(True) for t in (x, w, b)]
+        yr = torch.relu(F.linear(xr, wr, br))
+        yr.backward(g.double())
+        _close(y, yr, 1e-5)
+        _close(x.grad, xr.grad, 1e-5)
+        _close(w.grad, wr.grad, 1e-5)
+        _close(b.grad, br.grad, 1e-5)
+
+
+def test_fused_optimizers_match_torch():
+    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW, FusedSGD
+
+    torch.manual_seed(12)
+    shapes = [(64, 33), (7,), (128, 128), (3, 5, 9)]
+    for kind in ("adamw", "sgd"):
+        ps = [torch.randn(*s, device=DEV, requires_grad=True) for s in shapes]
+        qs = [p.detach().clone().requires_grad_(True) for p in ps]
+        if kind == "adamw":
+            opt = FusedAdamW(ps, lr=1e-2, weight_decay=0.1)
+            ref = torch.optim.AdamW(qs, lr=1e-2, weight_decay=0.1, foreach=False)
+        else:
+            opt = FusedSGD(ps, lr=1e-2, momentum=0.9)
+            ref = torch.optim.SGD(qs, lr=1e-2, momentum=0.9, foreach=False)
+        for step in range(4):
+            grads = [torch.randn_like(p) for p in ps]
+            opt.zero_grad()
+            ref.zero_grad()
+            for p, q, g in zip(ps, qs, grads):
+                p.grad = g.clone() if p.grad is None else p.grad.copy_(g)
+                q.grad = g.clone()
+            opt.step()
+            ref.step()
+        for p, q in zip(ps, qs):
+            _close(p, q, 1e-5)
+
+
+def test_ckpt_engine_writes_torch_loadable(tmp_path):
+    from ray_torch_distributed_checkpoint_amd.checkpoint import torchsave
+
+    torch.manual_seed(13)
+    sd = {"w": torch.randn(300, 77, device=DEV), "b": torch.arange(10, device=DEV),
+          "h": torch.randn(5, device=DEV).bfloat16(), "meta": {"epoch": 3, "losses": [1.5, 2.0]}}
+    p = str(tmp_path / "x.pt")
+    torchsave.save(sd, p)
+    got = torch.load(p, weights_only=True)
+    assert got["meta"] == sd["meta"]
+    for k in ("w", "b", "h"):
+        assert torch.equal(got[k], sd[k].cpu())
