@@ -1,0 +1,237 @@
+"""Headline benchmark: samples/sec (+ sharded checkpoint save/restore wall-clock) on 1-8 MI355X.
+
+Metric and configs come from BASELINE.json: "samples/sec/GPU + checkpoint save+restore
+wall-clock at 1/2/4/8 MI355X".  Flagship = GPT-2-small DDP (BASELINE config 3): per GPU a
+fixed micro-batch of 16 x 1024 tokens (weak scaling), bf16 compute on the hand-written
+gfx950 kernels, fp32 master weights + fused AdamW, bucketed gradient all-reduce on RCCL
+overlapped with backward.  Synthetic token data, random-init weights.
+
+Timed region: exactly K full training steps (forward, backward + all-reduce, optimizer
+step), bracketed by barrier + device synchronize, max over ranks.  After it, the checkpoint
+phase measures a DCP-format sharded save of the full train state (model + AdamW state +
+step): time until training can resume (HBM snapshot enqueued), time until every shard is
+durable and `.metadata` committed, training throughput while the write is in flight, and
+the restore wall-clock (sharded read + RCCL broadcast into the live model/optimizer).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model gpt2-small] [--batch 16]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE = os.path.join(ROOT, "BASELINE.json")
+
+
+def _baseline_metric():
+    try:
+        with open(BASELINE) as f:
+            b = json.load(f)
+        return b["metric"], b.get("published") or {}
+    except Exception:
+        return "samples/sec/GPU + checkpoint save+restore wall-clock at 1/2/4/8 MI355X", {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--batch", type=int, default=16, help="sequences per GPU per step")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--no-ckpt", action="store_true")
+    ap.add_argument("--ckpt-dir", default=None)
+    ap.add_argument("--overlap-steps", type=int, default=5)
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch one process per GPU (before anything touches the GPU)
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", "--master-port=29517", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
+    from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+    from ray_torch_distributed_checkpoint_amd.ops import _ext
+
+    _ext.gpu_ext()  # native kernels are mandatory on the GPU path
+    torch.manual_seed(1234)
+    cfg = GPT2Config.named(args.model)
+    T = min(args.seq_len, cfg.n_positions)
+    B = args.batch
+    model = GPT2(cfg).to(dev)
+    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
+    opt = FusedAdamW(model.parameters(), lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    pool = [torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev, generator=g) for _ in range(4)]
+
+    def step(i):
+        data = pool[i % len(pool)]
+        loss = net(data[:, :-1], data[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    for i in range(args.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    ms_per_step = dt / args.steps * 1e3
+    samples_per_s = world * B * args.steps / dt
+    final_loss = loss.item()
+
+    ck = {}
+    if not args.no_ckpt:
+        ck = checkpoint_phase(args, model, opt, net, pool, step, world, rank, dev, dcp)
+
+    metric, published = _baseline_metric()
+    base = published.get("samples_per_sec") if isinstance(published, dict) else None
+    flops_tok = model.flops_per_token(T)
+    out = {
+        "metric": metric,
+        "value": round(samples_per_s, 3),
+        "unit": "samples/s (sequences of %d tokens, all GPUs)" % T,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(samples_per_s / base, 4) if base else None),
+        "dtype": "bf16",
+        "data": "synthetic (random tokens), random-init weights",
+        "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
+                   "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "optimizer": "fused AdamW (fp32 master)",
+                   "params": model.num_params()},
+        "samples_per_sec_per_gpu": round(samples_per_s / world, 3),
+        "tokens_per_sec": round(samples_per_s * T, 1),
+        "model_tflops_per_gpu": round(flops_tok * samples_per_s * T / world / 1e12, 2),
+        "final_loss": round(final_loss, 4),
+    }
+    out.update(ck)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def checkpoint_phase(args, model, opt, net, pool, step, world, rank, dev, dcp):
+    base = args.ckpt_dir or os.environ.get("RTDC_BENCH_CKPT_DIR") or tempfile.gettempdir()
+    path = os.path.join(base, "rtdc_bench_ckpt")
+    if rank == 0:
+        shutil.rmtree(path, ignore_errors=True)
+        os.makedirs(path, exist_ok=True)
+    if world > 1:
+        dist.barrier()
+
+    def state():
+        return {"model": model.state_dict(), "optim": opt.state_dict(), "step": 1}
+
+    # ---- async save overlapped with training steps
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    h = dcp.async_save(state(), path)
+    t_resume = time.perf_counter() - t0  # training may continue from here
+    t1 = time.perf_counter()
+    for i in range(args.overlap_steps):
+        step(i)
+    torch.cuda.synchronize()
+    overlap_ms = (time.perf_counter() - t1) / max(1, args.overlap_steps) * 1e3
+    local_write = h.wait()
+    if world > 1:
+        dist.barrier()
+    h._finish()
+    if world > 1:
+        dist.barrier()
+    t_durable = time.perf_counter() - t0
+    nbytes = torch.tensor([float(h.nbytes)], device=dev)
+    if world > 1:
+        dist.all_reduce(nbytes)
+    # ---- blocking save (nothing overlapped) for the pure write bandwidth
+    path2 = path + "_sync"
+    if rank == 0:
+        shutil.rmtree(path2, ignore_errors=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    dcp.save(state(), path2)
+    t_sync = time.perf_counter() - t2
+    # ---- restore into the live model + optimizer
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t3 = time.perf_counter()
+    sd = state()
+    dcp.load(sd, path2)
+    opt.load_state_dict(sd["optim"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_restore = time.perf_counter() - t3
+    vals = torch.tensor([t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write], device=dev)
+    if world > 1:
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+    t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write = vals.tolist()
+    if rank == 0:
+        shutil.rmtree(path, ignore_errors=True)
+        shutil.rmtree(path2, ignore_errors=True)
+    total = nbytes.item()
+    return {
+        "ckpt_bytes_total": int(total),
+        "ckpt_save_blocking_s": round(t_resume, 4),
+        "ckpt_save_durable_s": round(t_durable, 4),
+        "ckpt_save_sync_s": round(t_sync, 4),
+        "ckpt_restore_s": round(t_restore, 4),
+        "ckpt_save_plus_restore_s": round(t_sync + t_restore, 4),
+        "ckpt_write_GBps": round(total / max(t_sync, 1e-9) / 1e9, 3),
+        "ms_per_step_during_async_save": round(overlap_ms, 3),
+        "ckpt_format": "torch.distributed.checkpoint (.metadata + __r_0.distcp), native engine",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,448 @@
+"""Sharded checkpoints in the `torch.distributed.checkpoint` (DCP) on-disk format, natively.
+
+Format (identical to torch DCP 2.x, so `torch.distributed.checkpoint.load` reads what we
+write and we read what it writes - torch/distributed/checkpoint/filesystem.py:97,319-372,763):
+  <dir>/__{rank}_0.distcp   back-to-back items: a torch.save zip archive per tensor chunk,
+                            torch.save bytes per non-tensor value (BYTE_IO)
+  <dir>/.metadata           pickled `Metadata` (tensor sizes/chunks, storage (file, off, len)),
+                            written by rank 0 via .tmp + fsync + rename (atomic commit)
+
+What is different from torch DCP, MI355X-first:
+* **Planning needs no collectives.**  Data-parallel state is replicated, so every rank
+  flattens the same state_dict, computes the same size-balanced owner assignment (the
+  dedup of _dedup_save_plans.py, but greedy by bytes) and the same file layouts (item sizes
+  are deterministic), so rank 0 can write `.metadata` without gather/scatter of plans.
+* **Snapshot in HBM, write in the background.**  Owned tensors are cloned on the compute
+  stream (a few D2D copies: ~0.1 ms per 100 MB at HBM rate; 288 GB leaves room for a full
+  copy of even the Llama-3-8B per-rank shard), then the C++ engine drains them through a
+  bounded pinned ring on its own copy stream to writer threads.  Training continues at once;
+  stream order protects the snapshot from the next optimizer step - no fence needed.
+* **Restore reads each byte once.**  Items are assigned to reader ranks (balanced), read
+  with parallel pread into pinned memory, copied H2D and broadcast over RCCL/xGMI, instead
+  of every rank reading the whole checkpoint.  Works across world sizes (resharding).
+"""
+from __future__ import annotations
+
+import dataclasses
+import io
+import os
+import pickle
+import struct
+import time
+import uuid
+
+import torch
+import torch.distributed as dist
+from torch.distributed.checkpoint._nested_dict import flatten_state_dict
+from torch.distributed.checkpoint.filesystem import _StorageInfo
+from torch.distributed.checkpoint.metadata import (BytesStorageMetadata, ChunkStorageMetadata, Metadata,
+                                                   MetadataIndex, StorageMeta, TensorProperties,
+                                                   TensorStorageMetadata)
+
+from ..ops import _ext
+from . import torchsave
+
+METADATA_FN = ".metadata"
+DCP_VERSION = "1.0.0"
+
+
+# ------------------------------------------------------------------------------ helpers
+def _world(pg=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(pg), dist.get_rank(pg)
+    return 1, 0
+
+
+def _resolve_stateful(state_dict: dict) -> dict:
+    out = {}
+    for k, v in state_dict.items():
+        if hasattr(v, "state_dict") and callable(v.state_dict) and not torch.is_tensor(v):
+            out[k] = v.state_dict()
+        else:
+            out[k] = v
+    return out
+
+
+def _bytes_of(obj) -> bytes:
+    buf = io.BytesIO()
+    torch.save(obj, buf)
+    return buf.getvalue()
+
+
+def _balanced_owner(items: list[tuple[str, int]], world: int) -> dict[str, int]:
+    """Deterministic greedy bin packing by bytes (largest first, ties by fqn)."""
+    load = [0] * world
+    owner = {}
+    for fqn, n in sorted(items, key=lambda x: (-x[1], x[0])):
+        r = min(range(world), key=lambda i: (load[i], i))
+        owner[fqn] = r
+        load[r] += max(n, 1)
+    return owner
+
+
+_pkl_cache: dict = {}
+
+
+def _shape_tensor(dtype, shape):
+    return torch.empty(shape, dtype=dtype, device="meta")
+
+
+def _pkl_for(dtype, shape) -> bytes:
+    key = (dtype, tuple(shape))
+    v = _pkl_cache.get(key)
+    if v is None:
+        v, _ = torchsave.pickle_state(_shape_tensor(dtype, shape))
+        _pkl_cache[key] = v
+    return v
+
+
+# ------------------------------------------------------------------------------ save
+@dataclasses.dataclass
+class _Item:
+    fqn: str
+    kind: str  # "tensor" | "bytes"
+    nbytes: int
+    tensor: torch.Tensor | None = None
+    data: bytes | None = None
+
+
+def _collect(state_dict):
+    sd = _resolve_stateful(state_dict)
+    flat, mapping = flatten_state_dict(sd)
+    items = []
+    for fqn, v in flat.items():
+        if torch.is_tensor(v):
+            t = v.detach()
+            items.append(_Item(fqn, "tensor", t.numel() * t.element_size(), tensor=t))
+        else:
+            b = _bytes_of(v)
+            items.append(_Item(fqn, "bytes", len(b), data=b))
+    return items, mapping
+
+
+def _archives_for(items: list[_Item], with_ptrs: bool):
+    arcs = []
+    for it in items:
+        if it.kind == "tensor":
+            t = it.tensor
+            ptr = t.data_ptr() if with_ptrs else 1
+            if it.nbytes == 0:
+                arcs.append((False, torchsave.build_records(_pkl_for(t.dtype, t.shape), [(0, 0, False)])))
+            else:
+                arcs.append((False, torchsave.build_records(_pkl_for(t.dtype, t.shape),
+                                                            [(ptr, it.nbytes, t.is_cuda and with_ptrs)])))
+        else:
+            arcs.append((True, [("bytes", it.data, 0, 0, False)]))
+    return arcs
+
+
+class AsyncSave:
+    """Handle of an in-flight sharded save on this rank."""
+
+    def __init__(self, checkpoint_id, handle, metadata, rank, t_start, t_return, nbytes, pg):
+        self.checkpoint_id, self._h, self._metadata = checkpoint_id, handle, metadata
+        self.rank, self.t_start, self.t_return, self.nbytes, self.pg = rank, t_start, t_return, nbytes, pg
+        self.write_s = None
+
+    def wait(self) -> float:
+        """Local shard durable.  Returns seconds since the save call."""
+        if self._h is not None:
+            self._h.wait()
+            self._h = None
+        if self.write_s is None:
+            self.write_s = time.perf_counter() - self.t_start
+        return self.write_s
+
+    def _finish(self):
+        """Rank 0: write `.metadata` atomically (call after every rank's wait())."""
+        if self.rank == 0 and self._metadata is not None:
+            write_metadata(self.checkpoint_id, self._metadata)
+
+    def result(self):
+        """wait + barrier + metadata commit + barrier (collective on `pg`)."""
+        self.wait()
+        w, _ = _world(self.pg)
+        if w > 1:
+            dist.barrier(group=self.pg)
+        self._finish()
+        if w > 1:
+            dist.barrier(group=self.pg)
+        return self
+
+
+def write_metadata(checkpoint_id: str, md: Metadata):
+    tmp = os.path.join(checkpoint_id, METADATA_FN + ".tmp")
+    with open(tmp, "wb") as f:
+        pickle.dump(md, f)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, os.path.join(checkpoint_id, METADATA_FN))
+    from ..train.storage import fsync_dir
+
+    fsync_dir(checkpoint_id)
+
+
+def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsync: bool = True,
+               crc: bool = True, replicated: bool = True) -> AsyncSave:
+    """Start a sharded save; returns once the HBM snapshot is enqueued (non-blocking)."""
+    t0 = time.perf_counter()
+    world, rank = _world(process_group)
+    os.makedirs(checkpoint_id, exist_ok=True)
+    items, mapping = _collect(state_dict)
+    if replicated:
+        owner = _balanced_owner([(it.fqn, it.nbytes) for it in items], world)
+        all_items = items
+    else:
+        # sharded state (e.g. per-rank shards): every rank writes its own items; fqns must be unique
+        owner = {it.fqn: rank for it in items}
+        all_items = items
+    per_rank: dict[int, list[_Item]] = {r: [] for r in range(world)}
+    for it in all_items:
+        per_rank[owner[it.fqn]].append(it)
+    mine = per_rank[rank]
+    # HBM / host snapshot of owned tensors: cloned in stream order on the compute stream
+    for it in mine:
+        if it.kind == "tensor":
+            it.tensor = it.tensor.clone(memory_format=torch.contiguous_format)
+    ready = None
+    if any(it.kind == "tensor" and it.tensor.is_cuda for it in mine):
+        ready = torch.cuda.Event()
+        ready.record()
+    ext = _ext.ext()
+    metadata = None
+    if rank == 0 or not replicated:
+        sd_md = {}
+        storage = {}
+        ranks = range(world) if replicated else [rank]
+        for r in ranks:
+            fname = f"__{r}_0.distcp"
+            arcs = _archives_for(per_rank[r], with_ptrs=False)
+            _, lay = ext.plan_layout(arcs)
+            for it, (base, size, _recs) in zip(per_rank[r], lay):
+                if it.kind == "tensor":
+                    t = it.tensor
+                    zeros = torch.Size([0] * t.dim())
+                    sd_md[it.fqn] = TensorStorageMetadata(
+                        properties=TensorProperties(dtype=t.dtype), size=torch.Size(t.shape),
+                        chunks=[ChunkStorageMetadata(offsets=zeros, sizes=torch.Size(t.shape))])
+                    storage[MetadataIndex(it.fqn, zeros, 0)] = _StorageInfo(fname, base, size)
+                else:
+                    sd_md[it.fqn] = BytesStorageMetadata()
+                    storage[MetadataIndex(it.fqn)] = _StorageInfo(fname, base, size)
+        metadata = Metadata(state_dict_metadata=sd_md, planner_data=mapping, storage_data=storage,
+                            storage_meta=StorageMeta(checkpoint_id=checkpoint_id, save_id=str(uuid.uuid4())),
+                            version=DCP_VERSION)
+        if not replicated and world > 1:
+            # gather per-rank metadata on rank 0 (CPU object collective)
+            parts = [None] * world
+            dist.all_gather_object(parts, metadata, group=process_group)
+            if rank == 0:
+                for p in parts[1:]:
+                    metadata.state_dict_metadata.update(p.state_dict_metadata)
+                    metadata.storage_data.update(p.storage_data)
+                    metadata.planner_data.update(p.planner_data)
+            else:
+                metadata = None
+    elif not replicated and world > 1:
+        pass
+    handle = None
+    nbytes = sum(it.nbytes for it in mine)
+    if mine:
+        arcs = _archives_for(mine, with_ptrs=True)
+        path = os.path.join(checkpoint_id, f"__{rank}_0.distcp")
+        handle = torchsave.submit_files([(path, fsync, crc, arcs)], [it.tensor for it in mine if it.tensor is not None],
+                                        nbytes, ready)
+    return AsyncSave(checkpoint_id, handle, metadata, rank, t0, time.perf_counter() - t0, nbytes, process_group)
+
+
+def save(state_dict: dict, checkpoint_id: str, process_group=None, **kw) -> AsyncSave:
+    """Blocking sharded save (collective): returns after `.metadata` is committed."""
+    return async_save(state_dict, checkpoint_id, process_group, **kw).result()
+
+
+# ------------------------------------------------------------------------------ load
+class _SafeUnpickler(pickle.Unpickler):
+    """Only the DCP metadata dataclasses and torch/builtin value types - no arbitrary code."""
+
+    _ALLOWED = {
+        ("torch.distributed.checkpoint.metadata", n) for n in (
+            "Metadata", "MetadataIndex", "TensorStorageMetadata", "BytesStorageMetadata", "ChunkStorageMetadata",
+            "TensorProperties", "StorageMeta", "_MEM_FORMAT_ENCODING")
+    } | {("torch.distributed.checkpoint.filesystem", "_StorageInfo"), ("torch", "Size"), ("torch", "strided"),
+         ("collections", "OrderedDict"), ("pathlib", "PosixPath"), ("torch", "device"),
+         ("torch.serialization", "_get_layout"),
+         ("torch.distributed.checkpoint._extension", "StreamTransformExtension")}
+
+    def find_class(self, module, name):
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        if module == "torch" and isinstance(getattr(torch, name, None), torch.dtype):
+            return getattr(torch, name)
+        if module == "torch" and name in ("layout",):
+            return getattr(torch, name)
+        raise pickle.UnpicklingError(f"disallowed global in checkpoint metadata: {module}.{name}")
+
+
+def read_metadata(checkpoint_id: str) -> Metadata:
+    with open(os.path.join(checkpoint_id, METADATA_FN), "rb") as f:
+        return _SafeUnpickler(f).load()
+
+
+def _zip_data_record(path: str, base: int, length: int) -> tuple[int, int]:
+    """(absolute data offset, size) of the tensor record '<prefix>/data/0' in a zip slice."""
+    with open(path, "rb") as f:
+        tail_len = min(length, 1 << 16)
+        f.seek(base + length - tail_len)
+        tail = f.read(tail_len)
+        eocd = tail.rfind(b"PK\x05\x06")
+        if eocd < 0:
+            raise IOError(f"{path}@{base}: no zip end record")
+        n, cd_size, cd_off = struct.unpack("<HII", tail[eocd + 10:eocd + 20])
+        f.seek(base + cd_off)
+        cd = f.read(cd_size)
+        pos = 0
+        for _ in range(n):
+            (sig,) = struct.unpack("<I", cd[pos:pos + 4])
+            assert sig == 0x02014B50
+            csize, = struct.unpack("<I", cd[pos + 20:pos + 24])
+            nlen, elen, clen = struct.unpack("<HHH", cd[pos + 28:pos + 34])
+            lho, = struct.unpack("<I", cd[pos + 42:pos + 46])
+            name = cd[pos + 46:pos + 46 + nlen].decode()
+            if name.endswith("/data/0"):
+                f.seek(base + lho)
+                lh = f.read(30)
+                lnlen, lelen = struct.unpack("<HH", lh[26:30])
+                return base + lho + 30 + lnlen + lelen, csize
+            pos += 46 + nlen + elen + clen
+    raise IOError(f"{path}@{base}: no tensor data record")
+
+
+def _pinned(n: int) -> torch.Tensor:
+    t = torch.empty(n, dtype=torch.uint8)
+    if torch.cuda.is_available():
+        t = t.pin_memory()
+    return t
+
+
+def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast: bool = True,
+         pinned_mb: int = 1024, threads: int = 8) -> dict:
+    """Load a DCP-format checkpoint IN PLACE into `state_dict` (tensors copied into, Stateful
+    objects get load_state_dict).  Collective when a process group is initialised."""
+    world, rank = _world(process_group)
+    md = read_metadata(checkpoint_id)
+    resolved = _resolve_stateful(state_dict)
+    flat, mapping = flatten_state_dict(resolved)
+    ext = _ext.ext()
+    # index storage entries per fqn
+    chunks_of: dict[str, list] = {}
+    for idx, info in md.storage_data.items():
+        chunks_of.setdefault(idx.fqn, []).append((idx, info))
+    tensor_fqns = [k for k, v in flat.items() if torch.is_tensor(v)]
+    missing = [k for k in flat if k not in md.state_dict_metadata]
+    if missing:
+        raise KeyError(f"checkpoint {checkpoint_id} is missing keys: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+    sizes = []
+    for k in tensor_fqns:
+        m = md.state_dict_metadata[k]
+        n = 1
+        for s in m.size:
+            n *= s
+        sizes.append((k, n * flat[k].element_size()))
+    reader = _balanced_owner(sizes, world) if broadcast else {k: rank for k in tensor_fqns}
+    my = [k for k in tensor_fqns if reader[k] == rank]
+    # ---- read my items: (dest tensor, chunk offsets, chunk sizes, file, data offset, nbytes)
+    reqs = []
+    for k in my:
+        dest = flat[k]
+        mdt = md.state_dict_metadata[k]
+        if tuple(mdt.size) != tuple(dest.shape):
+            raise ValueError(f"{k}: checkpoint shape {tuple(mdt.size)} != destination {tuple(dest.shape)}")
+        for idx, info in chunks_of[k]:
+            path = os.path.join(checkpoint_id, info.relative_path)
+            off, n = _zip_data_record(path, info.offset, info.length)
+            csizes = None
+            for c in mdt.chunks:
+                if tuple(c.offsets) == tuple(idx.offset):
+                    csizes = tuple(c.sizes)
+            reqs.append((dest, tuple(idx.offset), csizes or tuple(dest.shape), path, off, n, mdt.properties.dtype))
+    # batched: parallel pread into a pinned buffer, then H2D into the destination
+    cap = max(pinned_mb << 20, max([r[5] for r in reqs], default=0))
+    staging = _pinned(min(cap, sum(r[5] for r in reqs))) if reqs else None
+    i = 0
+    while i < len(reqs):
+        batch, used = [], 0
+        while i < len(reqs) and (not batch or used + reqs[i][5] <= cap):
+            batch.append((reqs[i], used))
+            used += reqs[i][5]
+            i += 1
+        by_file: dict[str, tuple[list, list, list]] = {}
+        base_ptr = staging.data_ptr()
+        for (dest, offs, csz, path, off, n, dt), at in batch:
+            o, l, d = by_file.setdefault(path, ([], [], []))
+            o.append(off)
+            l.append(n)
+            d.append(base_ptr + at)
+        for path, (o, l, d) in by_file.items():
+            ext.read_ranges(path, o, l, d, threads)
+        for (dest, offs, csz, path, off, n, dt), at in batch:
+            src = staging[at:at + n].view(dt).view(csz)
+            region = dest
+            for dim, (o, s) in enumerate(zip(offs, csz)):
+                region = region.narrow(dim, o, s)
+            with torch.no_grad():
+                region.copy_(src, non_blocking=dest.is_cuda)
+        if dest_is_cuda(batch):
+            torch.cuda.current_stream().synchronize()  # staging reuse
+    # ---- broadcast from readers
+    if broadcast and world > 1:
+        for k in tensor_fqns:
+            t = flat[k]
+            if t.is_contiguous():
+                dist.broadcast(t, src=_global_rank(reader[k], process_group), group=process_group)
+            else:
+                tmp = t.contiguous()
+                dist.broadcast(tmp, src=_global_rank(reader[k], process_group), group=process_group)
+                with torch.no_grad():
+                    t.copy_(tmp)
+    # ---- non-tensor values (rank 0 reads, broadcasts as objects)
+    obj_keys = [k for k in flat if not torch.is_tensor(flat[k])]
+    values = {}
+    if obj_keys:
+        if rank == 0 or not broadcast:
+            for k in obj_keys:
+                (idx, info), = chunks_of[k]
+                with open(os.path.join(checkpoint_id, info.relative_path), "rb") as f:
+                    f.seek(info.offset)
+                    values[k] = torch.load(io.BytesIO(f.read(info.length)), weights_only=True)
+        if broadcast and world > 1:
+            box = [values]
+            dist.broadcast_object_list(box, src=_global_rank(0, process_group), group=process_group)
+            values = box[0]
+    for k, v in values.items():
+        _set_path(resolved, mapping[k], v)
+    # Stateful objects
+    for key, v in state_dict.items():
+        if hasattr(v, "load_state_dict") and not torch.is_tensor(v):
+            v.load_state_dict(resolved[key])
+        else:
+            state_dict[key] = resolved[key]
+    if flat and any(torch.is_tensor(v) and v.is_cuda for v in flat.values()):
+        torch.cuda.current_stream().synchronize()
+    return state_dict
+
+
+def dest_is_cuda(batch) -> bool:
+    return any(b[0][0].is_cuda for b in batch)
+
+
+def _global_rank(group_rank: int, pg) -> int:
+    if pg is None:
+        return group_rank
+    return dist.get_global_rank(pg, group_rank)
+
+
+def _set_path(root, path, value):
+    cur = root
+    for p in path[:-1]:
+        cur = cur[p]
+    cur[path[-1]] = value

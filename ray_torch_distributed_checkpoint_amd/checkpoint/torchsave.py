@@ -152,7 +152,7 @@ def snapshot_tensors(tensors: list, stream=None) -> list:
 
 
 def submit_files(files: list, keepalive, nbytes: int, ready_event=None) -> SaveHandle:
-    """files: [(path, fsync, crc, records)] -> SaveHandle (non-blocking)."""
+    """files: [(path, fsync, crc, [(raw, records), ...])] -> SaveHandle (non-blocking)."""
     t0 = time.perf_counter()
     ev = 0
     if ready_event is not None:
@@ -191,7 +191,7 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
     stor = _storages_of(contig)
     nbytes = sum(s[1] for s in stor)
     recs = build_records(pkl, stor, prefix=os.path.splitext(os.path.basename(path))[0] or "archive")
-    h = submit_files([(path, fsync, crc, recs)], contig, nbytes, ready)
+    h = submit_files([(path, fsync, crc, [(False, recs)])], contig, nbytes, ready)
     if async_:
         return h
     h.wait()

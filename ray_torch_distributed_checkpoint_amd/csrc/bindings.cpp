@@ -263,11 +263,30 @@ static std::vector<Record> to_records(const py::list& recs) {
   return out;
 }
 
-static py::tuple plan_layout(const py::list& recs) {
-  auto r = to_records(recs);
-  uint64_t total = 0;
-  auto lay = rtdc_ckpt::plan_layout(r, &total);
-  return py::make_tuple(lay, total);
+// archive tuple: (raw: bool, records: list)
+static std::vector<rtdc_ckpt::Archive> to_archives(const py::list& arcs) {
+  std::vector<rtdc_ckpt::Archive> out;
+  for (auto item : arcs) {
+    auto t = item.cast<py::tuple>();
+    rtdc_ckpt::Archive a;
+    a.raw = t[0].cast<bool>();
+    a.recs = to_records(t[1].cast<py::list>());
+    out.push_back(std::move(a));
+  }
+  return out;
+}
+
+// -> (file_size, [(archive_base, archive_size, [(abs_data_offset, size), ...]), ...])
+static py::tuple plan_layout(const py::list& arcs) {
+  auto a = to_archives(arcs);
+  uint64_t total = rtdc_ckpt::layout_archives(a);
+  py::list out;
+  for (auto& x : a) {
+    py::list recs;
+    for (auto& r : x.recs) recs.append(py::make_tuple(x.base + r.data_off, rtdc_ckpt::rec_size(r)));
+    out.append(py::make_tuple(x.base, x.size, recs));
+  }
+  return py::make_tuple(total, out);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -292,7 +311,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("relu_dropout", &relu_dropout);
 
   m.def("have_gpu", &rtdc_ckpt::g_have_gpu);
-  m.def("plan_layout", &plan_layout, "zip layout: ([(data_offset, size)], total_bytes)");
+  m.def("plan_layout", &plan_layout, "file layout of a list of (raw, records) archives");
   m.def("crc32", [](py::bytes b) {
     std::string s = b;
     return (uint32_t)crc32(0L, (const Bytef*)s.data(), (uInt)s.size());
@@ -319,7 +338,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
               f->path = t[0].cast<std::string>();
               f->fsync_on = t[1].cast<bool>();
               f->crc_on = t[2].cast<bool>();
-              f->recs = to_records(t[3].cast<py::list>());
+              f->archives = to_archives(t[3].cast<py::list>());
               fj.push_back(f);
             }
             return e.submit(std::move(fj), reinterpret_cast<hipEvent_t>(ready_event));

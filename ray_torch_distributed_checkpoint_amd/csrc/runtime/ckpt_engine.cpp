@@ -234,19 +234,62 @@ class PinnedRing {
 // ------------------------------------------------------------------------------------------
 // Engine
 // ------------------------------------------------------------------------------------------
+// One file = a sequence of archives written back to back: a torch.save zip archive per tensor
+// item (the DCP `__r_i.distcp` layout: each item at a recorded (offset, length), readable by
+// `torch.load` on the slice), or a raw byte item (DCP BYTE_IO).  A `.pt` file is one archive.
+struct Archive {
+  std::vector<Record> recs;
+  bool raw = false;
+  uint64_t base = 0;      // file offset of the archive
+  uint64_t data_end = 0;  // archive-relative end of the last record (central dir starts here)
+  uint64_t size = 0;      // full archive size (incl. central directory)
+};
+
+static uint64_t cd_size(const std::vector<Record>& recs) {
+  uint64_t n = 22;
+  for (auto& r : recs) n += 46 + r.name.size();
+  return n;
+}
+
+// Assign archive bases and record offsets; returns the file size.
+static uint64_t layout_archives(std::vector<Archive>& arcs) {
+  uint64_t off = 0;
+  for (auto& a : arcs) {
+    a.base = off;
+    if (a.raw) {
+      uint64_t n = 0;
+      for (auto& r : a.recs) {
+        r.header_off = 0;
+        r.data_off = n;
+        r.extra_len = 0;
+        n += rec_size(r);
+      }
+      a.data_end = n;
+      a.size = n;
+    } else {
+      a.data_end = layout_records(a.recs, 0);
+      a.size = a.data_end + cd_size(a.recs);
+    }
+    off += a.size;
+  }
+  return off;
+}
+
 struct FileJob {
   std::string path;
-  std::vector<Record> recs;
+  std::vector<Archive> archives;
   int fd = -1;
   uint64_t total = 0;
   std::atomic<int> pending{0};
-  // per big-record ordered piece CRCs
-  std::map<int, std::vector<std::pair<uint32_t, uint64_t>>> piece_crc;  // rec -> (crc,len) by piece
+  // per big-record ordered piece CRCs, key = (archive << 24) | record
+  std::map<long long, std::vector<std::pair<uint32_t, uint64_t>>> piece_crc;
   std::mutex mu;
   bool fsync_on = true;
   bool crc_on = true;
   std::string error;
 };
+
+static inline long long rkey(size_t a, size_t r) { return ((long long)a << 24) | (long long)r; }
 
 struct SaveJob {
   int id;
@@ -291,21 +334,25 @@ class Engine {
     if (stream_) hipStreamDestroy(stream_);
   }
 
-  // files: list of (path, records, fsync, crc)
   int submit(std::vector<std::shared_ptr<FileJob>> files, hipEvent_t ready) {
     auto job = std::make_shared<SaveJob>();
     job->t_submit = now_s();
+    job->files = std::move(files);
+    job->files_left = (int)job->files.size();
+    job->ready = ready;
+    for (auto& f : job->files) {
+      f->total = layout_archives(f->archives);
+      for (auto& a : f->archives)
+        for (auto& r : a.recs) job->bytes += rec_size(r);
+    }
     {
       std::lock_guard<std::mutex> lk(jmu_);
       job->id = next_id_++;
       jobs_[job->id] = job;
     }
-    job->files = std::move(files);
-    job->files_left = (int)job->files.size();
-    job->ready = ready;
-    for (auto& f : job->files) {
-      f->total = layout_records(f->recs, 0);
-      for (auto& r : f->recs) job->bytes += rec_size(r);
+    if (job->files.empty()) {
+      finish_job(job);
+      return job->id;
     }
     {
       std::lock_guard<std::mutex> lk(qmu_);
@@ -336,8 +383,6 @@ class Engine {
     return {job->error, job->t_done - job->t_submit};
   }
 
-  std::vector<uint64_t> record_offsets(int /*unused*/) { return {}; }
-
   size_t slot_bytes() const { return ring_.slot_bytes(); }
   bool pinned() const { return ring_.pinned(); }
 
@@ -345,7 +390,8 @@ class Engine {
   struct WJob {
     std::shared_ptr<SaveJob> job;
     std::shared_ptr<FileJob> file;
-    int rec = -1, piece = -1;
+    long long key = -1;
+    int piece = -1;
     int slot = -1;
     const void* host = nullptr;  // direct host source (no slot)
     uint64_t len = 0, off = 0;
@@ -373,49 +419,54 @@ class Engine {
   }
 
   void run_job(std::shared_ptr<SaveJob> job) {
-    if (stream_ && job->ready) hipStreamWaitEvent(stream_, job->ready, 0);
     if (g_have_gpu()) hipSetDevice(device_);
+    if (stream_ && job->ready) hipStreamWaitEvent(stream_, job->ready, 0);
     const size_t S = ring_.slot_bytes();
     for (auto& f : job->files) {
       f->fd = ::open(f->path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
       if (f->fd < 0) throw std::runtime_error("open failed: " + f->path + ": " + strerror(errno));
-      // count pieces first so the finalizer knows when the file is complete
-      int pieces = 1;  // the small-records/headers write (done at finalize)
-      for (auto& r : f->recs)
-        if (r.src) pieces += (int)((r.nbytes + S - 1) / S);
+      int pieces = 1;  // the headers / small records / central directories (finalize)
+      for (auto& a : f->archives)
+        for (auto& r : a.recs)
+          if (r.src) pieces += (int)((r.nbytes + S - 1) / S);
       f->pending = pieces;
-      for (size_t ri = 0; ri < f->recs.size(); ++ri) {
-        auto& r = f->recs[ri];
-        if (!r.src) continue;
-        const int np = (int)((r.nbytes + S - 1) / S);
-        {
-          std::lock_guard<std::mutex> lk(f->mu);
-          f->piece_crc[(int)ri].assign(np, {0u, 0ull});
-        }
-        for (int p = 0; p < np; ++p) {
-          const uint64_t o = (uint64_t)p * S;
-          const uint64_t len = std::min<uint64_t>(S, r.nbytes - o);
-          WJob w;
-          w.job = job;
-          w.file = f;
-          w.rec = (int)ri;
-          w.piece = p;
-          w.len = len;
-          w.off = r.data_off + o;
-          if (r.on_device) {
-            const int s = ring_.acquire();
-            hipError_t e = hipMemcpyAsync(ring_.ptr(s), r.src + o, len, hipMemcpyDeviceToHost, stream_);
-            if (e != hipSuccess) throw std::runtime_error(std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
-            hipEventRecord(ring_.event(s), stream_);
-            w.slot = s;
-            w.wait_event = true;
-          } else {
-            w.host = r.src + o;
+      for (size_t ai = 0; ai < f->archives.size(); ++ai) {
+        auto& a = f->archives[ai];
+        for (size_t ri = 0; ri < a.recs.size(); ++ri) {
+          auto& r = a.recs[ri];
+          if (!r.src) continue;
+          const int np = (int)((r.nbytes + S - 1) / S);
+          {
+            std::lock_guard<std::mutex> lk(f->mu);
+            f->piece_crc[rkey(ai, ri)].assign(np, {0u, 0ull});
           }
-          push_write(std::move(w));
+          for (int p = 0; p < np; ++p) {
+            const uint64_t o = (uint64_t)p * S;
+            const uint64_t len = std::min<uint64_t>(S, r.nbytes - o);
+            WJob w;
+            w.job = job;
+            w.file = f;
+            w.key = rkey(ai, ri);
+            w.piece = p;
+            w.len = len;
+            w.off = a.base + r.data_off + o;
+            if (r.on_device) {
+              const int s = ring_.acquire();
+              hipError_t e = hipMemcpyAsync(ring_.ptr(s), r.src + o, len, hipMemcpyDeviceToHost, stream_);
+              if (e != hipSuccess) {
+                ring_.release(s);
+                throw std::runtime_error(std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+              }
+              hipEventRecord(ring_.event(s), stream_);
+              w.slot = s;
+              w.wait_event = true;
+            } else {
+              w.host = r.src + o;
+            }
+            push_write(std::move(w));
+          }
         }
       }
-      // header/small-record write job: runs after the data pieces (it needs their CRCs)
       WJob fin;
       fin.job = job;
       fin.file = f;
@@ -443,7 +494,7 @@ class Engine {
           if (wstop_) return;
           continue;
         }
-        // finalizers only after all data pieces of the file are written
+        // a file's finalizer runs only after all its data pieces are written
         auto it = wq_.begin();
         for (; it != wq_.end(); ++it) {
           if (!it->final_marker || it->file->pending.load() == 1) break;
@@ -470,10 +521,9 @@ class Engine {
           if (f.crc_on) c = (uint32_t)crc32(0L, (const Bytef*)src, (uInt)w.len);
           pwrite_all(f.fd, src, w.len, w.off);
           if (w.slot >= 0) ring_.release(w.slot);
-          {
-            std::lock_guard<std::mutex> lk(f.mu);
-            f.piece_crc[w.rec][w.piece] = {c, w.len};
-          }
+          w.slot = -1;
+          std::lock_guard<std::mutex> lk(f.mu);
+          f.piece_crc[w.key][w.piece] = {c, w.len};
         }
       } catch (std::exception& e) {
         if (w.slot >= 0) ring_.release(w.slot);
@@ -489,32 +539,38 @@ class Engine {
 
   void finalize_file(FileJob& f) {
     if (!f.error.empty()) throw std::runtime_error(f.error);
-    for (size_t ri = 0; ri < f.recs.size(); ++ri) {
-      auto& r = f.recs[ri];
-      if (r.src) {
-        uint32_t c = 0;
-        if (f.crc_on) {
-          auto& pcs = f.piece_crc[(int)ri];
-          bool first = true;
-          for (auto& pc : pcs) {
-            c = first ? pc.first : (uint32_t)crc32_combine(c, pc.first, (z_off_t)pc.second);
-            first = false;
+    for (size_t ai = 0; ai < f.archives.size(); ++ai) {
+      auto& a = f.archives[ai];
+      for (size_t ri = 0; ri < a.recs.size(); ++ri) {
+        auto& r = a.recs[ri];
+        if (r.src) {
+          uint32_t c = 0;
+          if (f.crc_on) {
+            auto& pcs = f.piece_crc[rkey(ai, ri)];
+            bool first = true;
+            for (auto& pc : pcs) {
+              c = first ? pc.first : (uint32_t)crc32_combine(c, pc.first, (z_off_t)pc.second);
+              first = false;
+            }
           }
-          if (pcs.empty()) c = 0;
+          r.crc = c;
+        } else {
+          r.crc = f.crc_on ? (uint32_t)crc32(0L, (const Bytef*)r.inline_data.data(), (uInt)r.inline_data.size()) : 0;
         }
-        r.crc = c;
-      } else {
-        r.crc = f.crc_on ? (uint32_t)crc32(0L, (const Bytef*)r.inline_data.data(), (uInt)r.inline_data.size()) : 0;
+      }
+      for (auto& r : a.recs) {
+        if (!a.raw) {
+          std::string h = local_header(r, rec_size(r));
+          pwrite_all(f.fd, h.data(), h.size(), a.base + r.header_off);
+        }
+        if (!r.src && !r.inline_data.empty())
+          pwrite_all(f.fd, r.inline_data.data(), r.inline_data.size(), a.base + r.data_off);
+      }
+      if (!a.raw) {
+        std::string cd = central_dir(a.recs, a.data_end);
+        pwrite_all(f.fd, cd.data(), cd.size(), a.base + a.data_end);
       }
     }
-    // headers + inline records
-    for (auto& r : f.recs) {
-      std::string h = local_header(r, rec_size(r));
-      pwrite_all(f.fd, h.data(), h.size(), r.header_off);
-      if (!r.src && !r.inline_data.empty()) pwrite_all(f.fd, r.inline_data.data(), r.inline_data.size(), r.data_off);
-    }
-    std::string cd = central_dir(f.recs, f.total);
-    pwrite_all(f.fd, cd.data(), cd.size(), f.total);
     if (f.fsync_on) ::fsync(f.fd);
     ::close(f.fd);
     f.fd = -1;
@@ -550,14 +606,6 @@ class Engine {
   std::atomic<bool> stop_{false};
   bool wstop_ = false;
 };
-
-// Layout helper for Python: offsets a file would get (so DCP metadata can be built up front).
-static std::vector<std::pair<uint64_t, uint64_t>> plan_layout(std::vector<Record>& recs, uint64_t* total) {
-  *total = layout_records(recs, 0);
-  std::vector<std::pair<uint64_t, uint64_t>> out;
-  for (auto& r : recs) out.push_back({r.data_off, rec_size(r)});
-  return out;
-}
 
 // Parallel pread of many (offset, len, dst) ranges of one file.
 static void read_ranges(const std::string& path, const std::vector<uint64_t>& offs,

@@ -1,0 +1,85 @@
+"""nn.Module wrappers over the native ops.  Parameters are fp32 masters; GPU compute is bf16
+(or exact fp32 for fp32 activations) on the hand-written gfx950 kernels."""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class Linear(nn.Module):
+    """y = act(x W^T + b); `relu=True` fuses the ReLU into the GEMM epilogue."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, relu: bool = False):
+        super().__init__()
+        self.in_features, self.out_features, self.relu = in_features, out_features, relu
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # nn.Linear's default init
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            bound = 1 / math.sqrt(self.in_features) if self.in_features > 0 else 0
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x, residual=None):
+        return ops.linear(x, self.weight, self.bias, relu=self.relu, residual=residual)
+
+    def extra_repr(self):
+        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}, fused_relu={self.relu}"
+
+
+class FusedReLU(nn.Module):
+    """Placeholder keeping nn.Sequential indices (and state_dict keys) of a ReLU that was
+    fused into the preceding Linear's epilogue."""
+
+    def forward(self, x):
+        return x
+
+    def extra_repr(self):
+        return "fused into previous Linear"
+
+
+class Dropout(nn.Module):
+    def __init__(self, p: float = 0.5):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        return ops.dropout(x, self.p, self.training)
+
+    def extra_repr(self):
+        return f"p={self.p}"
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.bias = nn.Parameter(torch.zeros(dim))
+
+    def forward(self, x):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return ops.rms_norm(x, self.weight, self.eps)
+
+
+class Embedding(nn.Module):
+    def __init__(self, num: int, dim: int):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(num, dim))
+        nn.init.normal_(self.weight, std=0.02)
