@@ -1,0 +1,81 @@
+"""GEMM microbenchmark: native gfx950 MFMA kernel vs torch.matmul (hipBLASLt) on the GPT-2
+shapes, all three nn.Linear layouts.  Random operands (cdna_hip_programming.md §5.4 rule 25),
+interleaved repetitions in one process (rule 24).
+
+    python benchmarks/gemm_bench.py [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from ray_torch_distributed_checkpoint_amd.ops import gemm as G  # noqa: E402
+
+SHAPES = [  # (name, M tokens, in K, out N)
+    ("qkv", 16384, 768, 2304),
+    ("attn_proj", 16384, 768, 768),
+    ("fc", 16384, 768, 3072),
+    ("mlp_proj", 16384, 3072, 768),
+    ("lm_head", 16384, 768, 50304),
+    ("sq4096", 4096, 4096, 4096),
+]
+
+
+def timeit(fn, reps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--sweep", action="store_true", help="also time every forced tile configuration (fwd)")
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    res = []
+    for name, M, K, N in SHAPES:
+        if args.only and args.only != name:
+            continue
+        x = torch.randn(M, K, device="cuda").bfloat16()
+        w = torch.randn(N, K, device="cuda").bfloat16()
+        dy = torch.randn(M, N, device="cuda").bfloat16()
+        flops = 2.0 * M * N * K
+        row = {"shape": name, "M": M, "K": K, "N": N}
+        for lay, ours, ref in [
+            ("fwd", lambda: G.linear_fwd(x, w), lambda: x @ w.t()),
+            ("dgrad", lambda: G.linear_dgrad(dy, w), lambda: dy @ w),
+            ("wgrad", lambda: G.linear_wgrad(dy, x), lambda: (dy.t() @ x)),
+        ]:
+            t_o = min(timeit(ours, args.reps) for _ in range(3))
+            t_r = min(timeit(ref, args.reps) for _ in range(3))
+            row[lay] = {"ours_TF": round(flops / t_o / 1e12, 1), "hipblaslt_TF": round(flops / t_r / 1e12, 1),
+                        "ours_us": round(t_o * 1e6, 1), "hipblaslt_us": round(t_r * 1e6, 1)}
+        if args.sweep:
+            for cfg in range(4):
+                y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+                t = min(timeit(lambda: G.gemm_bf16(x, w, y, M, N, K, K, K, N, tile_cfg=cfg), args.reps) for _ in range(3))
+                row[f"fwd_cfg{cfg}_TF"] = round(flops / t / 1e12, 1)
+        # correctness spot check (fwd)
+        ref = (x.float() @ w.float().t())
+        err = (G.linear_fwd(x, w).float() - ref).abs().max().item() / ref.abs().max().item()
+        row["fwd_rel_err"] = err
+        res.append(row)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

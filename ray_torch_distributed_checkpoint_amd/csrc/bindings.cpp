@@ -73,7 +73,8 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
                       c10::optional<Tensor> aux_in, c10::optional<Tensor> aux_out, int64_t M, int64_t N,
                       int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool a_kmajor, bool b_kmajor,
                       int64_t batch, int64_t batch_inner, int64_t sA0, int64_t sA1, int64_t sB0, int64_t sB1,
-                      int64_t sC0, int64_t sC1, double alpha, double beta, int64_t act, int64_t causal) {
+                      int64_t sC0, int64_t sC1, double alpha, double beta, int64_t act, int64_t causal,
+                      c10::optional<Tensor> ws, int64_t tile_cfg) {
   check_dev(A, "A");
   check_dev(B, "B");
   check_dev(C, "C");
@@ -96,6 +97,9 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
   a.batch_inner = (int)std::max<int64_t>(1, batch_inner);
   a.alpha = (float)alpha; a.beta = (float)beta;
   a.act = (int)act; a.causal = (int)causal;
+  a.ws = ws.has_value() ? ws->data_ptr<float>() : nullptr;
+  a.ws_elems = ws.has_value() ? ws->numel() : 0;
+  a.tile_cfg = (int)tile_cfg;
   TORCH_CHECK(!(act == 2) || a.aux_out, "gelu forward needs aux_out");
   TORCH_CHECK(!(act == 3 || act == 4) || a.aux_in, "activation backward needs aux_in");
   check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream()),

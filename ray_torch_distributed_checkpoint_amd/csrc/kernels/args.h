@@ -21,6 +21,11 @@ struct GemmArgs {
   int act;        // 0 none, 1 relu, 2 gelu_tanh, 3 *gelu'(aux_in), 4 *relu'(aux_in)
   int causal;     // 0 none, 1 skip tiles with n0 > m_last, 2 k < m0+BM, 3 k >= m0
   int bias_type;  // 0 none, 1 bf16, 2 fp32
+  // split-K (plain epilogue only): fp32 partial slabs [splitk][M][N] reduced by a second kernel
+  float* ws;
+  long long ws_elems;
+  int splitk;     // set by the launcher
+  int tile_cfg;   // -1 = auto; else force a tile configuration (benchmarks)
 };
 
 // fp32 MFMA GEMM (gemm_f32.hip)

@@ -12,12 +12,22 @@
 // LDS exactly as they sit in HBM (coalesced 16-B global_load_lds) and the k-strided MFMA
 // fragments are read back with the gfx950 transposing LDS read ds_read_b64_tr_b16.
 //
-// Geometry: 128x128 output tile, BK = 64, 256 threads = 4 waves (2x2), each wave 64x64 =
-// 4x4 v_mfma_f32_16x16x32_bf16 tiles.  LDS: 2 buffers x (A 16 KiB + B 16 KiB) = 64 KiB.
+// Tile configurations (BM x BN, waves WM x WN; BK = 64; v_mfma_f32_16x16x32_bf16):
+//   0: 128x128, 2x2 waves (256 threads), 64 KiB LDS, 2 blocks/CU    - small / batched GEMMs
+//   1: 256x128, 4x2 waves (512 threads), 96 KiB LDS                  - tall GEMMs
+//   2: 128x256, 2x4 waves (512 threads), 96 KiB LDS                  - wide GEMMs
+//   3: 256x256, 2x4 waves (512 threads), 128 KiB LDS, 128x64 / wave  - large GEMMs
+// chosen per shape by the launcher so the grid fills the 256 CUs in whole waves (a GEMM with
+// 192 tiles leaves 25% of the chip idle) while keeping the MFMA:LDS-byte ratio high.
 // Staging: global_load_lds_dwordx4 (1 KiB per wave-instruction, LDS image lane-linear), the
 // bank-conflict swizzle applied on the SOURCE address and on the read (cdna_hip_programming.md
-// §5.4 rule 21).  The MFMA is issued with the operands swapped (B-data as MFMA "A") so each
-// lane's accumulator holds 4 consecutive n of one output row: 8-16 B vector stores.
+// §5.4 rule 21); per-lane source pointers are computed once and advanced by k per stage.
+// The MFMA is issued with the operands swapped (B-data as MFMA "A") so each lane's
+// accumulator holds 4 consecutive n of one output row: 8-16 B vector stores.
+//
+// Split-K (wgrad: output 768x768..3072x768 but K = B*T = 16384 -> only 36..144 tiles): the
+// K range is cut into `splitk` slices over blockIdx.y, each writing an fp32 partial slab; a
+// second kernel sums the slabs in a fixed order (bitwise reproducible, no float atomics).
 //
 // Batching (attention) uses blockIdx.z with a two-level (outer, inner) stride per operand;
 // causal modes skip/limit work for the triangular attention products.
@@ -27,52 +37,76 @@
 namespace rtdc {
 
 namespace gemm {
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = 128 * BK * 2;  // 16 KiB per operand tile
+constexpr int BK = 64;
 }
 
+template <int BM_, int BN_, int WM_, int WN_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // MFMA tiles per wave
+  static constexpr int A_BYTES = BM * gemm::BK * 2, B_BYTES = BN * gemm::BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "pieces must split evenly over waves");
+};
+
 // ---- LDS image helpers ----------------------------------------------------------------
-// K-major image: 128 rows x 128 B (64 bf16 of k).  16-B chunk c of row r lives at
-// physical chunk c ^ ((r >> 1) & 7): a ds_read_b128 lane group (16 distinct rows, same
-// logical chunk) then touches 16 distinct 16-B slots of the 256-B bank row.
+// K-major image: ROWS rows x 128 B (64 bf16 of k).  16-B chunk c of row r lives at physical
+// chunk c ^ ((r >> 1) & 7): a ds_read_b128 lane group (16 distinct rows, same logical chunk)
+// then touches 16 distinct 16-B slots of the 256-B bank row.
 __device__ __forceinline__ int kmaj_off(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
-// MN-major image: 64 k-rows x 256 B (128 bf16 of m or n).  Chunk c of k-row kr lives at
-// c ^ f(kr); a 32-lane half of ds_read_b64_tr_b16 reads 8 k-rows x 2 chunks -> 16 slots.
+// MN-major image: 64 k-rows x (2*ROWS) B.  Chunk c of k-row kr lives at c ^ f(kr) (f < 16
+// keeps it in the same 256-B half); a 32-lane half of ds_read_b64_tr_b16 reads 8 k-rows x 2
+// chunks -> 16 distinct 16-B bank slots (k-rows start on the same bank: stride 256/512 B).
 __device__ __forceinline__ int mnmaj_swz(int kr) {
   return ((kr & 3) | (((kr >> 3) & 1) << 2)) << 1;
 }
 
-// Issue the global->LDS copy of one operand tile (rows [r0, r0+128), k [k0, k0+64)).
-template <bool KMAJOR>
-__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ X, int ld, int rows,
-                                           int r0, int k0, char* lds_tile, int wave, int lane) {
+// Per-lane global sources of one operand tile, computed once per block.
+template <bool KMAJOR, int ROWS, int NW>
+struct Stager {
+  static constexpr int PIECES = ROWS / 8;  // 1 KiB pieces per 64-deep k tile
+  static constexpr int PPW = PIECES / NW;
+  const bf16_t* src[PPW];
+  long long kmul;  // element stride per unit of k
+
+  __device__ __forceinline__ void init(const bf16_t* X, int ld, int rows, int r0, int wave, int lane) {
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii) {
-    const int piece = wave * 4 + ii;  // 16 pieces of 1 KiB
-    const bf16_t* src;
-    if constexpr (KMAJOR) {
-      const int row = piece * 8 + (lane >> 3);
-      const int pchunk = lane & 7;
-      const int lchunk = pchunk ^ ((row >> 1) & 7);
-      int gr = r0 + row;
-      gr = gr < rows ? gr : rows - 1;
-      src = X + (long long)gr * ld + k0 + lchunk * 8;
-    } else {
-      const int kr = piece * 4 + (lane >> 4);
-      const int pchunk = lane & 15;
-      const int lchunk = pchunk ^ mnmaj_swz(kr);
-      int gc = r0 + lchunk * 8;
-      gc = gc < rows ? gc : rows - 8;
-      src = X + (long long)(k0 + kr) * ld + gc;
+    for (int ii = 0; ii < PPW; ++ii) {
+      const int piece = wave * PPW + ii;
+      if constexpr (KMAJOR) {
+        const int row = piece * 8 + (lane >> 3);
+        const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
+        int gr = r0 + row;
+        gr = gr < rows ? gr : rows - 1;
+        src[ii] = X + (long long)gr * ld + lchunk * 8;
+      } else {
+        constexpr int CPR = ROWS / 8;     // 16-B chunks per k-row
+        constexpr int KRP = 1024 / (ROWS * 2);  // k-rows per piece
+        const int kr = piece * KRP + lane / CPR;
+        const int lchunk = (lane % CPR) ^ mnmaj_swz(kr);
+        int gc = r0 + lchunk * 8;
+        gc = gc < rows ? gc : rows - 8;
+        src[ii] = X + (long long)kr * ld + gc;
+      }
     }
-    __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+    kmul = KMAJOR ? 1 : ld;
   }
-}
+
+  __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
+    const long long koff = (long long)k0 * kmul;
+#pragma unroll
+    for (int ii = 0; ii < PPW; ++ii) {
+      const int piece = wave * PPW + ii;
+      __builtin_amdgcn_global_load_lds((const void*)(src[ii] + koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+    }
+  }
+};
 
 // Fragment for v_mfma_f32_16x16x32_bf16: lane l holds X(row = R0 + (l&15), k = ks*32 + 8(l>>4) + j).
-template <bool KMAJOR>
+template <bool KMAJOR, int ROWS>
 __device__ __forceinline__ bf16x8 load_frag(const char* lds_tile, int R0, int ks, int lane) {
   if constexpr (KMAJOR) {
     const int row = R0 + (lane & 15);
@@ -85,7 +119,7 @@ __device__ __forceinline__ bf16x8 load_frag(const char* lds_tile, int R0, int ks
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int kr = ks * 32 + 8 * g + 4 * h + q;
-      const int off = kr * 256 + ((c ^ mnmaj_swz(kr)) << 4) + ((p & 1) << 3);
+      const int off = kr * (ROWS * 2) + ((c ^ mnmaj_swz(kr)) << 4) + ((p & 1) << 3);
       v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) bf16x4*)(lds_tile + off));
     }
@@ -122,14 +156,15 @@ __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
   *(uint2*)p = x;
 }
 
-template <bool AK, bool BKM, typename OutT>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
+template <class CFG, bool AK, bool BKM, typename OutT>
+__global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
   using namespace gemm;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  constexpr int BM = CFG::BM, BN = CFG::BN, TM = CFG::TM, TN = CFG::TN, WN = CFG::WN, NW = CFG::NW;
+  __shared__ __attribute__((aligned(16))) char smem[2 * CFG::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 64x64 each
+  const int wm = wave / WN, wn = wave % WN;
 
   // XCD-aware, bijective remap of the flat tile id (cdna_hip_programming.md §5, T1) followed
   // by GROUP_M super-rows so consecutive tiles on one XCD share A row-panels in its L2.
@@ -160,61 +195,96 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
   int kb = 0, ke = a.K;
   if (a.causal == 2) ke = min(a.K, m0 + BM);
   if (a.causal == 3) kb = (m0 / BK) * BK;
+  if (a.splitk > 1) {
+    const int ktiles = (ke - kb) / BK;
+    const int per = (ktiles + a.splitk - 1) / a.splitk;
+    const int s = blockIdx.y;
+    const int k_lo = kb + s * per * BK;
+    ke = min(ke, k_lo + per * BK);
+    kb = k_lo;
+  }
   const int nt = ke > kb ? (ke - kb) / BK : 0;
 
-  f32x4 acc[4][4];
+  f32x4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // buffer b: A tile at smem + 2*b*TILE_BYTES, B tile right after it
-#define BUF_A(b) (smem + (b) * 2 * TILE_BYTES)
-#define BUF_B(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
+  Stager<AK, BM, NW> sa;
+  Stager<BKM, BN, NW> sb;
+  sa.init(A, a.lda, a.M, m0, wave, lane);
+  sb.init(B, a.ldb, a.N, n0, wave, lane);
+
+  // stage s: A tile at smem + s*STAGE, B tile right after it
+#define BUF_A(s) (smem + (s) * CFG::STAGE)
+#define BUF_B(s) (smem + (s) * CFG::STAGE + CFG::A_BYTES)
 
   if (nt > 0) {
-    stage_tile<AK>(A, a.lda, a.M, m0, kb, BUF_A(0), wave, lane);
-    stage_tile<BKM>(B, a.ldb, a.N, n0, kb, BUF_B(0), wave, lane);
+    sa.issue(kb, BUF_A(0), wave);
+    sb.issue(kb, BUF_B(0), wave);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     if (t + 1 < nt) {
-      stage_tile<AK>(A, a.lda, a.M, m0, kb + (t + 1) * BK, BUF_A(cur ^ 1), wave, lane);
-      stage_tile<BKM>(B, a.ldb, a.N, n0, kb + (t + 1) * BK, BUF_B(cur ^ 1), wave, lane);
+      sa.issue(kb + (t + 1) * BK, BUF_A(cur ^ 1), wave);
+      sb.issue(kb + (t + 1) * BK, BUF_B(cur ^ 1), wave);
     }
     const char* tA = BUF_A(cur);
     const char* tB = BUF_B(cur);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[4], fb[4];
+      bf16x8 fa[TM], fb[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = load_frag<AK>(tA, wm * 64 + i * 16, ks, lane);
+      for (int i = 0; i < TM; ++i) fa[i] = load_frag<AK, BM>(tA, wm * (TM * 16) + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = load_frag<BKM>(tB, wn * 64 + j * 16, ks, lane);
+      for (int j = 0; j < TN; ++j) fb[j] = load_frag<BKM, BN>(tB, wn * (TN * 16) + j * 16, ks, lane);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-
 #undef BUF_A
 #undef BUF_B
+
+  if (a.splitk > 1) {
+    // raw fp32 partial slab (alpha applied); epilogue happens in the reduce kernel
+    float* W = a.ws + (long long)blockIdx.y * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * (TN * 16) + j * 16 + 4 * (lane >> 4);
+        if (n >= a.N) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha;
+        store4<float>(W + (long long)m * a.N + n, v);
+      }
+    }
+    return;
+  }
+
   // ---- epilogue: lane holds C[m][n..n+3] ----
   OutT* C = (OutT*)a.C + coff;
   const OutT* Cin = a.Cin ? (const OutT*)a.Cin + coff : nullptr;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
     if (m >= a.M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (TN * 16) + j * 16 + 4 * (lane >> 4);
       if (n >= a.N) continue;
       float v[4];
 #pragma unroll
@@ -256,28 +326,117 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
   }
 }
 
+// out[m][n] = sum_s ws[s][m][n] (+ beta * Cin[m][n]); fixed slice order.
+template <typename OutT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                           OutT* C, const OutT* Cin, int ldc, float beta) {
+  const long long total4 = (long long)M * N / 4;
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < total4; q += (long long)gridDim.x * 256) {
+    const long long e = q * 4;
+    const int m = (int)(e / N), n = (int)(e % N);
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      f32x4 x = *(const f32x4*)(ws + (long long)s * M * N + e);
+      v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
+    }
+    const long long off = (long long)m * ldc + n;
+    if (Cin && beta != 0.f) {
+      float c[4];
+      load4<OutT>(Cin + off, c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += beta * c[r];
+    }
+    store4<OutT>(C + off, v);
+  }
+}
+
+using Cfg128x128 = TileCfg<128, 128, 2, 2>;
+using Cfg256x128 = TileCfg<256, 128, 4, 2>;
+using Cfg128x256 = TileCfg<128, 256, 2, 4>;
+using Cfg256x256 = TileCfg<256, 256, 2, 4>;
+
+template <class CFG>
+static inline long long ntiles(const GemmArgs& a) {
+  return (long long)((a.M + CFG::BM - 1) / CFG::BM) * ((a.N + CFG::BN - 1) / CFG::BN);
+}
+
+template <class CFG, bool AK, bool BKM, typename OutT>
+static void launch_cfg(const GemmArgs& a, int batch, hipStream_t st) {
+  dim3 grid((unsigned)ntiles<CFG>(a), a.splitk > 1 ? a.splitk : 1, batch), block(CFG::NT);
+  hipLaunchKernelGGL((gemm_bf16_kernel<CFG, AK, BKM, OutT>), grid, block, 0, st, a);
+}
+
+template <bool AK, bool BKM, typename OutT>
+static void launch_layout(const GemmArgs& a, int cfg, int batch, hipStream_t st) {
+  switch (cfg) {
+    case 1: launch_cfg<Cfg256x128, AK, BKM, OutT>(a, batch, st); break;
+    case 2: launch_cfg<Cfg128x256, AK, BKM, OutT>(a, batch, st); break;
+    case 3: launch_cfg<Cfg256x256, AK, BKM, OutT>(a, batch, st); break;
+    default: launch_cfg<Cfg128x128, AK, BKM, OutT>(a, batch, st); break;
+  }
+}
+
 }  // namespace rtdc
 
 using namespace rtdc;
 
-extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32,
-                              int batch, hipStream_t stream) {
-  const GemmArgs& a = *args;
+// Choose the tile configuration: the largest tile whose grid still fills the chip in whole
+// (or >= 90%-used) waves of 256 CUs.
+static int pick_cfg(const GemmArgs& a, int batch) {
+  if (a.tile_cfg >= 0) return a.tile_cfg;
+  if (batch > 1 || a.causal != 0 || a.M < 256 || a.N < 256) return 0;
+  auto eff = [](long long tiles) {
+    const long long waves = (tiles + 255) / 256;
+    return (double)tiles / (double)(waves * 256);
+  };
+  // Measured (benchmarks/gemm_bench.py --sweep, MI355X): with the 2-stage loop the 256-wide
+  // tiles only win when the per-tile prologue/epilogue is amortised - long K or a huge
+  // output (LM head 16384x50304: 749 vs 646 TF); at K = 768 the 128x128 tile is 10-25 %
+  // faster (qkv 743 vs 586 TF).
+  const long long t3 = ntiles<Cfg256x256>(a);
+  const bool big = a.K >= 4096 || (long long)a.M * a.N >= (1LL << 28);
+  if (big && t3 >= 256 && eff(t3) >= 0.85) return 3;
+  return 0;
+}
+
+extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
+                              hipStream_t stream) {
+  GemmArgs a = *args;
   if (a.K % gemm::BK != 0 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
-  const int tiles = ((a.M + gemm::BM - 1) / gemm::BM) * ((a.N + gemm::BN - 1) / gemm::BN);
-  dim3 grid(tiles, 1, batch), block(gemm::NT);
-#define LAUNCH(AK, BKM, T) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, T>), grid, block, 0, stream, a)
-  if (out_fp32) {
-    if (a_kmajor && b_kmajor) LAUNCH(true, true, float);
-    else if (a_kmajor && !b_kmajor) LAUNCH(true, false, float);
-    else if (!a_kmajor && !b_kmajor) LAUNCH(false, false, float);
-    else LAUNCH(false, true, float);
-  } else {
-    if (a_kmajor && b_kmajor) LAUNCH(true, true, bf16_t);
-    else if (a_kmajor && !b_kmajor) LAUNCH(true, false, bf16_t);
-    else if (!a_kmajor && !b_kmajor) LAUNCH(false, false, bf16_t);
-    else LAUNCH(false, true, bf16_t);
+  const int cfg = pick_cfg(a, batch);
+  a.splitk = 1;
+  // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
+  const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
+  long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
+                  : cfg == 2 ? ntiles<Cfg128x256>(a) : ntiles<Cfg128x128>(a);
+  const int ktiles = a.K / gemm::BK;
+  if (plain && a.ws && tiles < 200 && ktiles >= 32) {
+    int s = (int)((256 * 2 + tiles - 1) / tiles);  // aim at ~2 blocks per CU
+    s = s > 16 ? 16 : s;
+    while (s > 1 && (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems)) --s;
+    a.splitk = s;
   }
-#undef LAUNCH
+  if (out_fp32) {
+    if (a_kmajor && b_kmajor) launch_layout<true, true, float>(a, cfg, batch, stream);
+    else if (a_kmajor && !b_kmajor) launch_layout<true, false, float>(a, cfg, batch, stream);
+    else if (!a_kmajor && !b_kmajor) launch_layout<false, false, float>(a, cfg, batch, stream);
+    else launch_layout<false, true, float>(a, cfg, batch, stream);
+  } else {
+    if (a_kmajor && b_kmajor) launch_layout<true, true, bf16_t>(a, cfg, batch, stream);
+    else if (a_kmajor && !b_kmajor) launch_layout<true, false, bf16_t>(a, cfg, batch, stream);
+    else if (!a_kmajor && !b_kmajor) launch_layout<false, false, bf16_t>(a, cfg, batch, stream);
+    else launch_layout<false, true, bf16_t>(a, cfg, batch, stream);
+  }
+  if (a.splitk > 1) {
+    long long q = (long long)a.M * a.N / 4;
+    long long blocks = (q + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (out_fp32)
+      hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws,
+                         a.splitk, a.M, a.N, (float*)a.C, (const float*)a.Cin, a.ldc, a.beta);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws,
+                         a.splitk, a.M, a.N, (bf16_t*)a.C, (const bf16_t*)a.Cin, a.ldc, a.beta);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -15,6 +15,8 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
 CAUSAL_NONE, CAUSAL_SKIP_UPPER, CAUSAL_K_UPTO_M, CAUSAL_K_FROM_M = 0, 1, 2, 3
 
 _COLSUM_BLOCKS = 128
+SPLITK_MAX_OUT = 200 * 128 * 128  # outputs that fill < 200 tiles of 128x128
+SPLITK_WS_ELEMS = 48 << 20       # 192 MiB fp32 slab workspace cap
 _ws_cache: dict = {}
 
 
@@ -30,10 +32,15 @@ def workspace(device, numel: int, tag: str = "ws") -> torch.Tensor:
 
 def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, Cin=None, bias=None,
               aux_in=None, aux_out=None, alpha=1.0, beta=0.0, act=ACT_NONE, causal=CAUSAL_NONE,
-              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0)):
+              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0), tile_cfg=-1):
     sA0, sA1, sB0, sB1, sC0, sC1 = strides
+    ws = None
+    if act == ACT_NONE and bias is None and causal == CAUSAL_NONE and batch == 1 and M * N <= SPLITK_MAX_OUT:
+        # split-K slabs for long-K / small-output GEMMs (weight gradients); the launcher decides
+        ws = workspace(C.device, min(16 * M * N, SPLITK_WS_ELEMS), "splitk")
     gpu_ext().gemm_bf16(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
-                        batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act, causal)
+                        batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act, causal,
+                        ws, tile_cfg)
     return C
 
 

@@ -76,6 +76,20 @@ class Checkpoint:
         self.filesystem = None
         self._pending = None
 
+    @classmethod
+    def from_async_save(cls, handle) -> "Checkpoint":
+        """Wrap an in-flight `checkpoint.dcp.async_save` handle; `report()` commits it in the
+        background once every rank's shard is durable (rank 0 writes `.metadata`)."""
+        c = cls(handle.checkpoint_id)
+        c._pending = handle
+        c._handle = handle
+        return c
+
+    def _finish(self):
+        h = getattr(self, "_handle", None)
+        if h is not None:
+            h._finish()
+
     def __repr__(self):
         return f"Checkpoint(filesystem=local, path={self.path})"
 

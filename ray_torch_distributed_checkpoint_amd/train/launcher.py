@@ -68,6 +68,13 @@ class WorkerGroup:
                 "RTDC_STORE_PORT": str(self.port), "RTDC_ATTEMPT": str(attempt), "RTDC_PAYLOAD": payload_path,
             })
             env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            # workers import the user's modules (cloudpickle pickles module functions by
+            # reference) and this package exactly as the driver does
+            pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            paths = [pkg_root, os.getcwd()] + [p for p in sys.path if p]
+            if env.get("PYTHONPATH"):
+                paths.append(env["PYTHONPATH"])
+            env["PYTHONPATH"] = os.pathsep.join(dict.fromkeys(paths))
             if extra_env:
                 env.update(extra_env)
             cmd = [sys.executable, "-u", "-m", "ray_torch_distributed_checkpoint_amd.train._worker"]

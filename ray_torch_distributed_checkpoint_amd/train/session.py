@@ -120,23 +120,35 @@ class _Session:
     def report(self, metrics: dict, checkpoint: Checkpoint | None = None):
         if self._commit_err:
             raise self._commit_err
-        idx = self.next_index if checkpoint is not None else None
         rank = self.ctx.world_rank
+        n = self.n_reports
+        key = f"s{self.ctx.attempt}/r{n}"
+        stage = storage.staging_dir(self.ctx.trial_dir, self.next_index)
+        is_async = checkpoint is not None and (
+            checkpoint._pending is not None or os.path.abspath(checkpoint.path) == os.path.abspath(stage))
         if checkpoint is not None:
+            self.store.add(key + "/ck", 1)
+        if is_async:
+            self.store.add(key + "/async", 1)
+        self.barrier.wait(f"r{n}a")
+        any_ck = self.store.add(key + "/ck", 0) > 0
+        any_async = self.store.add(key + "/async", 0) > 0
+        idx = None
+        if any_ck:
+            idx = self.next_index
             self.next_index += 1
-            stage = storage.staging_dir(self.ctx.trial_dir, idx)
-            if checkpoint._pending is not None or os.path.abspath(checkpoint.path) == os.path.abspath(stage):
-                # async / in-place checkpoint: commit in the background once durable
+            if any_async:
+                # async / in-place shards: commit in the background once every rank is durable
                 self._enqueue_commit(idx, checkpoint, metrics)
-                checkpoint = None
             else:
-                if rank == 0:
+                if rank == 0 and checkpoint is not None:
                     storage.merge_into(checkpoint.path, stage, overwrite=True)
-                self.barrier.wait(f"r{self.n_reports}a")
-                if rank != 0:
+                self.barrier.wait(f"r{n}b")
+                if rank != 0 and checkpoint is not None:
                     storage.merge_into(checkpoint.path, stage, overwrite=False)
-                self.barrier.wait(f"r{self.n_reports}b")
+                self.barrier.wait(f"r{n}c")
                 if rank == 0:
+                    os.makedirs(stage, exist_ok=True)
                     path = storage.commit(self.ctx.trial_dir, idx)
                     self.logger.register(idx, path, dict(metrics))
         row = None
@@ -144,7 +156,7 @@ class _Session:
             row = self.logger.log(metrics, idx)
             self.last_metrics = row
             self._publish(row, None if idx is None else storage.final_dir(self.ctx.trial_dir, idx))
-        self.barrier.wait(f"r{self.n_reports}c")
+        self.barrier.wait(f"r{n}d")
         self.n_reports += 1
 
     def _publish(self, row, ckpt_path):
@@ -166,7 +178,8 @@ class _Session:
                 return
             idx, ck, metrics = item
             try:
-                ck.wait()  # this rank's shard files durable
+                if ck is not None:
+                    ck.wait()  # this rank's shard files durable
                 key = f"s{self.ctx.attempt}/commit/{idx}"
                 self.store.add(key, 1)
                 if self.ctx.world_rank == 0:
@@ -175,8 +188,9 @@ class _Session:
                         if time.time() - t0 > 3600:
                             raise TimeoutError("async checkpoint commit barrier timed out")
                         time.sleep(0.002)
-                    if hasattr(ck, "_finish"):
+                    if ck is not None and hasattr(ck, "_finish"):
                         ck._finish()  # rank-0 metadata write (DCP .metadata)
+                    os.makedirs(storage.staging_dir(self.ctx.trial_dir, idx), exist_ok=True)
                     path = storage.commit(self.ctx.trial_dir, idx)
                     self.logger.register(idx, path, metrics)
                     self.store.set(f"s{self.ctx.attempt}/committed/{idx}", path)

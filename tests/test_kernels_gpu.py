@@ -351,3 +351,33 @@ def test_ckpt_engine_writes_torch_loadable(tmp_path):
     assert got["meta"] == sd["meta"]
     for k in ("w", "b", "h"):
         assert torch.equal(got[k], sd[k].cpu())
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
+def test_gemm_tile_configs(cfg, a_k, b_k):
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(cfg * 7 + a_k * 2 + b_k)
+    M, N, K = 520, 392, 320  # partial tiles in every configuration
+    A = _bf(M, K) if a_k else _bf(K, M)
+    B = _bf(N, K) if b_k else _bf(K, N)
+    Af = A.float() if a_k else A.float().t()
+    Bf = B.float().t() if b_k else B.float()
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k, tile_cfg=cfg)
+    _close(C, Af @ Bf, 1e-5)
+
+
+def test_gemm_splitk_wgrad():
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(21)
+    M, N, K = 16384, 768, 256  # wgrad: dW[N,K] = dY^T X with 16384-long reduction
+    dy, x = _bf(M, N), _bf(M, K)
+    out = G.linear_wgrad(dy, x)
+    _close(out, dy.float().t() @ x.float(), 1e-5)
+    acc = torch.randn(N, K, device=DEV)
+    ref = acc + dy.float().t() @ x.float()
+    G.linear_wgrad(dy, x, out=acc, accumulate=True)
+    _close(acc, ref, 1e-5)

@@ -1,0 +1,125 @@
+"""TorchTrainer / report / retention / failure-restart / bit-exact resume on CPU (gloo)."""
+import json
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SMALL = {"RTDC_FMNIST_TRAIN": "2000", "RTDC_FMNIST_TEST": "500"}
+
+
+@pytest.fixture(autouse=True)
+def _small_data(monkeypatch):
+    for k, v in SMALL.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("RTDC_FORCE_CPU", "1")
+
+
+def _loop(config):
+    from ray_torch_distributed_checkpoint_amd import train
+
+    ctx = train.get_context()
+    start = 0
+    ck = train.get_checkpoint()
+    if ck is not None:
+        with ck.as_directory() as d:
+            start = json.load(open(os.path.join(d, "state.json")))["i"] + 1
+    for i in range(start, config["n"]):
+        d = None
+        if ctx.get_world_rank() == 0:
+            import tempfile
+
+            d = tempfile.mkdtemp()
+            json.dump({"i": i, "rank": ctx.get_world_rank()}, open(os.path.join(d, "state.json"), "w"))
+        train.report({"i": i, "score": [3, 1, 2, 5, 4][i % 5], "ws": ctx.get_world_size()},
+                     checkpoint=train.Checkpoint.from_directory(d) if d else None)
+
+
+def test_trainer_report_layout_and_retention(tmp_path):
+    from ray_torch_distributed_checkpoint_amd import train
+
+    t = train.TorchTrainer(_loop, train_loop_config={"n": 5},
+                           scaling_config=train.ScalingConfig(num_workers=2, use_gpu=False),
+                           run_config=train.RunConfig(storage_path=str(tmp_path), name="exp",
+                                                      checkpoint_config=train.CheckpointConfig(num_to_keep=2)))
+    r = t.fit()
+    assert r.metrics["i"] == 4 and r.metrics["ws"] == 2 and r.metrics["training_iteration"] == 5
+    assert os.path.basename(r.checkpoint.path) == "checkpoint_000004"
+    kept = sorted(d for d in os.listdir(r.path) if d.startswith("checkpoint_"))
+    assert kept == ["checkpoint_000003", "checkpoint_000004"]
+    assert os.path.exists(os.path.join(r.path, "result.json")) and os.path.exists(os.path.join(r.path, "progress.csv"))
+    df = r.metrics_dataframe
+    assert list(df["i"]) == [0, 1, 2, 3, 4]
+    assert r.path.startswith(str(tmp_path / "exp"))
+
+
+def test_trainer_retention_by_score(tmp_path):
+    from ray_torch_distributed_checkpoint_amd import train
+
+    cc = train.CheckpointConfig(num_to_keep=2, checkpoint_score_attribute="score", checkpoint_score_order="max")
+    r = train.TorchTrainer(_loop, train_loop_config={"n": 5},
+                           scaling_config=train.ScalingConfig(num_workers=1),
+                           run_config=train.RunConfig(storage_path=str(tmp_path), checkpoint_config=cc)).fit()
+    kept = sorted(d for d in os.listdir(r.path) if d.startswith("checkpoint_"))
+    # scores 3,1,2,5,4 -> best is index 3 (5); the latest (index 4) is always kept
+    assert kept == ["checkpoint_000003", "checkpoint_000004"]
+    assert r.get_best_checkpoint("score", "max").path.endswith("checkpoint_000003")
+
+
+def test_trainer_failure_restart_from_latest(tmp_path, monkeypatch):
+    from ray_torch_distributed_checkpoint_amd import train
+
+    monkeypatch.setenv("RTDC_FAIL_AT_REPORT", "2:0")  # rank 0 SIGKILLs itself after its 2nd report
+    r = train.TorchTrainer(_loop, train_loop_config={"n": 4},
+                           scaling_config=train.ScalingConfig(num_workers=2),
+                           run_config=train.RunConfig(storage_path=str(tmp_path),
+                                                      failure_config=train.FailureConfig(max_failures=1))).fit()
+    assert r.metrics["i"] == 3
+    rows = [json.loads(l) for l in open(os.path.join(r.path, "result.json"))]
+    assert [row["i"] for row in rows] == [0, 1, 2, 3]  # resumed at i=2, nothing repeated or lost
+
+
+def test_trainer_failure_without_restart_raises(tmp_path, monkeypatch):
+    from ray_torch_distributed_checkpoint_amd import train
+
+    def boom(config):
+        raise ValueError("boom at rank %d" % train.get_context().get_world_rank())
+
+    with pytest.raises(train.TrainingFailedError, match="boom"):
+        train.TorchTrainer(boom, scaling_config=train.ScalingConfig(num_workers=2),
+                           run_config=train.RunConfig(storage_path=str(tmp_path), verbose=0)).fit()
+
+
+def test_exact_resume_is_bit_equal(tmp_path, monkeypatch):
+    """BASELINE config 5: kill during training, restart from the latest checkpoint, and the
+    metrics of the next epoch are bit-identical to an uninterrupted run."""
+    import my_ray_module as m
+
+    a = m.train_fashion_mnist(num_workers=1, epochs=3, checkpoint_storage_path=str(tmp_path / "a"), seed=7,
+                              resume_mode="exact")
+    monkeypatch.setenv("RTDC_FAIL_AT_REPORT", "2")
+    b = m.train_fashion_mnist(num_workers=1, epochs=3, checkpoint_storage_path=str(tmp_path / "b"), seed=7,
+                              resume_mode="exact", max_failures=1)
+    rows_a = [json.loads(l) for l in open(os.path.join(a.path, "result.json"))]
+    rows_b = [json.loads(l) for l in open(os.path.join(b.path, "result.json"))]
+    assert len(rows_a) == len(rows_b) == 3
+    for ra, rb in zip(rows_a, rows_b):
+        assert ra["val_loss"] == rb["val_loss"] and ra["accuracy"] == rb["accuracy"]
+
+
+def test_warm_start_from_checkpoint(tmp_path):
+    import my_ray_module as m
+
+    a = m.train_fashion_mnist(num_workers=2, epochs=2, checkpoint_storage_path=str(tmp_path / "a"))
+    files = sorted(os.listdir(a.checkpoint.path))
+    assert "latest_model.pt" in files
+    sd = torch.load(os.path.join(a.checkpoint.path, "latest_model.pt"), weights_only=True)
+    assert set(["epoch", "model_state_dict", "optimizer_state_dict", "val_losses", "val_accuracy"]) <= set(sd)
+    assert all(k.startswith("module.linear_relu_stack.") for k in sd["model_state_dict"])
+    b = m.train_fashion_mnist(num_workers=1, epochs=1, checkpoint_storage_path=str(tmp_path / "b"),
+                              checkpoint=a.checkpoint)
+    assert b.metrics["val_loss"] < a.metrics["val_loss"] + 0.5

@@ -1,0 +1,100 @@
+"""RayTorchTrain - the reference training flow (R/train_flow.py) on the MI355X-native framework.
+
+    python train_flow.py [--environment=fast-bakery] run [--epochs 3] [--batch_size 32]
+        [--learning_rate 1e-3] [--from-run RayTorchTrain/<id>] [--from-task F/R/S/T]
+    python train_flow.py argo-workflows create | trigger
+
+Same flags, defaults and step graph (start -> train (gang of N_PARALLEL) -> join -> end) as
+the reference.  `current.ray_storage_path` is the per-task checkpoint root handed to
+RunConfig(storage_path=...); `--from-task` takes precedence over `--from-run`; the string
+"null" means unset.  Added (optional): --resume_mode best_weights|exact, --num_workers,
+--max_failures.
+"""
+from ray_torch_distributed_checkpoint_amd.flow import (FlowSpec, Parameter, Run, Task, current, gpu_profile,
+                                                       kubernetes, metaflow_ray, pypi, retry, schedule, step)
+
+N_PARALLEL = 2
+N_GPU_PER_WORKER = 1
+
+
+@schedule(cron="*/5 * * * *")
+class RayTorchTrain(FlowSpec):
+
+    epochs = Parameter("epochs", default=3)
+    global_batch_size = Parameter("batch_size", default=32)
+    learning_rate = Parameter("learning_rate", default=1e-3)
+    upstream_task_pathspec = Parameter(
+        "from-task",
+        default=None,
+        help="A task pathspec like flow_name/run_id/step_name/task_id containing a .results artifact with a checkpoint.",
+    )
+    upstream_run_pathspec = Parameter(
+        "from-run",
+        default=None,
+        help="A run pathspec like flow_name/run_id containing a .results artifact with a checkpoint.",
+    )
+    resume_mode = Parameter("resume_mode", default="best_weights",
+                            help="best_weights (reference warm start) or exact (optimizer/epoch/RNG/sampler).")
+    num_workers = Parameter("num_workers", default=0, help="0 = N_PARALLEL*N_GPU_PER_WORKER capped by visible GPUs")
+    max_failures = Parameter("max_failures", default=0, help="in-trainer restarts from the latest checkpoint")
+
+    @step
+    def start(self):
+        self.next(self.train, num_parallel=N_PARALLEL)
+
+    @retry(times=3)
+    @metaflow_ray(all_nodes_started_timeout=60 * 5)
+    @pypi(packages={})
+    @gpu_profile(interval=1)
+    @kubernetes(gpu=N_GPU_PER_WORKER, compute_pool="obp-gpu")
+    @step
+    def train(self):
+        import torch
+
+        from my_ray_module import train_fashion_mnist
+
+        use_gpu = torch.cuda.is_available()
+        n = int(self.num_workers) or N_PARALLEL * N_GPU_PER_WORKER
+        if use_gpu:
+            n = min(n, torch.cuda.device_count())
+        hyperparameters = dict(
+            epochs=int(self.epochs),
+            global_batch_size=int(self.global_batch_size),
+            learning_rate=float(self.learning_rate),
+        )
+        args = dict(
+            num_workers=n,
+            use_gpu=use_gpu,
+            checkpoint_storage_path=current.ray_storage_path,
+            resume_mode=self.resume_mode,
+            max_failures=int(self.max_failures),
+            **hyperparameters,
+        )
+        if self.upstream_task_pathspec is not None and self.upstream_task_pathspec != "null":
+            t = Task(self.upstream_task_pathspec)
+            args["checkpoint"] = t.data.result.checkpoint
+        elif self.upstream_run_pathspec is not None and self.upstream_run_pathspec != "null":
+            r = Run(self.upstream_run_pathspec)
+            args["checkpoint"] = r.data.result.checkpoint
+        else:
+            print("Training from newly initialized")
+
+        self.result = train_fashion_mnist(**args)
+        self.next(self.join)
+
+    @step
+    def join(self, inputs):
+        for i in inputs:
+            try:
+                self.result = i.result
+            except AttributeError:
+                pass
+        self.next(self.end)
+
+    @step
+    def end(self):
+        print(self.result)
+
+
+if __name__ == "__main__":
+    RayTorchTrain()
