@@ -53,6 +53,14 @@ int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long lon
 int rtdc_relu_dropout(const void* h, void* y, const void* dy, void* dx, long long n, float p,
                       unsigned long long seed, unsigned long long offset, int backward, int is_bf16,
                       hipStream_t st);
+int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, int Hkv, int Dh, float scale,
+                   hipStream_t st);
+int rtdc_rope(const void* x, void* y, const float* cosb, const float* sinb, int ntok, int T, int nrot_heads,
+              int ntot_heads, int Dh, int inverse, hipStream_t st);
+int rtdc_swiglu_fwd(const void* gu, void* h, long long M, int F, hipStream_t st);
+int rtdc_swiglu_bwd(const void* gu, const void* dh, void* dgu, long long M, int F, hipStream_t st);
+int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
+                   int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st);
 }
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -243,6 +251,42 @@ static void relu_dropout(Tensor h, c10::optional<Tensor> y, c10::optional<Tensor
            "relu_dropout");
 }
 
+// ---------------------------------------------------------------------------------- flash attention
+static void flash_fwd(Tensor qkv, Tensor out, Tensor lse, int64_t B, int64_t T, int64_t H, int64_t Hkv, int64_t Dh,
+                      double scale) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.is_contiguous() && out.is_contiguous(), "flash_fwd: contiguous tensors expected");
+  check_rc(rtdc_flash_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H, (int)Hkv,
+                          (int)Dh, (float)scale, cur_stream()),
+           "flash_fwd");
+}
+static void flash_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, Tensor dqkv, int64_t B, int64_t T,
+                      int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+  TORCH_CHECK(dout.is_contiguous() && dqkv.is_contiguous(), "flash_bwd: contiguous tensors expected");
+  check_rc(rtdc_flash_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                          delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)T, (int)H, (int)Hkv, (int)Dh,
+                          (float)scale, cur_stream()),
+           "flash_bwd");
+}
+
+// ---------------------------------------------------------------------------------- llama ops
+static void rope(Tensor x, Tensor y, Tensor cosb, Tensor sinb, int64_t T, int64_t nrot_heads, int64_t ntot_heads,
+                 int64_t Dh, bool inverse) {
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "rope: contiguous tensors expected");
+  const int64_t ntok = x.numel() / (ntot_heads * Dh);
+  check_rc(rtdc_rope(x.data_ptr(), y.data_ptr(), cosb.data_ptr<float>(), sinb.data_ptr<float>(), (int)ntok, (int)T,
+                     (int)nrot_heads, (int)ntot_heads, (int)Dh, inverse, cur_stream()),
+           "rope");
+}
+static void swiglu_fwd(Tensor gu, Tensor h) {
+  const int64_t F = h.size(-1), M = h.numel() / F;
+  check_rc(rtdc_swiglu_fwd(gu.data_ptr(), h.data_ptr(), M, (int)F, cur_stream()), "swiglu_fwd");
+}
+static void swiglu_bwd(Tensor gu, Tensor dh, Tensor dgu) {
+  const int64_t F = dh.size(-1), M = dh.numel() / F;
+  check_rc(rtdc_swiglu_bwd(gu.data_ptr(), dh.data_ptr(), dgu.data_ptr(), M, (int)F, cur_stream()), "swiglu_bwd");
+}
+
 // ---------------------------------------------------------------------------------- checkpoint engine
 using rtdc_ckpt::Engine;
 using rtdc_ckpt::FileJob;
@@ -313,6 +357,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("dropout", &dropout);
   m.def("relu_dropout", &relu_dropout);
+  m.def("flash_fwd", &flash_fwd);
+  m.def("flash_bwd", &flash_bwd);
+  m.def("rope", &rope);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
 
   m.def("have_gpu", &rtdc_ckpt::g_have_gpu);
   m.def("plan_layout", &plan_layout, "file layout of a list of (raw, records) archives");

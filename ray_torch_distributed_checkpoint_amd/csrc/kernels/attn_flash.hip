@@ -1,0 +1,454 @@
+// Fused causal flash attention (forward + backward) for gfx950, bf16 in / fp32 accumulate.
+//
+// Reads Q, K, V in place from the packed QKV activations [B, T, (H + 2*Hkv) * Dh] written by
+// the c_attn GEMM (GQA: q-head h uses kv-head h / (H/Hkv)) and never materialises the
+// T x T score matrix.  v_mfma_f32_16x16x32_bf16 everywhere; every product is laid out so
+// the accumulator of one MFMA is the B operand of the next with no data movement
+// (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"): the score
+// tile is computed transposed (D[key][q]) so a lane owns one query row and its P values feed
+// the P.V MFMA directly; the k-order permutation this implies (key = 32s + 16(j>>2) + 4g +
+// (j&3) for element j of lane group g) is reproduced on the other operand by reading V / dO
+// / Q / K tiles with the transposing LDS read ds_read_b64_tr_b16 (4 consecutive rows x 16
+// columns per 16-lane group).
+//
+//   fwd     : block = 64 query rows (4 waves x 16) of one (b, h); K/V tiles of 64 keys
+//             double-buffered in LDS by global_load_lds; online softmax in the log2 domain;
+//             writes O and the row log-sum-exp.
+//   bwd_dkdv: block = 64 keys (4 waves x 16) of one (b, kv-head); loops over the query
+//             blocks at or after the diagonal and over the q-heads of the GQA group; keeps
+//             dK/dV in registers - no atomics.
+//   bwd_dq  : block = 64 query rows; loops over key blocks up to the diagonal.  Recomputing
+//             P here instead of accumulating dQ with float atomics keeps the backward
+//             bitwise reproducible (MI355X_MICROARCH.md §Global float atomics).
+//   delta   : D[b,h,t] = sum_d dO * O (the softmax-backward row term).
+// Requires T % 64 == 0 and Dh in {64, 128}.
+#include "common.h"
+
+namespace rtdc {
+namespace fa {
+
+constexpr int BQ = 64, BKV = 64, NT = 256;
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct Args {
+  const bf16_t* qkv;  // [B, T, W]
+  bf16_t* out;        // [B, T, H*Dh]
+  float* lse;         // [B*H, T] natural-log LSE of the scaled scores
+  const bf16_t* dout; // [B, T, H*Dh]
+  const float* delta; // [B*H, T]
+  bf16_t* dqkv;       // [B, T, W]
+  int B, T, H, Hkv;
+  float scale;
+};
+
+// [64 rows][DH] bf16 LDS image, 16-B chunks XOR-swizzled per row (bank-conflict-free
+// ds_read_b128 row reads; 2-way on the transposing reads).
+template <int DH>
+__device__ __forceinline__ int toff(int row, int chunk) {
+  if constexpr (DH == 64) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+  else return row * 256 + ((chunk ^ (row & 15)) << 4);
+}
+
+// global -> LDS copy of rows [r0, r0+64) (row stride ld elements, column offset col0) by all
+// 4 waves: 1 KiB global_load_lds pieces, swizzle applied on the source address.
+template <int DH>
+__device__ __forceinline__ void stage(const bf16_t* base, long long ld, int r0, int col0, char* tile, int wave,
+                                      int lane) {
+  constexpr int RB = DH * 2, CPR = RB / 16, RPP = 1024 / RB, PIECES = 64 * RB / 1024, PPW = PIECES / 4;
+#pragma unroll
+  for (int ii = 0; ii < PPW; ++ii) {
+    const int piece = wave * PPW + ii;
+    const int row = piece * RPP + lane / CPR;
+    const int pch = lane % CPR;
+    int lch;
+    if constexpr (DH == 64) lch = pch ^ ((row >> 1) & 7);
+    else lch = pch ^ (row & 15);
+    const bf16_t* src = base + (long long)(r0 + row) * ld + col0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(tile + piece * 1024), 16, 0, 0);
+  }
+}
+
+// MFMA operand with rows = tile rows [R0, R0+16), k = columns 32*ks + 8g + j  (ds_read_b128)
+template <int DH>
+__device__ __forceinline__ bf16x8 frag_rows(const char* tile, int R0, int ks, int lane) {
+  return *(const bf16x8*)(tile + toff<DH>(R0 + (lane & 15), ks * 4 + (lane >> 4)));
+}
+
+// MFMA operand with rows = tile columns [d0, d0+16), k = tile rows in the accumulator order
+// kbase + 16(j>>2) + 4g + (j&3)  (two ds_read_b64_tr_b16)
+template <int DH>
+__device__ __forceinline__ bf16x8 frag_cols(const char* tile, int kbase, int d0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  bf16x4 v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = kbase + 16 * h + 4 * g + q;
+    const int off = toff<DH>(row, (d0 >> 3) + (p >> 1)) + ((p & 1) << 3);
+    v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(tile + off));
+  }
+  bf16x8 r;
+  r[0] = v[0][0]; r[1] = v[0][1]; r[2] = v[0][2]; r[3] = v[0][3];
+  r[4] = v[1][0]; r[5] = v[1][1]; r[6] = v[1][2]; r[7] = v[1][3];
+  return r;
+}
+
+// 16-B global load of row `row` columns [c, c+8) -> bf16x8
+__device__ __forceinline__ bf16x8 gload8(const bf16_t* p) { return *(const bf16x8*)p; }
+
+// two accumulator tiles (rows 16*(2s) and 16*(2s+1)) -> one bf16 B operand
+__device__ __forceinline__ bf16x8 pack_pair(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
+  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
+  return r;
+}
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------ forward
+template <int DH>
+__global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K[2], V[2]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = a.T / BQ;
+  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest (longest causal prefix) blocks first
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int grp = a.H / a.Hkv, kvh = h / grp;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const int qcol = h * DH, kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int q0w = qb * BQ + wave * 16;
+  const int myq = q0w + (lane & 15);
+  const float c = a.scale * LOG2E;
+
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (2 + (s)) * TILE)
+  const int nkb = qb + 1;
+  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
+  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) {
+      stage<DH>(base, W, (kb + 1) * BKV, kcol, KT(cur ^ 1), wave, lane);
+      stage<DH>(base, W, (kb + 1) * BKV, vcol, VT(cur ^ 1), wave, lane);
+    }
+    const char* kt = KT(cur);
+    const char* vt = VT(cur);
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[t] = mfma(frag_rows<DH>(kt, 16 * t, ks, lane), qf[ks], s[t]);
+    }
+    // scale (log2 domain), causal mask on the diagonal block, running max
+    float mx = -INFINITY;
+    const bool diag = (kb == qb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = s[t][r] * c;
+        if (diag) {
+          const int key = kb * BKV + 16 * t + 4 * g + r;
+          if (key > myq) v = -INFINITY;
+        }
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[t][r] - mn);
+        s[t][r] = p;
+        ps += p;
+      }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[d][r] *= alpha;
+    const bf16x8 p0 = pack_pair(s[0], s[1]), p1 = pack_pair(s[2], s[3]);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      o[d] = mfma(frag_cols<DH>(vt, 0, 16 * d, lane), p0, o[d]);
+      o[d] = mfma(frag_cols<DH>(vt, 32, 16 * d, lane), p1, o[d]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef KT
+#undef VT
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  bf16_t* orow = a.out + ((long long)b * a.T + myq) * C + h * DH;
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    const uint2 v = make_uint2(pack_bf2(o[d][0] * inv, o[d][1] * inv), pack_bf2(o[d][2] * inv, o[d][3] * inv));
+    *(uint2*)(orow + 16 * d + 4 * g) = v;
+  }
+  if (g == 0) a.lse[(long long)bh * a.T + myq] = (m + log2f(l)) / LOG2E;
+}
+
+// ------------------------------------------------------------------------------ delta
+__global__ __launch_bounds__(256) void delta_kernel(const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
+                                                   float* __restrict__ delta, int B, int T, int H, int DH) {
+  const long long idx = blockIdx.x * 256LL + threadIdx.x;  // (b, t, h)
+  if (idx >= (long long)B * T * H) return;
+  const int h = (int)(idx % H);
+  const long long bt = idx / H;
+  const int t = (int)(bt % T), b = (int)(bt / T);
+  const bf16_t* o = out + bt * H * DH + h * DH;
+  const bf16_t* d = dout + bt * H * DH + h * DH;
+  float s = 0.f;
+  for (int c = 0; c < DH; c += 8) {
+    uint4 x = *(const uint4*)(o + c), y = *(const uint4*)(d + c);
+    uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s += __uint_as_float(xa[i] << 16) * __uint_as_float(ya[i] << 16);
+      s += __uint_as_float(xa[i] & 0xffff0000u) * __uint_as_float(ya[i] & 0xffff0000u);
+    }
+  }
+  delta[((long long)b * H + h) * T + t] = s;
+}
+
+// ------------------------------------------------------------------------------ dK / dV
+template <int DH>
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // Q[2], dO[2]
+  __shared__ float s_lse[2][64], s_del[2][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nkb = a.T / BKV;
+  const int kb = (int)blockIdx.x;  // key block
+  const int bk = blockIdx.y, b = bk / a.Hkv, kvh = bk % a.Hkv;
+  const int grp = a.H / a.Hkv;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const bf16_t* dob = a.dout + (long long)b * a.T * C;
+  const int kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int k0w = kb * BKV + wave * 16;
+  const int mykey = k0w + (lane & 15);
+  const float c = a.scale * LOG2E;
+
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = gload8(base + (long long)mykey * W + kcol + ks * 32 + g * 8);
+    vf[ks] = gload8(base + (long long)mykey * W + vcol + ks * 32 + g * 8);
+  }
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) dk[d] = dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define QT(s) (smem + (s) * TILE)
+#define OT(s) (smem + (2 + (s)) * TILE)
+  const int nq = nkb - kb;     // q blocks at/after the diagonal
+  const int total = nq * grp;  // iterations over (q-head in group, q block)
+  auto issue = [&](int it, int buf) {
+    const int gi = it / nq, qb = kb + it % nq;
+    const int h = kvh * grp + gi;
+    stage<DH>(base, W, qb * BQ, h * DH, QT(buf), wave, lane);
+    stage<DH>(dob, C, qb * BQ, h * DH, OT(buf), wave, lane);
+    if (threadIdx.x < 64) {
+      const long long r = ((long long)b * a.H + h) * a.T + qb * BQ + threadIdx.x;
+      s_lse[buf][threadIdx.x] = a.lse[r] * LOG2E;
+      s_del[buf][threadIdx.x] = a.delta[r];
+    }
+  };
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < total) issue(it + 1, cur ^ 1);
+    const int qb = kb + it % nq;
+    const char* qt = QT(cur);
+    const char* ot = OT(cur);
+    const bool diag = (qb == kb);
+    f32x4 p[4], ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sacc = mfma(frag_rows<DH>(qt, 16 * t, ks, lane), kf[ks], sacc);   // D[q][key]
+        dpacc = mfma(frag_rows<DH>(ot, 16 * t, ks, lane), vf[ks], dpacc); // D[q][key]
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * t + 4 * g + r;
+        float pv = exp2f(sacc[r] * c - s_lse[cur][ql]);
+        if (diag && qb * BQ + ql < mykey) pv = 0.f;
+        p[t][r] = pv;
+        ds[t][r] = pv * (dpacc[r] - s_del[cur][ql]);
+      }
+    }
+    const bf16x8 p0 = pack_pair(p[0], p[1]), p1 = pack_pair(p[2], p[3]);
+    const bf16x8 d0 = pack_pair(ds[0], ds[1]), d1 = pack_pair(ds[2], ds[3]);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      dv[d] = mfma(frag_cols<DH>(ot, 0, 16 * d, lane), p0, dv[d]);
+      dv[d] = mfma(frag_cols<DH>(ot, 32, 16 * d, lane), p1, dv[d]);
+      dk[d] = mfma(frag_cols<DH>(qt, 0, 16 * d, lane), d0, dk[d]);
+      dk[d] = mfma(frag_cols<DH>(qt, 32, 16 * d, lane), d1, dk[d]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef QT
+#undef OT
+  bf16_t* krow = a.dqkv + ((long long)b * a.T + mykey) * W;
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    *(uint2*)(krow + kcol + 16 * d + 4 * g) =
+        make_uint2(pack_bf2(dk[d][0] * a.scale, dk[d][1] * a.scale), pack_bf2(dk[d][2] * a.scale, dk[d][3] * a.scale));
+    *(uint2*)(krow + vcol + 16 * d + 4 * g) = make_uint2(pack_bf2(dv[d][0], dv[d][1]), pack_bf2(dv[d][2], dv[d][3]));
+  }
+}
+
+// ------------------------------------------------------------------------------ dQ
+template <int DH>
+__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K[2], V[2]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = a.T / BQ;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int grp = a.H / a.Hkv, kvh = h / grp;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const int qcol = h * DH, kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int myq = qb * BQ + wave * 16 + (lane & 15);
+  const float c = a.scale * LOG2E;
+  const long long r = (long long)bh * a.T + myq;
+  const float lse2 = a.lse[r] * LOG2E, del = a.delta[r];
+
+  bf16x8 qf[KS], of[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
+    of[ks] = gload8(a.dout + ((long long)b * a.T + myq) * C + h * DH + ks * 32 + g * 8);
+  }
+  f32x4 dq[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (2 + (s)) * TILE)
+  const int nkb = qb + 1;
+  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
+  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) {
+      stage<DH>(base, W, (kb + 1) * BKV, kcol, KT(cur ^ 1), wave, lane);
+      stage<DH>(base, W, (kb + 1) * BKV, vcol, VT(cur ^ 1), wave, lane);
+    }
+    const char* kt = KT(cur);
+    const char* vt = VT(cur);
+    const bool diag = (kb == qb);
+    f32x4 ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sacc = mfma(frag_rows<DH>(kt, 16 * t, ks, lane), qf[ks], sacc);   // D[key][q]
+        dpacc = mfma(frag_rows<DH>(vt, 16 * t, ks, lane), of[ks], dpacc); // D[key][q]
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int key = kb * BKV + 16 * t + 4 * g + rr;
+        float pv = exp2f(sacc[rr] * c - lse2);
+        if (diag && key > myq) pv = 0.f;
+        ds[t][rr] = pv * (dpacc[rr] - del);
+      }
+    }
+    const bf16x8 d0 = pack_pair(ds[0], ds[1]), d1 = pack_pair(ds[2], ds[3]);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      dq[d] = mfma(frag_cols<DH>(kt, 0, 16 * d, lane), d0, dq[d]);
+      dq[d] = mfma(frag_cols<DH>(kt, 32, 16 * d, lane), d1, dq[d]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef KT
+#undef VT
+  bf16_t* qrow = a.dqkv + ((long long)b * a.T + myq) * W + qcol;
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+    *(uint2*)(qrow + 16 * d + 4 * g) =
+        make_uint2(pack_bf2(dq[d][0] * a.scale, dq[d][1] * a.scale), pack_bf2(dq[d][2] * a.scale, dq[d][3] * a.scale));
+}
+
+}  // namespace fa
+}  // namespace rtdc
+
+using namespace rtdc;
+
+extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, int Hkv, int Dh,
+                              float scale, hipStream_t st) {
+  if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
+  fa::Args a{};
+  a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.lse = lse;
+  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
+  dim3 grid(T / 64, B * H), block(256);
+  if (Dh == 64) hipLaunchKernelGGL(fa::fwd_kernel<64>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(fa::fwd_kernel<128>, grid, block, 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
+                              void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st) {
+  if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
+  const long long rows = (long long)B * T * H;
+  hipLaunchKernelGGL(fa::delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, (const bf16_t*)out,
+                     (const bf16_t*)dout, delta, B, T, H, Dh);
+  fa::Args a{};
+  a.qkv = (const bf16_t*)qkv; a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta;
+  a.dqkv = (bf16_t*)dqkv;
+  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
+  dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H), block(256);
+  if (Dh == 64) {
+    hipLaunchKernelGGL(fa::bwd_dkdv_kernel<64>, g1, block, 0, st, a);
+    hipLaunchKernelGGL(fa::bwd_dq_kernel<64>, g2, block, 0, st, a);
+  } else {
+    hipLaunchKernelGGL(fa::bwd_dkdv_kernel<128>, g1, block, 0, st, a);
+    hipLaunchKernelGGL(fa::bwd_dq_kernel<128>, g2, block, 0, st, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -17,6 +17,7 @@ this path when T grows.  GQA (Llama) reuses it with per-head K/V strides.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -108,6 +109,34 @@ class _CausalAttention(torch.autograd.Function):
         return dqkv, None, None, None, None, None
 
 
+class _FlashAttention(torch.autograd.Function):
+    """Fused causal flash attention (csrc/kernels/attn_flash.hip): no T x T matrix in HBM."""
+
+    @staticmethod
+    def forward(ctx, qkv, B, T, H, Hkv, Dh):
+        qkv = qkv.contiguous()
+        out = torch.empty((B, T, H * Dh), dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty((B * H, T), dtype=torch.float32, device=qkv.device)
+        scale = 1.0 / math.sqrt(Dh)
+        gpu_ext().flash_fwd(qkv, out, lse, B, T, H, Hkv, Dh, scale)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.dims = (B, T, H, Hkv, Dh, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        B, T, H, Hkv, Dh, scale = ctx.dims
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty((B * H, T), dtype=torch.float32, device=qkv.device)
+        gpu_ext().flash_bwd(qkv, out, dout.contiguous(), lse, delta, dqkv, B, T, H, Hkv, Dh, scale)
+        return dqkv, None, None, None, None, None
+
+
+def flash_supported(T: int, Dh: int) -> bool:
+    return T % 64 == 0 and Dh in (64, 128)
+
+
 def causal_attention_ref(qkv, B, T, H, Hkv, Dh):
     C = H * Dh
     q = qkv[..., :C].reshape(B, T, H, Dh).transpose(1, 2)
@@ -127,4 +156,7 @@ def causal_attention(qkv: torch.Tensor, n_head: int, n_kv_head: int | None = Non
     Dh = W // (n_head + 2 * Hkv)
     if not qkv.is_cuda or qkv.dtype != torch.bfloat16:
         return causal_attention_ref(qkv, B, T, n_head, Hkv, Dh)
+    impl = os.environ.get("RTDC_ATTN", "flash")
+    if impl == "flash" and flash_supported(T, Dh):
+        return _FlashAttention.apply(qkv, B, T, n_head, Hkv, Dh)
     return _CausalAttention.apply(qkv, B, T, n_head, Hkv, Dh)

@@ -381,3 +381,41 @@ def test_gemm_splitk_wgrad():
     ref = acc + dy.float().t() @ x.float()
     G.linear_wgrad(dy, x, out=acc, accumulate=True)
     _close(acc, ref, 1e-5)
+
+
+@pytest.mark.parametrize("impl", ["flash", "gemm"])
+@pytest.mark.parametrize("H,Hkv,Dh,T", [(4, 4, 64, 256), (4, 2, 64, 192), (2, 1, 128, 128), (3, 3, 128, 320)])
+def test_attention_impls(monkeypatch, impl, H, Hkv, Dh, T):
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref
+
+    monkeypatch.setenv("RTDC_ATTN", impl)
+    torch.manual_seed(H * 100 + Dh + T)
+    Bn = 2
+    W = (H + 2 * Hkv) * Dh
+    qkv = _bf(Bn, T, W).requires_grad_(True)
+    out = causal_attention(qkv, H, Hkv)
+    g = _bf(Bn, T, H * Dh)
+    out.backward(g)
+    qr = qkv.detach().float().requires_grad_(True)
+    ref = causal_attention_ref(qr, Bn, T, H, Hkv, Dh)
+    ref.backward(g.float())
+    _close(out, ref, 2e-2)
+    C = H * Dh
+    _close(qkv.grad[..., :C], qr.grad[..., :C], 3e-2)            # dQ
+    _close(qkv.grad[..., C:C + Hkv * Dh], qr.grad[..., C:C + Hkv * Dh], 3e-2)  # dK
+    _close(qkv.grad[..., C + Hkv * Dh:], qr.grad[..., C + Hkv * Dh:], 3e-2)    # dV
+
+
+def test_flash_attention_deterministic():
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+
+    torch.manual_seed(31)
+    qkv = _bf(2, 256, 3 * 4 * 64).requires_grad_(True)
+    g = _bf(2, 256, 4 * 64)
+    grads = []
+    for _ in range(2):
+        qkv.grad = None
+        causal_attention(qkv, 4).backward(g)
+        grads.append(qkv.grad.clone())
+    assert torch.equal(grads[0], grads[1])
