@@ -14,6 +14,8 @@ durable and `.metadata` committed, training throughput while the write is in fli
 the restore wall-clock (sharded read + RCCL broadcast into the live model/optimizer).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model gpt2-small] [--batch 16]
+    python bench.py --model resnet18 [--batch 256] [--image-size 224]      (BASELINE config 2)
+    python bench.py --model llama3-8b [--batch 1] [--seq-len 2048]         (BASELINE config 4)
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -50,13 +52,20 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="gpt2-small")
-    ap.add_argument("--batch", type=int, default=16, help="sequences per GPU per step")
-    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU per step (model default if unset)")
+    ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--no-ckpt", action="store_true")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--overlap-steps", type=int, default=5)
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (multi-rank rehearsal on 1 GPU)")
     args = ap.parse_args()
+    args.batch_set, args.seq_len_set = args.batch is not None, args.seq_len is not None
+    if args.batch is None:
+        args.batch = 16
+    if args.seq_len is None:
+        args.seq_len = 1024
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # self-launch one process per GPU (before anything touches the GPU)
@@ -68,33 +77,29 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
-    from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
-    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW
     from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
     from ray_torch_distributed_checkpoint_amd.ops import _ext
 
     _ext.gpu_ext()  # native kernels are mandatory on the GPU path
     torch.manual_seed(1234)
-    cfg = GPT2Config.named(args.model)
-    T = min(args.seq_len, cfg.n_positions)
-    B = args.batch
-    model = GPT2(cfg).to(dev)
+    wl = build_workload(args, dev, rank)
+    model, opt = wl["model"], wl["opt"]
     net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
-    opt = FusedAdamW(model.parameters(), lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
-
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    pool = [torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev, generator=g) for _ in range(4)]
+    B, T = wl["batch"], wl["seq_len"]
+    fwd_loss = wl["loss"]
 
     def step(i):
-        data = pool[i % len(pool)]
-        loss = net(data[:, :-1], data[:, 1:])
+        loss = fwd_loss(net, i)
         loss.backward()
         opt.step()
         opt.zero_grad()
@@ -124,15 +129,14 @@ def main():
 
     ck = {}
     if not args.no_ckpt:
-        ck = checkpoint_phase(args, model, opt, net, pool, step, world, rank, dev, dcp)
+        ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp)
 
     metric, published = _baseline_metric()
     base = published.get("samples_per_sec") if isinstance(published, dict) else None
-    flops_tok = model.flops_per_token(T)
     out = {
         "metric": metric,
         "value": round(samples_per_s, 3),
-        "unit": "samples/s (sequences of %d tokens, all GPUs)" % T,
+        "unit": wl["unit"],
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -141,15 +145,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": (round(samples_per_s / base, 4) if base else None),
         "dtype": "bf16",
-        "data": "synthetic (random tokens), random-init weights",
+        "data": wl["data"],
         "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
-                   "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "optimizer": "fused AdamW (fp32 master)",
+                   "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "optimizer": wl["optim_name"],
                    "params": model.num_params()},
         "samples_per_sec_per_gpu": round(samples_per_s / world, 3),
-        "tokens_per_sec": round(samples_per_s * T, 1),
-        "model_tflops_per_gpu": round(flops_tok * samples_per_s * T / world / 1e12, 2),
+        "model_tflops_per_gpu": round(wl["flops_per_sample"] * samples_per_s / world / 1e12, 2),
         "final_loss": round(final_loss, 4),
     }
+    if wl.get("tokens_per_sample"):
+        out["tokens_per_sec"] = round(samples_per_s * wl["tokens_per_sample"], 1)
     out.update(ck)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -158,7 +163,62 @@ def main():
         dist.destroy_process_group()
 
 
-def checkpoint_phase(args, model, opt, net, pool, step, world, rank, dev, dcp):
+def build_workload(args, dev, rank):
+    """Model + optimizer + synthetic batch pool for one BASELINE.json config."""
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW, FusedSGD
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    name = args.model
+    if name.startswith("resnet"):
+        from ray_torch_distributed_checkpoint_amd.models import ResNet18
+
+        hw = args.image_size
+        B = args.batch if args.batch_set else 256
+        model = ResNet18(num_classes=10).to(dev)
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+        pool = [(torch.randn(B, 3, hw, hw, device=dev, generator=g),
+                 torch.randint(0, 10, (B,), device=dev, generator=g)) for _ in range(2)]
+
+        def loss(net, i):
+            x, y = pool[i % len(pool)]
+            return ops.cross_entropy(net(x), y)
+
+        return dict(model=model, opt=opt, batch=B, seq_len=hw, loss=loss,
+                    unit=f"samples/s ({hw}x{hw} images, all GPUs)", optim_name="fused SGD momentum (fp32 master)",
+                    data="synthetic (random images/labels), random-init weights",
+                    flops_per_sample=model.flops_per_sample(hw))
+    if name.startswith("llama"):
+        from ray_torch_distributed_checkpoint_amd.models import Llama, LlamaConfig
+
+        cfg = LlamaConfig.named(name)
+        T = min(args.seq_len if args.seq_len_set else 2048, cfg.max_seq_len)
+        B = args.batch if args.batch_set else 1
+        model = Llama(cfg, device=dev)
+        vocab = cfg.vocab_size
+    else:
+        from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+
+        cfg = GPT2Config.named(name)
+        T = min(args.seq_len, cfg.n_positions)
+        B = args.batch
+        model = GPT2(cfg).to(dev)
+        vocab = cfg.vocab_size
+    opt = FusedAdamW(model.parameters(), lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    pool = [torch.randint(0, vocab, (B, T + 1), device=dev, generator=g) for _ in range(4)]
+
+    def loss(net, i):
+        data = pool[i % len(pool)]
+        return net(data[:, :-1], data[:, 1:])
+
+    return dict(model=model, opt=opt, batch=B, seq_len=T, loss=loss, tokens_per_sample=T,
+                unit=f"samples/s (sequences of {T} tokens, all GPUs)", optim_name="fused AdamW (fp32 master)",
+                data="synthetic (random tokens), random-init weights",
+                flops_per_sample=model.flops_per_token(T) * T)
+
+
+def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     base = args.ckpt_dir or os.environ.get("RTDC_BENCH_CKPT_DIR") or tempfile.gettempdir()
     path = os.path.join(base, "rtdc_bench_ckpt")
     if rank == 0:

@@ -59,6 +59,19 @@ int rtdc_rope(const void* x, void* y, const float* cosb, const float* sinb, int 
               int ntot_heads, int Dh, int inverse, hipStream_t st);
 int rtdc_swiglu_fwd(const void* gu, void* h, long long M, int F, hipStream_t st);
 int rtdc_swiglu_bwd(const void* gu, const void* dh, void* dgu, long long M, int F, hipStream_t st);
+int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
+                int pad, int K, int Kp, hipStream_t st);
+int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
+                int pad, int K, int Kp, hipStream_t st);
+int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma, const float* beta,
+                float* running_mean, float* running_var, long long N, int C, float eps, float momentum, int training,
+                int relu, float* ws, int nblk, hipStream_t st);
+int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
+                void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu, float* ws, int nblk,
+                hipStream_t st);
+int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, int B, int H, int W, int C, int Ho, int Wo,
+                 int K, int s, int p, int backward, hipStream_t st);
+int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st);
 int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                    int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st);
 }
@@ -287,6 +300,69 @@ static void swiglu_bwd(Tensor gu, Tensor dh, Tensor dgu) {
   check_rc(rtdc_swiglu_bwd(gu.data_ptr(), dh.data_ptr(), dgu.data_ptr(), M, (int)F, cur_stream()), "swiglu_bwd");
 }
 
+// ---------------------------------------------------------------------------------- conv / batchnorm / pooling
+// x: NHWC bf16 [B,H,W,C]; cols: [B*Ho*Wo, Kp] with K = KH*KW*C real columns (rest zero).
+static void im2col(Tensor x, Tensor cols, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  TORCH_CHECK(x.is_contiguous() && cols.is_contiguous() && x.dim() == 4, "im2col: contiguous NHWC expected");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = KH * KW * C, Kp = cols.size(1);
+  TORCH_CHECK(cols.size(0) == B * Ho * Wo && Kp >= K, "im2col: bad cols shape");
+  check_rc(rtdc_im2col(x.data_ptr(), cols.data_ptr(), (int)B, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH,
+                       (int)KW, (int)stride, (int)pad, (int)K, (int)Kp, cur_stream()),
+           "im2col");
+}
+static void col2im(Tensor dcols, Tensor dx, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride,
+                   int64_t pad) {
+  TORCH_CHECK(dx.is_contiguous() && dcols.is_contiguous() && dx.dim() == 4, "col2im: contiguous NHWC expected");
+  const int64_t B = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3), K = KH * KW * C, Kp = dcols.size(1);
+  TORCH_CHECK(dcols.size(0) == B * Ho * Wo && Kp >= K, "col2im: bad cols shape");
+  check_rc(rtdc_col2im(dcols.data_ptr(), dx.data_ptr(), (int)B, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH,
+                       (int)KW, (int)stride, (int)pad, (int)K, (int)Kp, cur_stream()),
+           "col2im");
+}
+static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta,
+                   c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var, double eps, double momentum,
+                   bool training, bool relu, Tensor ws, int64_t nblk) {
+  const int64_t C = x.size(-1), N = x.numel() / C;
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "bn_fwd: contiguous tensors expected");
+  TORCH_CHECK(!training || ws.numel() >= 2 * nblk * C, "bn_fwd: workspace too small");
+  check_rc(rtdc_bn_fwd(x.data_ptr(), ptr_or_null(res), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                       gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                       running_mean.has_value() ? running_mean->data_ptr<float>() : nullptr,
+                       running_var.has_value() ? running_var->data_ptr<float>() : nullptr, N, (int)C, (float)eps,
+                       (float)momentum, training, relu, ws.data_ptr<float>(), (int)nblk, cur_stream()),
+           "bn_fwd");
+}
+static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor dx,
+                   c10::optional<Tensor> dres, Tensor dgamma, Tensor dbeta, bool relu, Tensor ws, int64_t nblk) {
+  const int64_t C = x.size(-1), N = x.numel() / C;
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dx.is_contiguous(), "bn_bwd: contiguous tensors expected");
+  TORCH_CHECK(ws.numel() >= 2 * nblk * C, "bn_bwd: workspace too small");
+  check_rc(rtdc_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                       gamma.data_ptr<float>(), dx.data_ptr(), ptr_or_null(dres), dgamma.data_ptr<float>(),
+                       dbeta.data_ptr<float>(), N, (int)C, relu, ws.data_ptr<float>(), (int)nblk, cur_stream()),
+           "bn_bwd");
+}
+static void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t K, int64_t s, int64_t p) {
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && arg.scalar_type() == torch::kUInt8, "maxpool_fwd: bad args");
+  check_rc(rtdc_maxpool(x.data_ptr(), y.data_ptr(), arg.data_ptr(), nullptr, nullptr, (int)x.size(0), (int)x.size(1),
+                        (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)K, (int)s, (int)p, 0,
+                        cur_stream()),
+           "maxpool_fwd");
+}
+static void maxpool_bwd(Tensor dy, Tensor arg, Tensor dx, int64_t K, int64_t s, int64_t p) {
+  TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous(), "maxpool_bwd: contiguous tensors expected");
+  check_rc(rtdc_maxpool(nullptr, nullptr, arg.data_ptr(), dy.data_ptr(), dx.data_ptr(), (int)dx.size(0),
+                        (int)dx.size(1), (int)dx.size(2), (int)dx.size(3), (int)dy.size(1), (int)dy.size(2), (int)K,
+                        (int)s, (int)p, 1, cur_stream()),
+           "maxpool_bwd");
+}
+// x [B, HW, C] <-> y [B, C]
+static void avgpool(Tensor x, Tensor y, bool backward) {
+  const int64_t B = backward ? y.size(0) : x.size(0), C = backward ? y.size(-1) : x.size(-1);
+  const int64_t HW = (backward ? y.numel() : x.numel()) / (B * C);
+  check_rc(rtdc_avgpool(x.data_ptr(), y.data_ptr(), (int)B, (int)HW, (int)C, backward, cur_stream()), "avgpool");
+}
+
 // ---------------------------------------------------------------------------------- checkpoint engine
 using rtdc_ckpt::Engine;
 using rtdc_ckpt::FileJob;
@@ -362,6 +438,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope", &rope);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("im2col", &im2col);
+  m.def("col2im", &col2im);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool", &avgpool);
 
   m.def("have_gpu", &rtdc_ckpt::g_have_gpu);
   m.def("plan_layout", &plan_layout, "file layout of a list of (raw, records) archives");

@@ -1,0 +1,468 @@
+// Convolution support (NHWC, bf16) for gfx950: im2col / col2im around the MFMA GEMM, fused
+// BatchNorm(+residual)(+ReLU) forward/backward with deterministic two-stage channel
+// reductions, max-pool 3x3/s2 and global average pool.  ResNet-18 (BASELINE config 2).
+//
+// Channels-last puts the GEMM reduction dimension (kh, kw, c) contiguous, so a convolution is
+// Y[B*Ho*Wo, Cout] = cols[B*Ho*Wo, K] . Wmat[Cout, K]^T on the K-major x K-major GEMM, its
+// weight gradient the MN x MN GEMM (split-K: K-reduction over B*Ho*Wo) and its input gradient
+// dcols = dY . Wmat followed by a col2im GATHER (each input element sums the <= KH*KW columns
+// that read it: no atomics, bitwise reproducible).
+#include "common.h"
+
+namespace rtdc {
+
+struct ConvGeom {
+  int B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp;
+};
+
+// cols[(b,ho,wo)][k], k = (kh*KW + kw)*C + c ; zero for k >= K and for padding taps.
+__global__ __launch_bounds__(256) void im2col_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ cols,
+                                                    ConvGeom g, int vec) {
+  const long long rows = (long long)g.B * g.Ho * g.Wo;
+  const int per_row = vec ? g.Kp / 8 : g.Kp;
+  const long long total = rows * per_row;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long r = i / per_row;
+    const int kk = (int)(i % per_row) * (vec ? 8 : 1);
+    const int wo = (int)(r % g.Wo);
+    const int ho = (int)((r / g.Wo) % g.Ho);
+    const int b = (int)(r / ((long long)g.Wo * g.Ho));
+    if (vec) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (kk < g.K) {
+        const int c = kk % g.C, tap = kk / g.C, kw = tap % g.KW, kh = tap / g.KW;
+        const int h = ho * g.stride - g.pad + kh, w = wo * g.stride - g.pad + kw;
+        if (h >= 0 && h < g.H && w >= 0 && w < g.W)
+          v = *(const uint4*)(x + (((long long)b * g.H + h) * g.W + w) * g.C + c);
+      }
+      *(uint4*)(cols + r * g.Kp + kk) = v;
+    } else {
+      bf16_t v = 0;
+      if (kk < g.K) {
+        const int c = kk % g.C, tap = kk / g.C, kw = tap % g.KW, kh = tap / g.KW;
+        const int h = ho * g.stride - g.pad + kh, w = wo * g.stride - g.pad + kw;
+        if (h >= 0 && h < g.H && w >= 0 && w < g.W) v = x[(((long long)b * g.H + h) * g.W + w) * g.C + c];
+      }
+      cols[r * g.Kp + kk] = v;
+    }
+  }
+}
+
+// dx[b,h,w,c] = sum_{kh,kw} dcols[(b,ho,wo)][(kh,kw,c)] over taps with ho*s - p + kh = h.
+// 8 channels per thread (C % 8 == 0).
+__global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx,
+                                                    ConvGeom g) {
+  const long long total = (long long)g.B * g.H * g.W * (g.C / 8);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % (g.C / 8)) * 8;
+    const long long pix = i / (g.C / 8);
+    const int w = (int)(pix % g.W);
+    const int h = (int)((pix / g.W) % g.H);
+    const int b = (int)(pix / ((long long)g.W * g.H));
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int hs = h + g.pad - kh;
+      if (hs < 0 || hs % g.stride) continue;
+      const int ho = hs / g.stride;
+      if (ho >= g.Ho) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int ws = w + g.pad - kw;
+        if (ws < 0 || ws % g.stride) continue;
+        const int wo = ws / g.stride;
+        if (wo >= g.Wo) continue;
+        const long long r = ((long long)b * g.Ho + ho) * g.Wo + wo;
+        uint4 v = *(const uint4*)(dcols + r * g.Kp + (kh * g.KW + kw) * g.C + c);
+        uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(u[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
+    }
+    *(uint4*)(dx + pix * g.C + c) = make_uint4(pack_bf2(acc[0], acc[1]), pack_bf2(acc[2], acc[3]),
+                                               pack_bf2(acc[4], acc[5]), pack_bf2(acc[6], acc[7]));
+  }
+}
+
+// ---- BatchNorm: per-channel statistics over rows of a [N][C] (NHWC-flattened) bf16 tensor.
+// Stage 1: block b owns rows [b*R, (b+1)*R).  Thread = (row lane, 8-channel group): 16-B loads,
+// a wave covers 64 groups x 16 B of consecutive memory.  Sums are taken about a per-block pivot
+// (the block's first row) so sum/sum-of-squares do not cancel; lanes are combined in LDS in a
+// fixed order.  Stage 2 merges the block partials in fixed order (Chan) -> mean, rstd, running
+// stats.  No atomics anywhere: statistics are bitwise reproducible run to run.
+__device__ __forceinline__ void ld8f(const bf16_t* p, float* v) {
+  uint4 x = *(const uint4*)p;
+  uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+// mode 0 (forward): a = x            -> out0 = pivot + s1/n (block mean), out1 = M2
+// mode 1 (backward): a = dy, b = y (relu mask, may be null), c = x -> out0 = sum g, out1 = sum g*xhat
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ yb,
+                                                       const bf16_t* __restrict__ xb, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, long long N, int C, int R,
+                                                       int mode, float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float red[2][256][8];
+  const long long r0 = (long long)blockIdx.x * R;
+  const long long r1 = min(N, r0 + R);
+  const int n = (int)max(0LL, r1 - r0);
+  const int cg = C / 8;
+  for (int gbase = 0; gbase < cg; gbase += 256) {
+    const int chunk = min(256, cg - gbase);
+    const int rl = 256 / chunk;
+    const int t = threadIdx.x;
+    const int lane = t / chunk, gi = t % chunk;
+    const int c = (gbase + gi) * 8;
+    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float piv[8], m8[8], r8[8];
+    if (lane < rl && n > 0) {
+      if (mode == 0) {
+        ld8f(a + r0 * C + c, piv);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          m8[e] = mean[c + e];
+          r8[e] = rstd[c + e];
+        }
+      }
+      for (long long r = r0 + lane; r < r1; r += rl) {
+        float v[8];
+        ld8f(a + r * C + c, v);
+        if (mode == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = v[e] - piv[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        } else {
+          float xv[8];
+          ld8f(xb + r * C + c, xv);
+          if (yb) {
+            float yv[8];
+            ld8f(yb + r * C + c, yv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = yv[e] > 0.f ? v[e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += v[e];
+            s2[e] += v[e] * (xv[e] - m8[e]) * r8[e];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][t][e] = s1[e];
+      red[1][t][e] = s2[e];
+    }
+    __syncthreads();
+    if (t < chunk) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float A = 0.f, Bq = 0.f;
+        for (int l = 0; l < rl; ++l) {
+          A += red[0][l * chunk + t][e];
+          Bq += red[1][l * chunk + t][e];
+        }
+        float o0 = A, o1 = Bq;
+        if (mode == 0) {
+          const float p = n > 0 ? bf2f(a[r0 * C + c + e]) : 0.f;
+          o0 = n > 0 ? p + A / n : 0.f;
+          o1 = n > 0 ? fmaxf(Bq - A * A / n, 0.f) : 0.f;
+        }
+        out0[(long long)blockIdx.x * C + c + e] = o0;
+        out1[(long long)blockIdx.x * C + c + e] = o1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// one wave per channel: lanes merge block partials b = lane, lane+64, ... (Chan), then a fixed
+// xor-shuffle tree merges the 64 lane states.
+__global__ __launch_bounds__(64) void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                        int nblk, long long N, int R, int C, float eps, float momentum,
+                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                        float* running_mean, float* running_var) {
+  const int c = blockIdx.x, l = threadIdx.x;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int b = l; b < nblk; b += 64) {
+    const float nb = (float)max(0LL, min((long long)R, N - (long long)b * R));
+    if (nb <= 0.f) break;
+    const float mb = pmean[(long long)b * C + c], m2b = pm2[(long long)b * C + c];
+    const float tot = n + nb, d = mb - mean;
+    mean += d * nb / tot;
+    m2 += m2b + d * d * n * nb / tot;
+    n = tot;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float n2 = __shfl_xor(n, o, 64), mean2 = __shfl_xor(mean, o, 64), m22 = __shfl_xor(m2, o, 64);
+    const float tot = n + n2;
+    if (tot > 0.f) {
+      // symmetric form so both partners compute the identical result
+      const float d = mean2 - mean;
+      const float nm = (n * mean + n2 * mean2) / tot;
+      m2 = m2 + m22 + d * d * (n * n2 / tot);
+      mean = nm;
+      n = tot;
+    }
+  }
+  if (l == 0) {
+    const float var = m2 / n;
+    mean_out[c] = mean;
+    rstd_out[c] = rsqrtf(var + eps);
+    if (running_mean) {
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (n > 1.f ? m2 / (n - 1.f) : var);
+    }
+  }
+}
+
+// y = act((x - mean) * rstd * gamma + beta (+ res)); 8 channels per thread (C % 8 == 0).
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                      bf16_t* __restrict__ y, const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, long long N, int C, int relu) {
+  const long long total = N * (C / 8);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % (C / 8)) * 8;
+    const long long off = (i / (C / 8)) * C + c;
+    uint4 v = *(const uint4*)(x + off);
+    uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    float o[8], rr[8];
+    if (res) {
+      uint4 q = *(const uint4*)(res + off);
+      uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        rr[2 * e] = __uint_as_float(w[e] << 16);
+        rr[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xv = e & 1 ? __uint_as_float(u[e >> 1] & 0xffff0000u) : __uint_as_float(u[e >> 1] << 16);
+      float t = (xv - mean[c + e]) * rstd[c + e] * gamma[c + e] + beta[c + e];
+      if (res) t += rr[e];
+      if (relu) t = fmaxf(t, 0.f);
+      o[e] = t;
+    }
+    *(uint4*)(y + off) = make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
+  }
+}
+
+__global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psumx,
+                                                            int nblk, int C, float* __restrict__ dbeta,
+                                                            float* __restrict__ dgamma) {
+  const int c = blockIdx.x, l = threadIdx.x;
+  float s = 0.f, sx = 0.f;
+  for (int b = l; b < nblk; b += 64) {
+    s += psum[(long long)b * C + c];
+    sx += psumx[(long long)b * C + c];
+  }
+  s = wave_sum(s);
+  sx = wave_sum(sx);
+  if (l == 0) {
+    dbeta[c] = s;
+    dgamma[c] = sx;
+  }
+}
+
+// dx = gamma*rstd/N * (N*g - sum(g) - xhat*sum(g*xhat)); dres = g (when res given). 8 ch/thread.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          const bf16_t* __restrict__ x, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                          const float* __restrict__ dbeta, const float* __restrict__ dgamma,
+                                                          bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long N,
+                                                          int C, int relu) {
+  const long long total = N * (C / 8);
+  const float invN = 1.f / (float)N;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % (C / 8)) * 8;
+    const long long off = (i / (C / 8)) * C + c;
+    float gv[8], xv[8], o[8];
+    ld8f(dy + off, gv);
+    ld8f(x + off, xv);
+    if (relu) {
+      float yv[8];
+      ld8f(y + off, yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (xv[e] - mean[c + e]) * rstd[c + e];
+      o[e] = gamma[c + e] * rstd[c + e] * (gv[e] - dbeta[c + e] * invN - xh * dgamma[c + e] * invN);
+    }
+    *(uint4*)(dx + off) = make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
+    if (dres)
+      *(uint4*)(dres + off) =
+          make_uint4(pack_bf2(gv[0], gv[1]), pack_bf2(gv[2], gv[3]), pack_bf2(gv[4], gv[5]), pack_bf2(gv[6], gv[7]));
+  }
+}
+
+// max pool (KxK, stride s, pad p), NHWC; argmax tap index kept for the backward gather
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ arg, int B, int H, int W, int C, int Ho,
+                                                         int Wo, int K, int s, int p) {
+  const long long total = (long long)B * Ho * Wo * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int wo = (int)(pix % Wo), ho = (int)((pix / Wo) % Ho), b = (int)(pix / ((long long)Wo * Ho));
+    float best = -INFINITY;
+    int bi = 0;
+    for (int kh = 0; kh < K; ++kh)
+      for (int kw = 0; kw < K; ++kw) {
+        const int h = ho * s - p + kh, w = wo * s - p + kw;
+        if (h < 0 || h >= H || w < 0 || w >= W) continue;
+        const float v = bf2f(x[(((long long)b * H + h) * W + w) * C + c]);
+        if (v > best) {
+          best = v;
+          bi = kh * K + kw;
+        }
+      }
+    y[i] = f2bf(best);
+    arg[i] = (uint8_t)bi;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                         bf16_t* __restrict__ dx, int B, int H, int W, int C, int Ho,
+                                                         int Wo, int K, int s, int p) {
+  const long long total = (long long)B * H * W * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H), b = (int)(pix / ((long long)W * H));
+    float acc = 0.f;
+    for (int kh = 0; kh < K; ++kh) {
+      const int hs = h + p - kh;
+      if (hs < 0 || hs % s) continue;
+      const int ho = hs / s;
+      if (ho >= Ho) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int ws = w + p - kw;
+        if (ws < 0 || ws % s) continue;
+        const int wo = ws / s;
+        if (wo >= Wo) continue;
+        const long long o = (((long long)b * Ho + ho) * Wo + wo) * C + c;
+        if (arg[o] == kh * K + kw) acc += bf2f(dy[o]);
+      }
+    }
+    dx[i] = f2bf(acc);
+  }
+}
+
+// global average pool [B][HW][C] -> [B][C] (fp32 accumulate, bf16 out)
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
+                                                         int HW, int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i % C;
+  float s = 0.f;
+  for (int j = 0; j < HW; ++j) s += bf2f(x[((long long)b * HW + j) * C + c]);
+  y[i] = f2bf(s / HW);
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int B,
+                                                         int HW, int C) {
+  const long long total = (long long)B * HW * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int b = (int)(i / ((long long)HW * C));
+    dx[i] = f2bf(bf2f(dy[(long long)b * C + c]) / HW);
+  }
+}
+
+}  // namespace rtdc
+
+using namespace rtdc;
+
+static inline unsigned gsz(long long work) {
+  long long b = (work + 255) / 256;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+extern "C" int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW,
+                           int stride, int pad, int K, int Kp, hipStream_t st) {
+  ConvGeom g{B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp};
+  const int vec = (C % 8 == 0 && Kp % 8 == 0) ? 1 : 0;
+  const long long work = (long long)B * Ho * Wo * (vec ? Kp / 8 : Kp);
+  hipLaunchKernelGGL(im2col_kernel, dim3(gsz(work)), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)cols, g, vec);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW,
+                           int stride, int pad, int K, int Kp, hipStream_t st) {
+  if (C % 8 != 0) return 1;
+  ConvGeom g{B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp};
+  hipLaunchKernelGGL(col2im_kernel, dim3(gsz((long long)B * H * W * (C / 8))), dim3(256), 0, st,
+                     (const bf16_t*)dcols, (bf16_t*)dx, g);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma,
+                           const float* beta, float* running_mean, float* running_var, long long N, int C, float eps,
+                           float momentum, int training, int relu, float* ws, int nblk, hipStream_t st) {
+  if (C % 8 != 0) return 1;
+  if (training) {
+    const int R = (int)((N + nblk - 1) / nblk);
+    hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)nullptr,
+                       (const bf16_t*)nullptr, (const float*)nullptr, (const float*)nullptr, N, C, R, 0, ws,
+                       ws + (long long)nblk * C);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
+                       (const float*)(ws + (long long)nblk * C), nblk, N, R, C, eps, momentum, mean, rstd, running_mean,
+                       running_var);
+  }
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)res,
+                     (bf16_t*)y, (const float*)mean, (const float*)rstd, gamma, beta, N, C, relu);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd,
+                           const float* gamma, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C,
+                           int relu, float* ws, int nblk, hipStream_t st) {
+  const int R = (int)((N + nblk - 1) / nblk);
+  if (C % 8 != 0) return 1;
+  hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)(relu ? y : nullptr), (const bf16_t*)x, mean, rstd, N, C, R, 1, ws,
+                     ws + (long long)nblk * C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
+                     (const float*)(ws + (long long)nblk * C), nblk, C, dbeta, dgamma);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                     (const bf16_t*)x, mean, rstd, gamma, (const float*)dbeta, (const float*)dgamma, (bf16_t*)dx,
+                     (bf16_t*)dres, N, C, relu);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, int B, int H, int W, int C,
+                            int Ho, int Wo, int K, int s, int p, int backward, hipStream_t st) {
+  if (!backward)
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(gsz((long long)B * Ho * Wo * C)), dim3(256), 0, st, (const bf16_t*)x,
+                       (bf16_t*)y, (uint8_t*)arg, B, H, W, C, Ho, Wo, K, s, p);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(gsz((long long)B * H * W * C)), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const uint8_t*)arg, (bf16_t*)dx, B, H, W, C, Ho, Wo, K, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st) {
+  if (!backward)
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((B * C + 255) / 256), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y, B,
+                       HW, C);
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(gsz((long long)B * HW * C)), dim3(256), 0, st, (const bf16_t*)x,
+                       (bf16_t*)y, B, HW, C);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -1,0 +1,156 @@
+"""ResNet-18 (BASELINE config 2: "ResNet-18 DDP bf16 on 2xMI355X, sharded DCP save every N
+steps") on the native channels-last kernels (ops/cnn.py).
+
+No torchvision in this image, so the network is defined here with the standard ResNet-18
+topology (7x7/2 stem + 3x3/2 max-pool, four stages of two BasicBlocks with 64/128/256/512
+channels, 1x1/2 projection shortcuts, global average pool, FC) and the usual state-dict keys
+(`conv1.weight`, `bn1.running_mean`, `layer2.0.downsample.1.weight`, `fc.bias`, ...), so a
+checkpoint lines up with any other ResNet-18 of the same class count.  10 classes -> 11.18 M
+parameters.
+
+On the GPU activations are NHWC bf16 end to end: the input NCHW fp32 batch is converted once,
+every BatchNorm is fused with its ReLU (and with the residual add + ReLU at the end of a
+block).  On CPU the same module runs the fp32 PyTorch reference ops (gloo/CPU tests).
+BatchNorm running statistics are buffers: DDP broadcasts them from rank 0 before every
+forward and they are part of the DCP checkpoint.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..ops import cnn
+
+
+class BatchNorm2d(nn.Module):
+    """BatchNorm over the channel axis of NHWC activations, optionally fused with a residual
+    add and ReLU: y = relu?(BN(x) + residual?)."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def forward(self, x, residual=None, relu: bool = False):
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        return cnn.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
+                              self.momentum, self.eps, residual=residual, relu=relu)
+
+    def extra_repr(self):
+        return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, layout=NHWC"
+
+
+class Conv2d(nn.Module):
+    def __init__(self, cin: int, cout: int, k: int, stride: int = 1, pad: int = 0):
+        super().__init__()
+        self.stride, self.pad = stride, pad
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        nn.init.kaiming_normal_(self.weight, mode="fan_out", nonlinearity="relu")
+
+    def forward(self, x):
+        return cnn.conv2d(x, self.weight, self.stride, self.pad)
+
+    def extra_repr(self):
+        o, i, k, _ = self.weight.shape
+        return f"{i}, {o}, kernel_size={k}, stride={self.stride}, padding={self.pad}, bias=False, layout=NHWC"
+
+
+class Downsample(nn.Sequential):
+    """1x1/stride projection + BN, keys `downsample.0.weight`, `downsample.1.*`."""
+
+    def __init__(self, cin, cout, stride):
+        super().__init__(Conv2d(cin, cout, 1, stride, 0), BatchNorm2d(cout))
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, cin: int, cout: int, stride: int = 1):
+        super().__init__()
+        self.conv1 = Conv2d(cin, cout, 3, stride, 1)
+        self.bn1 = BatchNorm2d(cout)
+        self.conv2 = Conv2d(cout, cout, 3, 1, 1)
+        self.bn2 = BatchNorm2d(cout)
+        self.downsample = Downsample(cin, cout, stride) if (stride != 1 or cin != cout) else None
+
+    def forward(self, x):
+        h = self.bn1(self.conv1(x), relu=True)
+        sc = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
+        return self.bn2(self.conv2(h), residual=sc, relu=True)
+
+
+class ResNet18(nn.Module):
+    def __init__(self, num_classes: int = 10, in_channels: int = 3, widths=(64, 128, 256, 512)):
+        super().__init__()
+        self.num_classes = num_classes
+        self.conv1 = Conv2d(in_channels, widths[0], 7, 2, 3)
+        self.bn1 = BatchNorm2d(widths[0])
+        cin = widths[0]
+        for i, w in enumerate(widths):
+            stride = 1 if i == 0 else 2
+            setattr(self, f"layer{i + 1}", nn.Sequential(BasicBlock(cin, w, stride), BasicBlock(w, w, 1)))
+            cin = w
+        self.fc_in = cin
+        self.fc = _FC(cin, num_classes)
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def forward(self, x):
+        """x: NCHW images (any float dtype).  Returns [B, num_classes] logits."""
+        if x.is_cuda:
+            h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+        else:
+            h = x.permute(0, 2, 3, 1).float().contiguous()
+        h = self.bn1(self.conv1(h), relu=True)
+        h = cnn.max_pool2d(h, 3, 2, 1)
+        h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
+        return self.fc(cnn.global_avg_pool(h))
+
+    def flops_per_sample(self, hw: int = 224) -> float:
+        """Training FLOPs (3x forward MACs x 2) at a square input of side `hw`."""
+        macs = 0
+        for m, (ho, wo) in _spatial_sizes(self, hw).items():
+            o, i, k, _ = m.weight.shape
+            macs += o * i * k * k * ho * wo
+        macs += self.fc_in * self.num_classes
+        return 6.0 * macs
+
+
+class _FC(nn.Module):
+    def __init__(self, cin, n):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(n, cin))
+        self.bias = nn.Parameter(torch.empty(n))
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        bound = 1 / math.sqrt(cin)
+        nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):
+        return cnn.classifier(x, self.weight, self.bias)
+
+
+def _spatial_sizes(model: ResNet18, hw: int) -> dict:
+    out = {}
+
+    def conv_out(m, h):
+        k = m.weight.shape[-1]
+        return (h + 2 * m.pad - k) // m.stride + 1
+
+    h = conv_out(model.conv1, hw)
+    out[model.conv1] = (h, h)
+    h = (h + 2 - 3) // 2 + 1  # max-pool
+    for li in range(1, 5):
+        for blk in getattr(model, f"layer{li}"):
+            h1 = conv_out(blk.conv1, h)
+            out[blk.conv1] = (h1, h1)
+            out[blk.conv2] = (h1, h1)
+            if blk.downsample is not None:
+                out[blk.downsample[0]] = (h1, h1)
+            h = h1
+    return out

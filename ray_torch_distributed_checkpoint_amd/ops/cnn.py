@@ -1,0 +1,267 @@
+"""Convolution, BatchNorm and pooling on the native gfx950 kernels (channels-last bf16).
+
+Reference workload: BASELINE config 2, "ResNet-18 DDP bf16 on 2xMI355X" (SURVEY.md §2 row
+"conv 7x7/3x3/1x1 fwd + dgrad + wgrad, BatchNorm2d fwd/bwd + running stats, max/avg-pool,
+FC, CE").  torchvision is not available here, so the ops are defined from scratch.
+
+Design (NHWC, so the GEMM reduction axis (kh, kw, c) is contiguous in memory):
+
+* `conv2d` - im2col (16-B vector gathers; zero-padded to K % 64 and M % 64) -> MFMA GEMM
+  `cols[M, Kp] . Wmat[Cout, Kp]^T`.  Backward: weight gradient = split-K MN x MN GEMM
+  `dY^T . cols` (fp32), input gradient = `dY . Wmat` then a deterministic col2im gather.
+  1x1/stride-1 convolutions skip im2col entirely (the NHWC activation IS the column matrix).
+  Weights stay in the torch layout `[Cout, Cin, KH, KW]` (so state_dicts match the usual
+  ResNet naming); the bf16 `[Cout, KH*KW*Cin]` GEMM operand is rebuilt from the bf16 shadow
+  each forward (<= 4.7 MB per conv).
+* `batch_norm` - two-stage deterministic channel statistics (pivot-shifted block sums, Chan
+  merge), apply fused with the residual add and ReLU; backward fuses the ReLU mask and emits
+  the residual-branch gradient in the same pass.
+* `max_pool2d` (uint8 argmax, gather backward) and `global_avg_pool`.
+
+CPU tensors run the PyTorch reference of every op (NHWC in, NHWC out).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import gemm as G
+from ._ext import gpu_ext
+from .shadow import shadow_of
+
+
+def _ceil(a: int, m: int) -> int:
+    return (a + m - 1) // m * m
+
+
+def _out_hw(H, W, KH, KW, stride, pad):
+    return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+
+
+def _weight_matrix(w: torch.Tensor, Kp: int) -> torch.Tensor:
+    """bf16 GEMM operand [Cout, Kp] with k = (kh*KW + kw)*Cin + c (zero-padded columns)."""
+    s = shadow_of(w)
+    Cout = s.shape[0]
+    m = s.permute(0, 2, 3, 1).reshape(Cout, -1)
+    if m.shape[1] != Kp:
+        m = F.pad(m, (0, Kp - m.shape[1]))
+    return m.contiguous()
+
+
+def _rows_padded(t: torch.Tensor, Mp: int) -> torch.Tensor:
+    if t.shape[0] == Mp:
+        return t
+    out = torch.zeros((Mp, t.shape[1]), dtype=t.dtype, device=t.device)
+    out[: t.shape[0]].copy_(t)
+    return out
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        B, H, W, C = x.shape
+        Cout, Cin, KH, KW = w.shape
+        assert Cin == C, (x.shape, w.shape)
+        Ho, Wo = _out_hw(H, W, KH, KW, stride, pad)
+        K = KH * KW * C
+        Kp = _ceil(K, 64)
+        M = B * Ho * Wo
+        Mp = _ceil(M, 64)
+        x = x.contiguous()
+        direct = KH == 1 and KW == 1 and stride == 1 and pad == 0 and K == Kp and M == Mp
+        if direct:
+            cols = x.view(M, C)
+        else:
+            cols = torch.empty((Mp, Kp), dtype=torch.bfloat16, device=x.device)
+            if Mp > M:
+                cols[M:].zero_()
+            gpu_ext().im2col(x, cols[:M] if Mp > M else cols, Ho, Wo, KH, KW, stride, pad)
+        wm = _weight_matrix(w, Kp)
+        y = G.linear_fwd(cols, wm)  # [Mp, Cout]
+        ctx.save_for_backward(cols, wm)
+        ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, direct)
+        return y[:M].view(B, Ho, Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, wm = ctx.saved_tensors
+        B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, direct = ctx.geom
+        Cout = wm.shape[0]
+        dy2 = _rows_padded(dy.reshape(M, Cout).contiguous(), Mp)
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
+            dw = dwm[:, :K].view(Cout, KH, KW, C).permute(0, 3, 1, 2).contiguous()
+        if ctx.needs_input_grad[0]:
+            dcols = G.linear_dgrad(dy2, wm)  # [Mp, Kp] bf16
+            if direct:
+                dx = dcols.view(B, H, W, C)
+            else:
+                dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
+                gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
+        return dx, dw, None, None
+
+
+def conv2d_ref(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.to(x.dtype), stride=stride, padding=pad)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
+    """NHWC convolution (no bias): x [B, H, W, Cin] -> [B, Ho, Wo, Cout]; w [Cout, Cin, KH, KW]."""
+    if not x.is_cuda or x.dtype != torch.bfloat16:
+        return conv2d_ref(x, w, stride, pad)
+    return _Conv2d.apply(x, w, stride, pad)
+
+
+def _bn_blocks(N: int, C: int) -> int:
+    # ~32 16-B loads per thread in the statistics pass; bounded so the merge stays cheap
+    return max(1, min(2048, (N * C) // (256 * 8 * 32)))
+
+
+class _BatchNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu):
+        C = x.shape[-1]
+        x = x.contiguous()
+        N = x.numel() // C
+        y = torch.empty_like(x)
+        if training:
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+            nblk = _bn_blocks(N, C)
+            ws = G.workspace(x.device, 2 * nblk * C, "bn")
+        else:
+            mean = running_mean.float()
+            rstd = torch.rsqrt(running_var.float() + eps)
+            nblk, ws = 1, G.workspace(x.device, 2 * C, "bn")
+        res = residual.contiguous() if residual is not None else None
+        gpu_ext().bn_fwd(x, res, y, mean, rstd, weight, bias, running_mean if training else None,
+                         running_var if training else None, eps, momentum, training, relu, ws, nblk)
+        ctx.save_for_backward(x, y if relu else None, mean, rstd, weight)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd, weight = ctx.saved_tensors
+        C = x.shape[-1]
+        N = x.numel() // C
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        nblk = _bn_blocks(N, C)
+        ws = G.workspace(x.device, 2 * nblk * C, "bn")
+        gpu_ext().bn_bwd(dy, y if ctx.relu else x, x, mean, rstd, weight, dx, dres, dgamma, dbeta, ctx.relu, ws, nblk)
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+def batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5,
+                   residual=None, relu=False):
+    y = F.batch_norm(x.permute(0, 3, 1, 2).float(), running_mean, running_var, weight, bias, training, momentum, eps)
+    y = y.permute(0, 2, 3, 1).to(x.dtype)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = torch.relu(y)
+    return y.contiguous()
+
+
+def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
+               eps: float = 1e-5, residual=None, relu: bool = False) -> torch.Tensor:
+    """y = relu?(BN(x) (+ residual)) over the channel (last) axis of an NHWC tensor."""
+    if not x.is_cuda or x.dtype != torch.bfloat16:
+        return batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
+    return _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu)
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        B, H, W, C = x.shape
+        Ho, Wo = _out_hw(H, W, k, k, s, p)
+        x = x.contiguous()
+        y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        gpu_ext().maxpool_fwd(x, y, arg, k, s, p)
+        ctx.save_for_backward(arg)
+        ctx.meta = (x.shape, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        shape, k, s, p = ctx.meta
+        dx = torch.empty(shape, dtype=dy.dtype, device=dy.device)
+        gpu_ext().maxpool_bwd(dy.contiguous(), arg, dx, k, s, p)
+        return dx, None, None, None
+
+
+def max_pool2d(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
+    if not x.is_cuda or x.dtype != torch.bfloat16:
+        return F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous()
+    return _MaxPool.apply(x, k, s, p)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, C = x.shape[0], x.shape[-1]
+        x = x.contiguous()
+        y = torch.empty((B, C), dtype=x.dtype, device=x.device)
+        gpu_ext().avgpool(x, y, False)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.empty(ctx.shape, dtype=dy.dtype, device=dy.device)
+        gpu_ext().avgpool(dy.contiguous(), dx, True)
+        return dx
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """[B, H, W, C] -> [B, C] mean over the spatial axes."""
+    if not x.is_cuda or x.dtype != torch.bfloat16:
+        return x.float().mean(dim=(1, 2)).to(x.dtype)
+    return _AvgPool.apply(x)
+
+
+class _Classifier(torch.autograd.Function):
+    """logits[B, N] = x[B, K] . w[N, K]^T + b for small N (class count): the GEMM runs on
+    zero-padded operands (N and B -> multiples of 64: they are reduction axes of the two
+    backward GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        Bn, K = x.shape
+        N = w.shape[0]
+        Np, Mp = _ceil(N, 64), _ceil(Bn, 64)
+        ws = shadow_of(w)
+        wp = F.pad(ws, (0, 0, 0, Np - N)) if Np != N else ws
+        bp = F.pad(b, (0, Np - N)) if Np != N else b
+        xp = _rows_padded(x.contiguous(), Mp)
+        y = G.linear_fwd(xp, wp.contiguous(), bias=bp.contiguous())
+        ctx.save_for_backward(xp, wp)
+        ctx.meta = (Bn, N, Np, Mp)
+        return y[:Bn, :N].contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xp, wp = ctx.saved_tensors
+        Bn, N, Np, Mp = ctx.meta
+        dyp = torch.zeros((Mp, Np), dtype=torch.bfloat16, device=dy.device)
+        dyp[:Bn, :N].copy_(dy)
+        dx = G.linear_dgrad(dyp, wp)[:Bn] if ctx.needs_input_grad[0] else None
+        dw = G.linear_wgrad(dyp, xp)[:N] if ctx.needs_input_grad[1] else None
+        db = G.colsum(dyp)[:N] if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def classifier(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if not x.is_cuda or x.dtype != torch.bfloat16:
+        return F.linear(x, w.to(x.dtype), b.to(x.dtype))
+    return _Classifier.apply(x, w, b)

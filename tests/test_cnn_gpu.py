@@ -1,0 +1,188 @@
+"""Conv / BatchNorm / pooling kernels (ResNet-18 path) vs plain PyTorch fp32 references (GPU)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _close(out, ref, rel, what=""):
+    err = (out.float() - ref.float()).abs().max().item()
+    mag = ref.float().abs().max().item() + 1e-6
+    assert err <= rel * mag, f"{what} max err {err} vs {rel}*{mag}"
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize(
+    "B,H,C,Cout,k,s,p",
+    [
+        (2, 16, 64, 64, 3, 1, 1),  # stage conv
+        (2, 16, 64, 128, 3, 2, 1),  # strided stage entry
+        (2, 16, 64, 128, 1, 2, 0),  # projection shortcut
+        (2, 32, 3, 64, 7, 2, 3),  # stem (C=3: scalar im2col, K padded 147 -> 192)
+        (4, 8, 128, 64, 1, 1, 0),  # 1x1/s1: direct (no im2col)
+        (1, 7, 64, 64, 3, 1, 1),  # M = 49: rows padded to 64
+    ],
+)
+def test_conv2d(B, H, C, Cout, k, s, p):
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(B * H + C + k)
+    x = torch.randn(B, C, H, H, device=DEV)
+    w = torch.randn(Cout, C, k, k, device=DEV) * 0.1
+    xb = x.to(torch.bfloat16)
+    ref_x = xb.float().requires_grad_(C != 3)
+    ref_w = w.to(torch.bfloat16).float().requires_grad_(True)
+    ref = F.conv2d(ref_x, ref_w, stride=s, padding=p)
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+
+    xin = _nhwc(xb).requires_grad_(C != 3)
+    wp = w.clone().requires_grad_(True)
+    y = cnn.conv2d(xin, wp, s, p)
+    assert y.shape == (B, ref.shape[2], ref.shape[3], Cout)
+    _close(y, _nhwc(ref), 0.02, "y")
+    y.backward(_nhwc(gy).to(torch.bfloat16))
+    _close(wp.grad, ref_w.grad, 0.02, "dw")
+    if C != 3:
+        _close(xin.grad, _nhwc(ref_x.grad), 0.03, "dx")
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("B,H,C", [(4, 14, 64), (2, 7, 512), (8, 56, 64)])
+def test_batch_norm_train(relu, res, B, H, C):
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(C + H)
+    x = (torch.randn(B, H, H, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    r = torch.randn(B, H, H, C, device=DEV).to(torch.bfloat16) if res else None
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm.clone(), rv.clone()
+
+    xr = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    ref = F.batch_norm(xr.permute(0, 3, 1, 2), rm2, rv2, gr, br, True, 0.1, 1e-5).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + rr
+    if relu:
+        ref = torch.relu(ref)
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+
+    xi = x.clone().requires_grad_(True)
+    gi, bi = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ri = r.clone().requires_grad_(True) if res else None
+    y = cnn.batch_norm(xi, gi, bi, rm, rv, True, 0.1, 1e-5, residual=ri, relu=relu)
+    _close(y, ref, 0.02, "y")
+    _close(rm, rm2, 1e-4, "running_mean")
+    _close(rv, rv2, 1e-4, "running_var")
+    y.backward(gy.to(torch.bfloat16))
+    _close(xi.grad, xr.grad, 0.03, "dx")
+    _close(gi.grad, gr.grad, 0.01, "dgamma")
+    _close(bi.grad, br.grad, 0.01, "dbeta")
+    if res:
+        _close(ri.grad, rr.grad, 0.01, "dres")
+
+
+def test_batch_norm_eval_and_determinism():
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(3)
+    C = 128
+    x = (torch.randn(16, 28, 28, C, device=DEV) + 3).to(torch.bfloat16)
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    outs = []
+    for _ in range(2):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        outs.append((cnn.batch_norm(x, g, b, rm, rv, True), rm, rv))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    rm, rv = outs[0][1], outs[0][2]
+    y = cnn.batch_norm(x, g, b, rm, rv, False, relu=True)
+    ref = torch.relu(F.batch_norm(x.float().permute(0, 3, 1, 2), rm, rv, g, b, False).permute(0, 2, 3, 1))
+    _close(y, ref, 0.02, "eval")
+
+
+def test_pools_and_classifier():
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(5)
+    x = torch.randn(4, 64, 28, 28, device=DEV).to(torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    xi = _nhwc(x).requires_grad_(True)
+    y = cnn.max_pool2d(xi, 3, 2, 1)
+    _close(y, _nhwc(ref), 1e-6, "maxpool")
+    y.backward(_nhwc(gy).to(torch.bfloat16))
+    _close(xi.grad, _nhwc(xr.grad), 0.01, "maxpool dx")
+
+    xa = torch.randn(6, 7, 7, 512, device=DEV).to(torch.bfloat16)
+    xar = xa.float().requires_grad_(True)
+    ref = xar.mean((1, 2))
+    g2 = torch.randn_like(ref)
+    ref.backward(g2)
+    xai = xa.clone().requires_grad_(True)
+    y = cnn.global_avg_pool(xai)
+    _close(y, ref, 0.01, "avgpool")
+    y.backward(g2.to(torch.bfloat16))
+    _close(xai.grad, xar.grad, 0.01, "avgpool dx")
+
+    h = torch.randn(6, 512, device=DEV).to(torch.bfloat16)
+    w, b = torch.randn(10, 512, device=DEV) * 0.05, torch.randn(10, device=DEV)
+    hr, wr, br = h.float().requires_grad_(True), w.to(torch.bfloat16).float().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = F.linear(hr, wr, br)
+    g3 = torch.randn_like(ref)
+    ref.backward(g3)
+    hi, wi, bi = h.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = cnn.classifier(hi, wi, bi)
+    _close(y, ref, 0.02, "fc")
+    y.backward(g3.to(torch.bfloat16))
+    _close(hi.grad, hr.grad, 0.02, "fc dx")
+    _close(wi.grad, wr.grad, 0.02, "fc dw")
+    _close(bi.grad, br.grad, 0.01, "fc db")
+
+
+def test_resnet18_matches_reference_and_trains():
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.models import ResNet18
+    from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
+
+    torch.manual_seed(0)
+    ref = ResNet18(10)
+    gpu = copy.deepcopy(ref).cuda()
+    x = torch.randn(8, 3, 64, 64)
+    t = torch.randint(0, 10, (8,))
+    lr = F.cross_entropy(ref(x), t)
+    lr.backward()
+    lg = ops.cross_entropy(gpu(x.cuda()), t.cuda())
+    lg.backward()
+    assert abs(lg.item() - lr.item()) < 0.05 * lr.item() + 0.02
+    for (n, p), (_, q) in zip(ref.named_parameters(), gpu.named_parameters()):
+        err = (p.grad - q.grad.cpu()).abs().max().item()
+        mag = p.grad.abs().max().item() + 1e-8
+        assert err < 0.15 * mag, f"{n}: grad err {err} vs {mag}"
+    for (n, b1), (_, b2) in zip(ref.named_buffers(), gpu.named_buffers()):
+        _close(b2.cpu(), b1, 0.02, n)
+
+    opt = FusedSGD(gpu.parameters(), lr=0.05, momentum=0.9)
+    xs = torch.randn(16, 3, 64, 64, device=DEV)
+    ts = torch.randint(0, 10, (16,), device=DEV)
+    losses = []
+    for _ in range(15):
+        opt.zero_grad()
+        l = ops.cross_entropy(gpu(xs), ts)
+        l.backward()
+        opt.step()
+        losses.append(l.item())
+    assert losses[-1] < 0.5 * losses[0], losses
