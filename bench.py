@@ -177,7 +177,7 @@ def build_workload(args, dev, rank):
         hw = args.image_size
         B = args.batch if args.batch_set else 256
         model = ResNet18(num_classes=10).to(dev)
-        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+        opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5)
         pool = [(torch.randn(B, 3, hw, hw, device=dev, generator=g),
                  torch.randint(0, 10, (B,), device=dev, generator=g)) for _ in range(2)]
 

@@ -18,6 +18,7 @@ extern "C" {
 int rtdc_gemm_bf16(const rtdc::GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
                    hipStream_t stream);
 int rtdc_gemm_f32(const rtdc::GemmF32Args* args, hipStream_t st);
+int rtdc_conv_gemm(const rtdc::GemmArgs* args, int mode, hipStream_t stream);
 int rtdc_layernorm_fwd(const void* x, const void* g, const void* b, void* y, float* mean, float* rstd,
                        int M, int D, float eps, hipStream_t st);
 int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rstd, int M, int D, float eps,
@@ -301,6 +302,45 @@ static void swiglu_bwd(Tensor gu, Tensor dh, Tensor dgu) {
 }
 
 // ---------------------------------------------------------------------------------- conv / batchnorm / pooling
+// Implicit-GEMM convolution products (gemm_bf16.hip, rtdc_conv_gemm):
+//   mode 1: C[npix, N] bf16 = im2col(X) . other[N, K]^T          (other K-major, ld = ld_other)
+//   mode 2: C[M, N]    fp32 = other[K, M]^T . im2col(X)           (other = dY, MN-major, ld = ld_other)
+// X is NHWC [B, H, W, Cx]; the window is KH x KW (K = KH*KW*Cx in mode 1, N in mode 2).
+static void conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K, int64_t ld_other,
+                      int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad, c10::optional<Tensor> ws) {
+  check_dev(X, "X");
+  check_dev(other, "other");
+  TORCH_CHECK(X.is_contiguous() && X.dim() == 4 && X.scalar_type() == at::kBFloat16, "conv_gemm: X must be NHWC bf16");
+  TORCH_CHECK(other.scalar_type() == at::kBFloat16 && C.is_contiguous(), "conv_gemm: bad operands");
+  const int64_t npix = X.size(0) * Ho * Wo;
+  if (mode == 1) {
+    TORCH_CHECK(C.scalar_type() == at::kBFloat16 && C.size(0) == npix && C.size(1) == N && M == npix, "conv_gemm: C");
+  } else {
+    TORCH_CHECK(C.scalar_type() == at::kFloat && C.size(0) == M && C.size(1) == N && K >= npix, "conv_gemm: C");
+    TORCH_CHECK(other.size(0) >= K, "conv_gemm: dY must have K (padded) rows");
+  }
+  rtdc::GemmArgs a{};
+  a.A = (const uint16_t*)(mode == 1 ? X.data_ptr() : other.data_ptr());
+  a.B = (const uint16_t*)(mode == 1 ? other.data_ptr() : X.data_ptr());
+  a.C = C.data_ptr();
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.lda = mode == 1 ? 0 : (int)ld_other;
+  a.ldb = mode == 1 ? (int)ld_other : 0;
+  a.ldc = (int)N;
+  a.batch_inner = 1;
+  a.alpha = 1.f;
+  a.beta = 0.f;
+  a.tile_cfg = -1;
+  if (ws.has_value()) {
+    a.ws = ws->data_ptr<float>();
+    a.ws_elems = ws->numel();
+  }
+  a.cv_H = (int)X.size(1); a.cv_W = (int)X.size(2); a.cv_C = (int)X.size(3);
+  a.cv_Ho = (int)Ho; a.cv_Wo = (int)Wo; a.cv_KW = (int)KW; a.cv_stride = (int)stride; a.cv_pad = (int)pad;
+  a.cv_npix = (int)npix;
+  check_rc(rtdc_conv_gemm(&a, (int)mode, cur_stream()), "conv_gemm");
+}
+
 // x: NHWC bf16 [B,H,W,C]; cols: [B*Ho*Wo, Kp] with K = KH*KW*C real columns (rest zero).
 static void im2col(Tensor x, Tensor cols, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
   TORCH_CHECK(x.is_contiguous() && cols.is_contiguous() && x.dim() == 4, "im2col: contiguous NHWC expected");
@@ -439,6 +479,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("im2col", &im2col);
+  m.def("conv_gemm", &conv_gemm);
   m.def("col2im", &col2im);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);

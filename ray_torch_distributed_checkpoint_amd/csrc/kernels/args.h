@@ -26,6 +26,10 @@ struct GemmArgs {
   long long ws_elems;
   int splitk;     // set by the launcher
   int tile_cfg;   // -1 = auto; else force a tile configuration (benchmarks)
+  // implicit-GEMM convolution (rtdc_conv_gemm): operand gathered from an NHWC tensor
+  // X [B][cv_H][cv_W][cv_C] through a KHxKW window (stride, pad) over a cv_Ho x cv_Wo grid of
+  // cv_npix output pixels.  Mode 1: A(m = pixel, k = tap*C + c), mode 2: B(k = pixel, n = tap*C + c).
+  int cv_H, cv_W, cv_C, cv_Ho, cv_Wo, cv_KW, cv_stride, cv_pad, cv_npix;
 };
 
 // fp32 MFMA GEMM (gemm_f32.hip)

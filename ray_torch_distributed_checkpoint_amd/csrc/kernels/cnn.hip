@@ -15,73 +15,117 @@ struct ConvGeom {
   int B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp;
 };
 
+// All element/chunk counts handled below are < 2^31 (checked by the launchers), so index
+// arithmetic is 32-bit: 64-bit integer division is a long software sequence on CDNA.
+
 // cols[(b,ho,wo)][k], k = (kh*KW + kw)*C + c ; zero for k >= K and for padding taps.
 __global__ __launch_bounds__(256) void im2col_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ cols,
                                                     ConvGeom g, int vec) {
-  const long long rows = (long long)g.B * g.Ho * g.Wo;
+  const int rows = g.B * g.Ho * g.Wo;
   const int per_row = vec ? g.Kp / 8 : g.Kp;
-  const long long total = rows * per_row;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long r = i / per_row;
-    const int kk = (int)(i % per_row) * (vec ? 8 : 1);
-    const int wo = (int)(r % g.Wo);
-    const int ho = (int)((r / g.Wo) % g.Ho);
-    const int b = (int)(r / ((long long)g.Wo * g.Ho));
+  const int total = rows * per_row;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = i / per_row;
+    const int kk = (i - r * per_row) * (vec ? 8 : 1);
+    const int q = r / g.Wo, wo = r - q * g.Wo;
+    const int b = q / g.Ho, ho = q - b * g.Ho;
+    bf16_t* dst = cols + (size_t)r * g.Kp + kk;
     if (vec) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (kk < g.K) {
-        const int c = kk % g.C, tap = kk / g.C, kw = tap % g.KW, kh = tap / g.KW;
+        const int tap = kk / g.C, c = kk - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
         const int h = ho * g.stride - g.pad + kh, w = wo * g.stride - g.pad + kw;
-        if (h >= 0 && h < g.H && w >= 0 && w < g.W)
-          v = *(const uint4*)(x + (((long long)b * g.H + h) * g.W + w) * g.C + c);
+        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+          v = *(const uint4*)(x + ((size_t)(b * g.H + h) * g.W + w) * g.C + c);
       }
-      *(uint4*)(cols + r * g.Kp + kk) = v;
+      *(uint4*)dst = v;
     } else {
       bf16_t v = 0;
       if (kk < g.K) {
-        const int c = kk % g.C, tap = kk / g.C, kw = tap % g.KW, kh = tap / g.KW;
+        const int tap = kk / g.C, c = kk - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
         const int h = ho * g.stride - g.pad + kh, w = wo * g.stride - g.pad + kw;
-        if (h >= 0 && h < g.H && w >= 0 && w < g.W) v = x[(((long long)b * g.H + h) * g.W + w) * g.C + c];
+        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) v = x[((size_t)(b * g.H + h) * g.W + w) * g.C + c];
       }
-      cols[r * g.Kp + kk] = v;
+      *dst = v;
     }
   }
+}
+
+// Small-channel stem (C = 3, 7x7): one thread per 8-element (16-B) chunk of a column row;
+// the (tap, c) decomposition divides by compile-time constants, stores are full 16 B.
+template <int C, int KW>
+__global__ __launch_bounds__(256) void im2col_small_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ cols,
+                                                          ConvGeom g) {
+  const int per_row = g.Kp / 8;
+  const int total = g.B * g.Ho * g.Wo * per_row;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = i / per_row;
+    const int k0 = (i - r * per_row) * 8;
+    const int q = r / g.Wo, wo = r - q * g.Wo;
+    const int b = q / g.Ho, ho = q - b * g.Ho;
+    const int hb = ho * g.stride - g.pad, wb = wo * g.stride - g.pad;
+    const bf16_t* xb = x + (size_t)b * g.H * g.W * C;
+    uint32_t u[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      uint32_t pair = 0;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int k = k0 + 2 * e2 + h2;
+        uint32_t v = 0;
+        if (k < g.K) {
+          const int tap = k / C, c = k - tap * C, kh = tap / KW, kw = tap - kh * KW;
+          const int h = hb + kh, w = wb + kw;
+          if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) v = xb[(h * g.W + w) * C + c];
+        }
+        pair |= v << (16 * h2);
+      }
+      u[e2] = pair;
+    }
+    *(uint4*)(cols + (size_t)r * g.Kp + k0) = make_uint4(u[0], u[1], u[2], u[3]);
+  }
+}
+
+__device__ __forceinline__ void acc8(float* acc, uint4 v) {
+  uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    acc[2 * e] += __uint_as_float(u[e] << 16);
+    acc[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* o) {
+  return make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
 }
 
 // dx[b,h,w,c] = sum_{kh,kw} dcols[(b,ho,wo)][(kh,kw,c)] over taps with ho*s - p + kh = h.
 // 8 channels per thread (C % 8 == 0).
 __global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx,
                                                     ConvGeom g) {
-  const long long total = (long long)g.B * g.H * g.W * (g.C / 8);
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % (g.C / 8)) * 8;
-    const long long pix = i / (g.C / 8);
-    const int w = (int)(pix % g.W);
-    const int h = (int)((pix / g.W) % g.H);
-    const int b = (int)(pix / ((long long)g.W * g.H));
+  const int cg = g.C / 8;
+  const int total = g.B * g.H * g.W * cg;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / cg, c = (i - pix * cg) * 8;
+    const int q = pix / g.W, w = pix - q * g.W;
+    const int b = q / g.H, h = q - b * g.H;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kh = 0; kh < g.KH; ++kh) {
       const int hs = h + g.pad - kh;
-      if (hs < 0 || hs % g.stride) continue;
+      if (hs < 0) break;
+      if (hs % g.stride) continue;
       const int ho = hs / g.stride;
       if (ho >= g.Ho) continue;
       for (int kw = 0; kw < g.KW; ++kw) {
         const int ws = w + g.pad - kw;
-        if (ws < 0 || ws % g.stride) continue;
+        if (ws < 0) break;
+        if (ws % g.stride) continue;
         const int wo = ws / g.stride;
         if (wo >= g.Wo) continue;
-        const long long r = ((long long)b * g.Ho + ho) * g.Wo + wo;
-        uint4 v = *(const uint4*)(dcols + r * g.Kp + (kh * g.KW + kw) * g.C + c);
-        uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[2 * e] += __uint_as_float(u[e] << 16);
-          acc[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
-        }
+        const int r = (b * g.Ho + ho) * g.Wo + wo;
+        acc8(acc, *(const uint4*)(dcols + (size_t)r * g.Kp + (kh * g.KW + kw) * g.C + c));
       }
     }
-    *(uint4*)(dx + pix * g.C + c) = make_uint4(pack_bf2(acc[0], acc[1]), pack_bf2(acc[2], acc[3]),
-                                               pack_bf2(acc[4], acc[5]), pack_bf2(acc[6], acc[7]));
+    *(uint4*)(dx + (size_t)pix * g.C + c) = pack8(acc);
   }
 }
 
@@ -231,10 +275,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
                                                       bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                       const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, long long N, int C, int relu) {
-  const long long total = N * (C / 8);
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % (C / 8)) * 8;
-    const long long off = (i / (C / 8)) * C + c;
+  const int cg = C / 8;
+  const int total = (int)(N * cg);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int row = i / cg, c = (i - row * cg) * 8;
+    const size_t off = (size_t)row * C + c;
     uint4 v = *(const uint4*)(x + off);
     uint32_t u[4] = {v.x, v.y, v.z, v.w};
     float o[8], rr[8];
@@ -283,11 +328,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                           const float* __restrict__ dbeta, const float* __restrict__ dgamma,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long N,
                                                           int C, int relu) {
-  const long long total = N * (C / 8);
+  const int cg = C / 8;
+  const int total = (int)(N * cg);
   const float invN = 1.f / (float)N;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % (C / 8)) * 8;
-    const long long off = (i / (C / 8)) * C + c;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int row = i / cg, c = (i - row * cg) * 8;
+    const size_t off = (size_t)row * C + c;
     float gv[8], xv[8], o[8];
     ld8f(dy + off, gv);
     ld8f(x + off, xv);
@@ -309,56 +355,82 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   }
 }
 
-// max pool (KxK, stride s, pad p), NHWC; argmax tap index kept for the backward gather
+// max pool (KxK, stride s, pad p), NHWC, 8 channels per thread; the argmax tap index (uint8)
+// is kept for the backward gather.  Ties keep the first tap in (kh, kw) order (= PyTorch).
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          uint8_t* __restrict__ arg, int B, int H, int W, int C, int Ho,
                                                          int Wo, int K, int s, int p) {
-  const long long total = (long long)B * Ho * Wo * C;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    const long long pix = i / C;
-    const int wo = (int)(pix % Wo), ho = (int)((pix / Wo) % Ho), b = (int)(pix / ((long long)Wo * Ho));
-    float best = -INFINITY;
-    int bi = 0;
-    for (int kh = 0; kh < K; ++kh)
+  const int cg = C / 8;
+  const int total = B * Ho * Wo * cg;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / cg, c = (i - pix * cg) * 8;
+    const int q = pix / Wo, wo = pix - q * Wo;
+    const int b = q / Ho, ho = q - b * Ho;
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      bi[e] = 0;
+    }
+    for (int kh = 0; kh < K; ++kh) {
+      const int h = ho * s - p + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
       for (int kw = 0; kw < K; ++kw) {
-        const int h = ho * s - p + kh, w = wo * s - p + kw;
-        if (h < 0 || h >= H || w < 0 || w >= W) continue;
-        const float v = bf2f(x[(((long long)b * H + h) * W + w) * C + c]);
-        if (v > best) {
-          best = v;
-          bi = kh * K + kw;
-        }
+        const int w = wo * s - p + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        acc8(v, *(const uint4*)(x + ((size_t)(b * H + h) * W + w) * C + c));
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) {
+            best[e] = v[e];
+            bi[e] = kh * K + kw;
+          }
       }
-    y[i] = f2bf(best);
-    arg[i] = (uint8_t)bi;
+    }
+    const size_t o = (size_t)pix * C + c;
+    *(uint4*)(y + o) = pack8(best);
+    *(uint2*)(arg + o) = make_uint2(bi[0] | bi[1] << 8 | bi[2] << 16 | bi[3] << 24,
+                                    bi[4] | bi[5] << 8 | bi[6] << 16 | bi[7] << 24);
   }
 }
 
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                          bf16_t* __restrict__ dx, int B, int H, int W, int C, int Ho,
                                                          int Wo, int K, int s, int p) {
-  const long long total = (long long)B * H * W * C;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    const long long pix = i / C;
-    const int w = (int)(pix % W), h = (int)((pix / W) % H), b = (int)(pix / ((long long)W * H));
-    float acc = 0.f;
+  const int cg = C / 8;
+  const int total = B * H * W * cg;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / cg, c = (i - pix * cg) * 8;
+    const int q = pix / W, w = pix - q * W;
+    const int b = q / H, h = q - b * H;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kh = 0; kh < K; ++kh) {
       const int hs = h + p - kh;
-      if (hs < 0 || hs % s) continue;
+      if (hs < 0) break;
+      if (hs % s) continue;
       const int ho = hs / s;
       if (ho >= Ho) continue;
       for (int kw = 0; kw < K; ++kw) {
         const int ws = w + p - kw;
-        if (ws < 0 || ws % s) continue;
+        if (ws < 0) break;
+        if (ws % s) continue;
         const int wo = ws / s;
         if (wo >= Wo) continue;
-        const long long o = (((long long)b * Ho + ho) * Wo + wo) * C + c;
-        if (arg[o] == kh * K + kw) acc += bf2f(dy[o]);
+        const size_t o = ((size_t)(b * Ho + ho) * Wo + wo) * C + c;
+        const uint2 a8 = *(const uint2*)(arg + o);
+        float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        acc8(g, *(const uint4*)(dy + o));
+        const uint32_t tap = kh * K + kw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ae = ((e < 4 ? a8.x : a8.y) >> (8 * (e & 3))) & 0xffu;
+          if (ae == tap) acc[e] += g[e];
+        }
       }
     }
-    dx[i] = f2bf(acc);
+    *(uint4*)(dx + (size_t)pix * C + c) = pack8(acc);
   }
 }
 
@@ -367,19 +439,19 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restri
                                                          int HW, int C) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= B * C) return;
-  const int b = i / C, c = i % C;
+  const int b = i / C, c = i - b * C;
   float s = 0.f;
-  for (int j = 0; j < HW; ++j) s += bf2f(x[((long long)b * HW + j) * C + c]);
+  for (int j = 0; j < HW; ++j) s += bf2f(x[((size_t)b * HW + j) * C + c]);
   y[i] = f2bf(s / HW);
 }
 
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int B,
                                                          int HW, int C) {
-  const long long total = (long long)B * HW * C;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    const int b = (int)(i / ((long long)HW * C));
-    dx[i] = f2bf(bf2f(dy[(long long)b * C + c]) / HW);
+  const int total = B * HW * C;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int c = i % C;
+    const int b = i / (HW * C);
+    dx[i] = f2bf(bf2f(dy[b * C + c]) / HW);
   }
 }
 
@@ -399,13 +471,19 @@ extern "C" int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C
   ConvGeom g{B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp};
   const int vec = (C % 8 == 0 && Kp % 8 == 0) ? 1 : 0;
   const long long work = (long long)B * Ho * Wo * (vec ? Kp / 8 : Kp);
+  if (work >= (1LL << 31) || (long long)B * H * W * C >= (1LL << 31)) return 1;
+  if (C == 3 && KW == 7 && Kp % 8 == 0) {
+    hipLaunchKernelGGL((im2col_small_kernel<3, 7>), dim3(gsz((long long)B * Ho * Wo * (Kp / 8))), dim3(256), 0, st,
+                       (const bf16_t*)x, (bf16_t*)cols, g);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   hipLaunchKernelGGL(im2col_kernel, dim3(gsz(work)), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)cols, g, vec);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 extern "C" int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW,
                            int stride, int pad, int K, int Kp, hipStream_t st) {
-  if (C % 8 != 0) return 1;
+  if (C % 8 != 0 || (long long)B * Ho * Wo * Kp >= (1LL << 31) || (long long)B * H * W * C >= (1LL << 31)) return 1;
   ConvGeom g{B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp};
   hipLaunchKernelGGL(col2im_kernel, dim3(gsz((long long)B * H * W * (C / 8))), dim3(256), 0, st,
                      (const bf16_t*)dcols, (bf16_t*)dx, g);
@@ -415,7 +493,7 @@ extern "C" int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int
 extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma,
                            const float* beta, float* running_mean, float* running_var, long long N, int C, float eps,
                            float momentum, int training, int relu, float* ws, int nblk, hipStream_t st) {
-  if (C % 8 != 0) return 1;
+  if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
   if (training) {
     const int R = (int)((N + nblk - 1) / nblk);
     hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)nullptr,
@@ -434,7 +512,7 @@ extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const f
                            const float* gamma, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C,
                            int relu, float* ws, int nblk, hipStream_t st) {
   const int R = (int)((N + nblk - 1) / nblk);
-  if (C % 8 != 0) return 1;
+  if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
   hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)(relu ? y : nullptr), (const bf16_t*)x, mean, rstd, N, C, R, 1, ws,
                      ws + (long long)nblk * C);
@@ -448,16 +526,18 @@ extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const f
 
 extern "C" int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, int B, int H, int W, int C,
                             int Ho, int Wo, int K, int s, int p, int backward, hipStream_t st) {
+  if (C % 8 != 0 || K * K > 255 || (long long)B * H * W * C >= (1LL << 31)) return 1;
   if (!backward)
-    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(gsz((long long)B * Ho * Wo * C)), dim3(256), 0, st, (const bf16_t*)x,
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(gsz((long long)B * Ho * Wo * C / 8)), dim3(256), 0, st, (const bf16_t*)x,
                        (bf16_t*)y, (uint8_t*)arg, B, H, W, C, Ho, Wo, K, s, p);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(gsz((long long)B * H * W * C)), dim3(256), 0, st, (const bf16_t*)dy,
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(gsz((long long)B * H * W * C / 8)), dim3(256), 0, st, (const bf16_t*)dy,
                        (const uint8_t*)arg, (bf16_t*)dx, B, H, W, C, Ho, Wo, K, s, p);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 extern "C" int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st) {
+  if ((long long)B * HW * C >= (1LL << 31)) return 1;
   if (!backward)
     hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((B * C + 255) / 256), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y, B,
                        HW, C);

@@ -34,6 +34,8 @@
 #include "common.h"
 #include "args.h"
 
+#include <type_traits>
+
 namespace rtdc {
 
 namespace gemm {
@@ -57,11 +59,17 @@ struct TileCfg {
 __device__ __forceinline__ int kmaj_off(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
-// MN-major image: 64 k-rows x (2*ROWS) B.  Chunk c of k-row kr lives at c ^ f(kr) (f < 16
-// keeps it in the same 256-B half); a 32-lane half of ds_read_b64_tr_b16 reads 8 k-rows x 2
-// chunks -> 16 distinct 16-B bank slots (k-rows start on the same bank: stride 256/512 B).
+// MN-major image: 64 k-rows x (2*ROWS) B.  Chunk c of k-row kr lives at c ^ f(kr); a 32-lane
+// half of ds_read_b64_tr_b16 reads 8 k-rows {q, 8+q : q < 4} x 2 chunks -> 16 distinct 16-B
+// bank slots.  ROWS >= 128 (k-rows start on the same bank, stride 256/512 B): f < 16 keeps the
+// chunk inside its row.  ROWS = 64 (128-B k-rows, two per bank row: kr&1 already separates
+// halves): f in {0,2,4,6} from bits 1 and 3 of kr.
+template <int ROWS>
 __device__ __forceinline__ int mnmaj_swz(int kr) {
-  return ((kr & 3) | (((kr >> 3) & 1) << 2)) << 1;
+  if constexpr (ROWS >= 128)
+    return ((kr & 3) | (((kr >> 3) & 1) << 2)) << 1;
+  else
+    return (((kr >> 1) & 1) | (((kr >> 3) & 1) << 1)) << 1;
 }
 
 // Per-lane global sources of one operand tile, computed once per block.
@@ -86,7 +94,7 @@ struct Stager {
         constexpr int CPR = ROWS / 8;     // 16-B chunks per k-row
         constexpr int KRP = 1024 / (ROWS * 2);  // k-rows per piece
         const int kr = piece * KRP + lane / CPR;
-        const int lchunk = (lane % CPR) ^ mnmaj_swz(kr);
+        const int lchunk = (lane % CPR) ^ mnmaj_swz<ROWS>(kr);
         int gc = r0 + lchunk * 8;
         gc = gc < rows ? gc : rows - 8;
         src[ii] = X + (long long)kr * ld + gc;
@@ -105,6 +113,108 @@ struct Stager {
   }
 };
 
+// ---- implicit-GEMM convolution stagers ---------------------------------------------------
+// Zero source for taps that fall into the padding (global_load_lds needs a real address).
+__device__ __attribute__((aligned(16))) uint4 g_conv_zero[4];
+
+// q = x / d for 0 <= x < 2^24 via the fp32 reciprocal (one correction step is exact there)
+__device__ __forceinline__ int fdivq(int x, int d, float rd) {
+  int q = (int)((float)x * rd);
+  const int r = x - q * d;
+  q += (r < 0) ? -1 : (r >= d ? 1 : 0);
+  return q;
+}
+
+// Mode 1: A (K-major) = im2col(X) gathered on the fly.  A 64-deep k tile lies inside one tap
+// (C % 64 == 0), so row m of the tile is 128 contiguous bytes of X at pixel
+// (b, ho*s - p + kh, wo*s - p + kw), channels c0..c0+63 - exactly the 8 x 16-B pieces the
+// plain K-major stager moves; out-of-image taps read the zero page.
+template <int ROWS, int NW>
+struct ConvStagerK {
+  static constexpr int PIECES = ROWS / 8, PPW = PIECES / NW;
+  const bf16_t* X;
+  int hb[PPW], wb[PPW], pb[PPW], co[PPW];
+  int H, W, C, KW;
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* Xp, int rows, int r0, int wave, int lane) {
+    X = Xp;
+    H = a.cv_H; W = a.cv_W; C = a.cv_C; KW = a.cv_KW;
+    const float rWo = 1.f / (float)a.cv_Wo, rHo = 1.f / (float)a.cv_Ho;
+#pragma unroll
+    for (int ii = 0; ii < PPW; ++ii) {
+      const int piece = wave * PPW + ii;
+      const int row = piece * 8 + (lane >> 3);
+      const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = r0 + row;
+      gr = gr < rows ? gr : rows - 1;
+      const int q = fdivq(gr, a.cv_Wo, rWo), wo = gr - q * a.cv_Wo;
+      const int b = fdivq(q, a.cv_Ho, rHo), ho = q - b * a.cv_Ho;
+      hb[ii] = ho * a.cv_stride - a.cv_pad;
+      wb[ii] = wo * a.cv_stride - a.cv_pad;
+      pb[ii] = b * H;
+      co[ii] = lchunk * 8;
+    }
+  }
+
+  __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
+    const int tap = k0 / C, c0 = k0 - tap * C, kh = tap / KW, kw = tap - kh * KW;
+#pragma unroll
+    for (int ii = 0; ii < PPW; ++ii) {
+      const int piece = wave * PPW + ii;
+      const int h = hb[ii] + kh, w = wb[ii] + kw;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const bf16_t* src = ok ? X + (size_t)((pb[ii] + h) * W + w) * C + c0 + co[ii] : (const bf16_t*)g_conv_zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// Mode 2: B (MN-major) = im2col(X) with k = output pixel, n = tap*C + c (weight gradient
+// dW = dY^T . im2col(X)).  A lane's 16-B chunk has a fixed (tap, c) for the whole loop; its
+// k-row (pixel) advances by 64 per tile and is decomposed with fp32-reciprocal divisions.
+template <int ROWS, int NW>
+struct ConvStagerMN {
+  static constexpr int PIECES = ROWS / 8, PPW = PIECES / NW;
+  static constexpr int CPR = ROWS / 8, KRP = 1024 / (ROWS * 2);
+  const bf16_t* X;
+  int kr[PPW], dh[PPW], dw[PPW], cc[PPW];
+  int H, W, C, Ho, Wo, stride, npix;
+  float rWo, rHo;
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* Xp, int cols, int c0, int wave, int lane) {
+    X = Xp;
+    H = a.cv_H; W = a.cv_W; C = a.cv_C; Ho = a.cv_Ho; Wo = a.cv_Wo; stride = a.cv_stride; npix = a.cv_npix;
+    rWo = 1.f / (float)Wo;
+    rHo = 1.f / (float)Ho;
+#pragma unroll
+    for (int ii = 0; ii < PPW; ++ii) {
+      const int piece = wave * PPW + ii;
+      kr[ii] = piece * KRP + lane / CPR;
+      const int lchunk = (lane % CPR) ^ mnmaj_swz<ROWS>(kr[ii]);
+      int gc = c0 + lchunk * 8;
+      gc = gc < cols ? gc : cols - 8;
+      const int tap = gc / C, c = gc - tap * C, kh = tap / a.cv_KW, kw = tap - kh * a.cv_KW;
+      dh[ii] = kh - a.cv_pad;
+      dw[ii] = kw - a.cv_pad;
+      cc[ii] = c;
+    }
+  }
+
+  __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
+#pragma unroll
+    for (int ii = 0; ii < PPW; ++ii) {
+      const int piece = wave * PPW + ii;
+      const int pix = k0 + kr[ii];
+      const int q = fdivq(pix, Wo, rWo), wo = pix - q * Wo;
+      const int b = fdivq(q, Ho, rHo), ho = q - b * Ho;
+      const int h = ho * stride + dh[ii], w = wo * stride + dw[ii];
+      const bool ok = pix < npix && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const bf16_t* src = ok ? X + (size_t)((b * H + h) * W + w) * C + cc[ii] : (const bf16_t*)g_conv_zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+    }
+  }
+};
+
 // Fragment for v_mfma_f32_16x16x32_bf16: lane l holds X(row = R0 + (l&15), k = ks*32 + 8(l>>4) + j).
 template <bool KMAJOR, int ROWS>
 __device__ __forceinline__ bf16x8 load_frag(const char* lds_tile, int R0, int ks, int lane) {
@@ -119,7 +229,7 @@ __device__ __forceinline__ bf16x8 load_frag(const char* lds_tile, int R0, int ks
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int kr = ks * 32 + 8 * g + 4 * h + q;
-      const int off = kr * (ROWS * 2) + ((c ^ mnmaj_swz(kr)) << 4) + ((p & 1) << 3);
+      const int off = kr * (ROWS * 2) + ((c ^ mnmaj_swz<ROWS>(kr)) << 4) + ((p & 1) << 3);
       v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) bf16x4*)(lds_tile + off));
     }
@@ -156,7 +266,7 @@ __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
   *(uint2*)p = x;
 }
 
-template <class CFG, bool AK, bool BKM, typename OutT>
+template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0>
 __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
   using namespace gemm;
   constexpr int BM = CFG::BM, BN = CFG::BN, TM = CFG::TM, TN = CFG::TN, WN = CFG::WN, NW = CFG::NW;
@@ -211,10 +321,14 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stager<AK, BM, NW> sa;
-  Stager<BKM, BN, NW> sb;
-  sa.init(A, a.lda, a.M, m0, wave, lane);
-  sb.init(B, a.ldb, a.N, n0, wave, lane);
+  using SA = std::conditional_t<GM == 1, ConvStagerK<BM, NW>, Stager<AK, BM, NW>>;
+  using SB = std::conditional_t<GM == 2, ConvStagerMN<BN, NW>, Stager<BKM, BN, NW>>;
+  SA sa;
+  SB sb;
+  if constexpr (GM == 1) sa.init(a, A, a.M, m0, wave, lane);
+  else sa.init(A, a.lda, a.M, m0, wave, lane);
+  if constexpr (GM == 2) sb.init(a, B, a.N, n0, wave, lane);
+  else sb.init(B, a.ldb, a.N, n0, wave, lane);
 
   // stage s: A tile at smem + s*STAGE, B tile right after it
 #define BUF_A(s) (smem + (s) * CFG::STAGE)
@@ -354,16 +468,18 @@ using Cfg128x128 = TileCfg<128, 128, 2, 2>;
 using Cfg256x128 = TileCfg<256, 128, 4, 2>;
 using Cfg128x256 = TileCfg<128, 256, 2, 4>;
 using Cfg256x256 = TileCfg<256, 256, 2, 4>;
+using Cfg256x64 = TileCfg<256, 64, 4, 1>;   // narrow outputs (Cout = 64 convolutions)
+using Cfg64x256 = TileCfg<64, 256, 1, 4>;   // short outputs (Cout = 64 weight gradients)
 
 template <class CFG>
 static inline long long ntiles(const GemmArgs& a) {
   return (long long)((a.M + CFG::BM - 1) / CFG::BM) * ((a.N + CFG::BN - 1) / CFG::BN);
 }
 
-template <class CFG, bool AK, bool BKM, typename OutT>
+template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0>
 static void launch_cfg(const GemmArgs& a, int batch, hipStream_t st) {
   dim3 grid((unsigned)ntiles<CFG>(a), a.splitk > 1 ? a.splitk : 1, batch), block(CFG::NT);
-  hipLaunchKernelGGL((gemm_bf16_kernel<CFG, AK, BKM, OutT>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<CFG, AK, BKM, OutT, GM>), grid, block, 0, st, a);
 }
 
 template <bool AK, bool BKM, typename OutT>
@@ -372,6 +488,8 @@ static void launch_layout(const GemmArgs& a, int cfg, int batch, hipStream_t st)
     case 1: launch_cfg<Cfg256x128, AK, BKM, OutT>(a, batch, st); break;
     case 2: launch_cfg<Cfg128x256, AK, BKM, OutT>(a, batch, st); break;
     case 3: launch_cfg<Cfg256x256, AK, BKM, OutT>(a, batch, st); break;
+    case 4: launch_cfg<Cfg256x64, AK, BKM, OutT>(a, batch, st); break;
+    case 5: launch_cfg<Cfg64x256, AK, BKM, OutT>(a, batch, st); break;
     default: launch_cfg<Cfg128x128, AK, BKM, OutT>(a, batch, st); break;
   }
 }
@@ -384,6 +502,11 @@ using namespace rtdc;
 // (or >= 90%-used) waves of 256 CUs.
 static int pick_cfg(const GemmArgs& a, int batch) {
   if (a.tile_cfg >= 0) return a.tile_cfg;
+  if (batch == 1 && a.causal == 0) {
+    // 64-wide outputs (Cout = 64 convolutions): a 128x128 tile would idle half its MFMAs
+    if (a.N <= 64 && a.M >= 4096) return 4;
+    if (a.M <= 64 && a.N >= 4096) return 5;
+  }
   if (batch > 1 || a.causal != 0 || a.M < 256 || a.N < 256) return 0;
   auto eff = [](long long tiles) {
     const long long waves = (tiles + 255) / 256;
@@ -399,6 +522,17 @@ static int pick_cfg(const GemmArgs& a, int batch) {
   return 0;
 }
 
+// split-K when the output tiles cannot fill the chip and K is long (weight gradients): aim at
+// ~2 blocks per CU, >= 8 k-tiles per slice, slabs within the workspace.
+static int pick_splitk(const GemmArgs& a, long long tiles) {
+  const int ktiles = a.K / gemm::BK;
+  if (!a.ws || tiles >= 200 || ktiles < 32) return 1;
+  int s = (int)((256 * 2 + tiles - 1) / tiles);
+  s = s > 128 ? 128 : s;
+  while (s > 1 && (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems)) --s;
+  return s;
+}
+
 extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
                               hipStream_t stream) {
   GemmArgs a = *args;
@@ -408,14 +542,9 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
   long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
-                  : cfg == 2 ? ntiles<Cfg128x256>(a) : ntiles<Cfg128x128>(a);
-  const int ktiles = a.K / gemm::BK;
-  if (plain && a.ws && tiles < 200 && ktiles >= 32) {
-    int s = (int)((256 * 2 + tiles - 1) / tiles);  // aim at ~2 blocks per CU
-    s = s > 16 ? 16 : s;
-    while (s > 1 && (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems)) --s;
-    a.splitk = s;
-  }
+                  : cfg == 2 ? ntiles<Cfg128x256>(a) : cfg == 4 ? ntiles<Cfg256x64>(a)
+                  : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
+  if (plain) a.splitk = pick_splitk(a, tiles);
   if (out_fp32) {
     if (a_kmajor && b_kmajor) launch_layout<true, true, float>(a, cfg, batch, stream);
     else if (a_kmajor && !b_kmajor) launch_layout<true, false, float>(a, cfg, batch, stream);
@@ -437,6 +566,39 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws,
                          a.splitk, a.M, a.N, (bf16_t*)a.C, (const bf16_t*)a.Cin, a.ldc, a.beta);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Implicit-GEMM convolution products on the same MFMA kernel (see ConvStagerK / ConvStagerMN):
+//   mode 1: C[npix][N] (bf16) = im2col(X)[npix][K] . B[N][K]^T     conv forward / stride-1 dgrad
+//   mode 2: C[M][N]   (fp32) = A[K=npix][M]^T . im2col(X)[npix][N] weight gradient (split-K)
+extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream) {
+  GemmArgs a = *args;
+  if (a.cv_C % 64 != 0 || a.cv_npix >= (1 << 24) || a.K % gemm::BK != 0 || a.N % 8 != 0) return 1;
+  if (mode == 2 && a.M % 8 != 0) return 1;  // mode 1: rows (pixels) are clamped + masked, any count
+  if ((long long)a.cv_H * a.cv_W * a.cv_C * ((long long)a.cv_npix / ((long long)a.cv_Ho * a.cv_Wo)) >= (1LL << 31))
+    return 1;
+  a.splitk = 1;
+  if (mode == 1) {
+    if (a.M != a.cv_npix) return 1;
+    if (a.N <= 64) launch_cfg<Cfg256x64, true, true, bf16_t, 1>(a, 1, stream);
+    else launch_cfg<Cfg128x128, true, true, bf16_t, 1>(a, 1, stream);
+  } else if (mode == 2) {
+    if (a.K < a.cv_npix) return 1;
+    const bool narrow = a.M <= 64;
+    a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a));
+    if (narrow) launch_cfg<Cfg64x256, false, false, float, 2>(a, 1, stream);
+    else launch_cfg<Cfg128x128, false, false, float, 2>(a, 1, stream);
+    if (a.splitk > 1) {
+      long long q = (long long)a.M * a.N / 4;
+      long long blocks = (q + 255) / 256;
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws, a.splitk,
+                         a.M, a.N, (float*)a.C, (const float*)a.Cin, a.ldc, a.beta);
+    }
+  } else {
+    return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

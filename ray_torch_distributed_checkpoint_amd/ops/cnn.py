@@ -56,6 +56,10 @@ def _rows_padded(t: torch.Tensor, Mp: int) -> torch.Tensor:
     return out
 
 
+def _implicit_ok(C: int, M: int) -> bool:
+    return C % 64 == 0 and M < (1 << 24)
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad):
@@ -64,10 +68,18 @@ class _Conv2d(torch.autograd.Function):
         assert Cin == C, (x.shape, w.shape)
         Ho, Wo = _out_hw(H, W, KH, KW, stride, pad)
         K = KH * KW * C
-        Kp = _ceil(K, 64)
         M = B * Ho * Wo
-        Mp = _ceil(M, 64)
         x = x.contiguous()
+        if _implicit_ok(C, M):
+            # implicit GEMM: the MFMA kernel gathers im2col(x) tiles straight from NHWC x
+            wm = _weight_matrix(w, K)
+            y = torch.empty((M, Cout), dtype=torch.bfloat16, device=x.device)
+            gpu_ext().conv_gemm(x, wm, y, 1, M, Cout, K, K, Ho, Wo, KW, stride, pad, None)
+            ctx.save_for_backward(x, wm)
+            ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, K, M, M, "implicit")
+            return y.view(B, Ho, Wo, Cout)
+        Kp = _ceil(K, 64)
+        Mp = _ceil(M, 64)
         direct = KH == 1 and KW == 1 and stride == 1 and pad == 0 and K == Kp and M == Mp
         if direct:
             cols = x.view(M, C)
@@ -79,27 +91,57 @@ class _Conv2d(torch.autograd.Function):
         wm = _weight_matrix(w, Kp)
         y = G.linear_fwd(cols, wm)  # [Mp, Cout]
         ctx.save_for_backward(cols, wm)
-        ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, direct)
+        ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, "direct" if direct else "cols")
         return y[:M].view(B, Ho, Wo, Cout)
 
     @staticmethod
     def backward(ctx, dy):
-        cols, wm = ctx.saved_tensors
-        B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, direct = ctx.geom
+        saved, wm = ctx.saved_tensors
+        B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, mode = ctx.geom
         Cout = wm.shape[0]
-        dy2 = _rows_padded(dy.reshape(M, Cout).contiguous(), Mp)
+        dy = dy.contiguous()
+        Mp = _ceil(M, 64)
+        dy2 = _rows_padded(dy.view(M, Cout), Mp)
         dx = dw = None
+        if mode == "implicit":
+            x = saved
+            if ctx.needs_input_grad[1]:
+                dwm = torch.empty((Cout, K), dtype=torch.float32, device=dy.device)
+                ws = G.workspace(dy.device, G.SPLITK_WS_ELEMS, "splitk")
+                gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws)
+                dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2).contiguous()
+            if ctx.needs_input_grad[0]:
+                if stride == 1 and _implicit_ok(Cout, B * H * W):
+                    # stride-1 dgrad is itself a convolution of dY with the flipped, transposed
+                    # kernel (padding KH-1-pad): implicit GEMM again, no column matrix
+                    s = shadow_of_w(ctx, wm, Cout, C, KH, KW)
+                    dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
+                    Kt = KH * KW * Cout
+                    gpu_ext().conv_gemm(dy, s, dx.view(B * H * W, C), 1, B * H * W, C, Kt, Kt, H, W, KW, 1,
+                                        KH - 1 - pad, None)
+                else:
+                    dcols = G.linear_dgrad(dy2, wm)  # [Mp, K]
+                    dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
+                    gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
+            return dx, dw, None, None
+        cols = saved
         if ctx.needs_input_grad[1]:
             dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
             dw = dwm[:, :K].view(Cout, KH, KW, C).permute(0, 3, 1, 2).contiguous()
         if ctx.needs_input_grad[0]:
             dcols = G.linear_dgrad(dy2, wm)  # [Mp, Kp] bf16
-            if direct:
+            if mode == "direct":
                 dx = dcols.view(B, H, W, C)
             else:
                 dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                 gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
         return dx, dw, None, None
+
+
+def shadow_of_w(ctx, wm, Cout, C, KH, KW):
+    """dgrad operand W'[c][(kh', kw', co)] = W[co][c][KH-1-kh'][KW-1-kw'] from the forward's
+    [Cout, (kh, kw, c)] matrix (bf16, built once per backward)."""
+    return wm.view(Cout, KH, KW, C).flip(1, 2).permute(3, 1, 2, 0).reshape(C, KH * KW * Cout).contiguous()
 
 
 def conv2d_ref(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
