@@ -504,8 +504,8 @@ static int pick_cfg(const GemmArgs& a, int batch) {
   if (a.tile_cfg >= 0) return a.tile_cfg;
   if (batch == 1 && a.causal == 0) {
     // 64-wide outputs (Cout = 64 convolutions): a 128x128 tile would idle half its MFMAs
-    if (a.N <= 64 && a.M >= 4096) return 4;
-    if (a.M <= 64 && a.N >= 4096) return 5;
+    if (a.N <= 64 && a.M >= 256) return 4;
+    if (a.M <= 64 && a.N >= 128) return 5;
   }
   if (batch > 1 || a.causal != 0 || a.M < 256 || a.N < 256) return 0;
   auto eff = [](long long tiles) {
