@@ -227,8 +227,11 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     if world > 1:
         dist.barrier()
 
+    from ray_torch_distributed_checkpoint_amd.checkpoint.state_dict import get_state_dict, set_state_dict
+
     def state():
-        return {"model": model.state_dict(), "optim": opt.state_dict(), "step": 1}
+        msd, osd = get_state_dict(model, opt)
+        return {"model": msd, "optim": osd, "step": 1}
 
     # ---- async save overlapped with training steps
     torch.cuda.synchronize()
@@ -267,7 +270,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     t3 = time.perf_counter()
     sd = state()
     dcp.load(sd, path2)
-    opt.load_state_dict(sd["optim"])
+    set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd["optim"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

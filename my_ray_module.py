@@ -64,13 +64,15 @@ def _rng_state(dev):
 
 
 def _set_rng_state(st, dev):
-    torch.set_rng_state(st["torch_cpu"])
+    # the checkpoint may have been loaded with map_location=<gpu>: RNG states live on the host
+    torch.set_rng_state(st["torch_cpu"].cpu())
     ops.default_stream().load_state_dict(st["philox"])
     if "numpy" in st:
         n = st["numpy"]
-        np.random.set_state(("MT19937", n["keys"].numpy().astype(np.uint32), n["pos"], n["has_gauss"], n["gauss"]))
+        np.random.set_state(("MT19937", n["keys"].cpu().numpy().astype(np.uint32), n["pos"], n["has_gauss"],
+                             n["gauss"]))
     if dev.type == "cuda" and "torch_cuda" in st:
-        torch.cuda.set_rng_state(st["torch_cuda"], dev)
+        torch.cuda.set_rng_state(st["torch_cuda"].cpu(), dev)
 
 
 def train_func_per_worker(config: Dict):

@@ -47,8 +47,8 @@ int rtdc_softmax_bwd(const void* P, const void* dP, void* dS, long long rows, in
                      hipStream_t st);
 int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int ntok, int T, int D,
                    hipStream_t st);
-int rtdc_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int B, int T, int D,
-                   int accumulate_wpe, hipStream_t st);
+int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe, int B, int T,
+                   int D, int accumulate_wpe, hipStream_t st);
 int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
                  unsigned long long offset, int is_bf16, hipStream_t st);
 int rtdc_relu_dropout(const void* h, void* y, const void* dy, void* dx, long long n, float p,
@@ -246,10 +246,12 @@ static void embed_fwd(Tensor idx, Tensor wte, c10::optional<Tensor> wpe, Tensor 
                           (int)idx.numel(), (int)T, D, cur_stream()),
            "embed_fwd");
 }
-static void embed_bwd(Tensor idx, Tensor dout, Tensor dwte, c10::optional<Tensor> dwpe, int64_t B, int64_t T,
-                      bool accumulate_wpe) {
+// sidx / perm: stably sorted token ids and their original positions (deterministic backward)
+static void embed_bwd(Tensor sidx, Tensor perm, Tensor dout, Tensor dwte, c10::optional<Tensor> dwpe, int64_t B,
+                      int64_t T, bool accumulate_wpe) {
   const int D = (int)dwte.size(1);
-  check_rc(rtdc_embed_bwd(idx.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
+  TORCH_CHECK(sidx.is_contiguous() && perm.is_contiguous() && sidx.numel() == B * T, "embed_bwd: bad sort arrays");
+  check_rc(rtdc_embed_bwd(sidx.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
                           (float*)ptr_or_null(dwpe), (int)B, (int)T, D, accumulate_wpe, cur_stream()),
            "embed_bwd");
 }

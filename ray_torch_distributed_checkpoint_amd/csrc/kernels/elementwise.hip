@@ -39,19 +39,32 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   }
 }
 
-// dwte[idx[t], :] += dout[t, :]  (fp32 atomics: rows repeat across tokens)
-__global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ idx,
+// dwte[v, :] = sum over tokens t with idx[t] == v of dout[t, :], deterministic: the tokens
+// arrive stably sorted by id (sidx = sorted ids, perm = their original positions), one wave per
+// sorted position; only the wave at the start of a run of equal ids works, summing the run in
+// original token order and writing the row once.  No float atomics (bitwise reproducible).
+__global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ sidx,
+                                                           const int64_t* __restrict__ perm,
                                                            const bf16_t* __restrict__ dout,
                                                            float* __restrict__ dwte, int ntok, int D) {
   const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= ntok) return;
-  const long long row = idx[t];
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= ntok) return;
+  const int64_t row = sidx[i];
+  if (i > 0 && sidx[i - 1] == row) return;
+  int e = i + 1;
+  while (e < ntok && sidx[e] == row) ++e;
   for (int c = lane * 8; c < D; c += 512) {
-    float g[8];
-    ld8e(dout + (long long)t * D + c, g);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = i; j < e; ++j) {
+      float g[8];
+      ld8e(dout + perm[j] * D + c, g);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(dwte + row * D + c + e, g[e]);
+      for (int q = 0; q < 8; ++q) acc[q] += g[q];
+    }
+    float* o = dwte + row * D + c;
+    *(float4*)o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   }
 }
 
@@ -143,11 +156,13 @@ extern "C" int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* w
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-extern "C" int rtdc_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int B, int T,
-                              int D, int accumulate_wpe, hipStream_t st) {
+// sidx/perm: token ids stably sorted and their original positions (dwte rows that no token
+// uses are left untouched: the caller zero-fills).
+extern "C" int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe,
+                              int B, int T, int D, int accumulate_wpe, hipStream_t st) {
   if (D % 8 != 0) return 1;
   const int ntok = B * T;
-  hipLaunchKernelGGL(embed_bwd_wte_kernel, dim3((ntok + 3) / 4), dim3(256), 0, st, idx, (const bf16_t*)dout,
+  hipLaunchKernelGGL(embed_bwd_wte_kernel, dim3((ntok + 3) / 4), dim3(256), 0, st, sidx, perm, (const bf16_t*)dout,
                      dwte, ntok, D);
   if (dwpe)
     hipLaunchKernelGGL(embed_bwd_wpe_kernel, dim3(T, (D + 255) / 256), dim3(256), 0, st, (const bf16_t*)dout,

@@ -1,4 +1,9 @@
-"""Token + position embedding (gather) and its backward (fp32 scatter-add) on native kernels."""
+"""Token + position embedding (gather) and its backward on native kernels.
+
+The token-table gradient is a scatter-add where rows repeat; instead of float atomics (whose
+summation order changes run to run) the token ids are stably sorted once and the native
+kernel sums each run of equal ids in original token order: bitwise-reproducible gradients,
+required for bit-exact resume (BASELINE config 5)."""
 from __future__ import annotations
 
 import torch
@@ -29,7 +34,8 @@ class _Embedding(torch.autograd.Function):
         dwpe = None
         if wpe_shape is not None:
             dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device)
-        gpu_ext().embed_bwd(idx, dout.contiguous(), dwte, dwpe, B, T, False)
+        sidx, perm = torch.sort(idx.reshape(-1), stable=True)
+        gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False)
         return None, dwte, dwpe
 
 

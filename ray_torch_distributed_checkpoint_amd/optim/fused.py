@@ -63,6 +63,28 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 st[k] = FlatParamSpace.view(self._bufs[k], seg)
         return st
 
+    @torch.no_grad()
+    def init_state(self) -> None:
+        """Materialise every per-parameter state entry (zeros, step 0) without stepping, so
+        `state_dict()` has its full structure before the first step - what a sharded
+        checkpoint load fills in place (torch.distributed.checkpoint.state_dict does the same
+        with a zero-grad step, T/distributed/checkpoint/state_dict.py `_init_optim_state`).
+        Numerically a no-op for AdamW; for SGD a zero momentum buffer equals torch's
+        first-step `buf = g` whenever dampening == 0."""
+        for p in self._all_params():
+            st = self.state[p]
+            if self._use_native():
+                self._ensure_space()
+                self._bind_state(p)
+            else:
+                for k in self._state_keys:
+                    if k not in st:
+                        st[k] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            self._init_extra(st)
+
+    def _init_extra(self, st) -> None:
+        pass
+
     def zero_grad(self, set_to_none: bool = True):
         if self._space is not None and self._space.grad is not None:
             self._space.zero_grad()
@@ -95,6 +117,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
 
 class FusedAdamW(_FlatOptimizer):
     _state_keys = ("exp_avg", "exp_avg_sq")
+
+    def _init_extra(self, st) -> None:
+        if "step" not in st:
+            st["step"] = torch.tensor(0.0)
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
                  maximize=False):
@@ -155,6 +181,10 @@ class FusedAdamW(_FlatOptimizer):
 
 class FusedSGD(_FlatOptimizer):
     _state_keys = ("momentum_buffer",)
+
+    def init_state(self) -> None:
+        if all(g["momentum"] != 0.0 for g in self.param_groups):
+            super().init_state()
 
     def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
                  maximize=False):

@@ -1,0 +1,78 @@
+"""BASELINE config 5 on the GPU: kill at step K, restore, bit-equal continuation.
+
+* toy flow (my_ray_module, native fp32 MFMA kernels + Philox dropout + fused SGD): a worker
+  is SIGKILLed at its 2nd report, the supervisor restarts it from the latest committed
+  checkpoint and every later epoch's metrics equal the uninterrupted run bit for bit;
+* GPT-2 (bf16 kernels, flash attention, deterministic embedding backward, fused AdamW):
+  a DCP checkpoint of model + optimizer + Philox state taken at step K, restored into a
+  fresh model, reproduces the next steps' losses bitwise.
+"""
+import json
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_toy_flow_kill_and_exact_resume_gpu(tmp_path, monkeypatch):
+    import my_ray_module as m
+
+    monkeypatch.setenv("RTDC_FMNIST_TRAIN", "4000")
+    monkeypatch.setenv("RTDC_FMNIST_TEST", "1000")
+    monkeypatch.delenv("RTDC_FORCE_CPU", raising=False)
+    a = m.train_fashion_mnist(num_workers=1, use_gpu=True, epochs=3, checkpoint_storage_path=str(tmp_path / "a"),
+                              seed=11, resume_mode="exact")
+    monkeypatch.setenv("RTDC_FAIL_AT_REPORT", "2")
+    b = m.train_fashion_mnist(num_workers=1, use_gpu=True, epochs=3, checkpoint_storage_path=str(tmp_path / "b"),
+                              seed=11, resume_mode="exact", max_failures=1)
+    rows_a = [json.loads(l) for l in open(os.path.join(a.path, "result.json"))]
+    rows_b = [json.loads(l) for l in open(os.path.join(b.path, "result.json"))]
+    assert len(rows_a) == len(rows_b) == 3
+    for ra, rb in zip(rows_a, rows_b):
+        assert ra["val_loss"] == rb["val_loss"] and ra["accuracy"] == rb["accuracy"], (ra, rb)
+
+
+def test_gpt2_checkpoint_resume_bit_equal(tmp_path):
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
+    from ray_torch_distributed_checkpoint_amd.checkpoint.state_dict import get_state_dict, set_state_dict
+    from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW
+
+    cfg = GPT2Config.named("gpt2-tiny")
+    data = torch.randint(0, cfg.vocab_size, (8, 4, 129), device="cuda",
+                         generator=torch.Generator(device="cuda").manual_seed(3))
+
+    def make():
+        torch.manual_seed(0)
+        model = GPT2(cfg).cuda()
+        return model, FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.1)
+
+    def step(model, opt, i):
+        loss = model(data[i, :, :-1], data[i, :, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss.detach().clone()
+
+    K = 4
+    model, opt = make()
+    ops.manual_seed(1234)
+    for i in range(K):
+        step(model, opt, i)
+    msd, osd = get_state_dict(model, opt)
+    dcp.save({"model": msd, "optim": osd, "philox": ops.default_stream().state_dict()}, str(tmp_path / "ck"))
+    ref = [step(model, opt, i) for i in range(K, 8)]
+
+    model2, opt2 = make()
+    ops.manual_seed(999)  # restored below
+    msd2, osd2 = get_state_dict(model2, opt2)  # load targets, optimizer state materialised
+    sd = {"model": msd2, "optim": osd2, "philox": ops.default_stream().state_dict()}
+    dcp.load(sd, str(tmp_path / "ck"))
+    set_state_dict(model2, opt2, model_state_dict=sd["model"], optim_state_dict=sd["optim"])
+    ops.default_stream().load_state_dict(sd["philox"])
+    got = [step(model2, opt2, i) for i in range(K, 8)]
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g), (ref, got)

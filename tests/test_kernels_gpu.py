@@ -277,6 +277,18 @@ def test_embedding():
     _close(wte.grad, wr.grad, 1e-4)
     _close(wpe.grad, pr.grad, 1e-4)
 
+    # heavy id repetition: the sorted-run reduction must be bitwise reproducible
+    idx = torch.randint(0, 7, (8, 256), device=DEV)
+    g = _bf(8, 256, D)
+    grads = []
+    for _ in range(3):
+        w = torch.randn(V, D, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1)).requires_grad_(True)
+        embedding(idx, w, None).backward(g)
+        grads.append(w.grad)
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+    ref = torch.zeros(V, D, device=DEV).index_add_(0, idx.reshape(-1), g.reshape(-1, D).float())
+    _close(grads[0], ref, 1e-5)
+
 
 def test_dropout_mask_consistency():
     from ray_torch_distributed_checkpoint_amd.ops import dropout
