@@ -43,7 +43,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
-    ap.add_argument("--sweep", action="store_true", help="also time every forced tile configuration (fwd)")
+    ap.add_argument("--sweep", action="store_true", help="also time forced tile configurations (all layouts)")
+    ap.add_argument("--cfgs", default="0,3,6", help="tile configurations for --sweep")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -65,10 +66,17 @@ def main():
             row[lay] = {"ours_TF": round(flops / t_o / 1e12, 1), "hipblaslt_TF": round(flops / t_r / 1e12, 1),
                         "ours_us": round(t_o * 1e6, 1), "hipblaslt_us": round(t_r * 1e6, 1)}
         if args.sweep:
-            for cfg in range(4):
-                y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-                t = min(timeit(lambda: G.gemm_bf16(x, w, y, M, N, K, K, K, N, tile_cfg=cfg), args.reps) for _ in range(3))
-                row[f"fwd_cfg{cfg}_TF"] = round(flops / t / 1e12, 1)
+            y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            dx = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+            dw = torch.empty(N, K, device="cuda", dtype=torch.float32)
+            for cfg in [int(c) for c in args.cfgs.split(",")]:
+                for lay, fn in [
+                    ("fwd", lambda: G.gemm_bf16(x, w, y, M, N, K, K, K, N, tile_cfg=cfg)),
+                    ("dgrad", lambda: G.gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, tile_cfg=cfg)),
+                    ("wgrad", lambda: G.gemm_bf16(dy, x, dw, N, K, M, N, K, K, False, False, tile_cfg=cfg)),
+                ]:
+                    t = min(timeit(fn, args.reps) for _ in range(3))
+                    row[f"{lay}_cfg{cfg}_TF"] = round(flops / t / 1e12, 1)
         # correctness spot check (fwd)
         ref = (x.float() @ w.float().t())
         err = (G.linear_fwd(x, w).float() - ref).abs().max().item() / ref.abs().max().item()

@@ -168,7 +168,7 @@ static void rmsnorm_fwd(Tensor x, Tensor g, Tensor y, Tensor rstd, double eps) {
 static void layernorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
                           Tensor dx, Tensor ws, Tensor dg, Tensor db, int64_t nwaves, bool accumulate) {
   const int D = (int)x.size(-1), M = (int)(x.numel() / D);
-  TORCH_CHECK(ws.numel() >= 2 * nwaves * D, "layernorm_bwd workspace too small");
+  TORCH_CHECK(ws.numel() >= (2 * (nwaves / 4) + 128) * D, "layernorm_bwd workspace too small");
   check_rc(rtdc_layernorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr<float>(),
                               rstd.data_ptr<float>(), ptr_or_null(dres), dx.data_ptr(), ws.data_ptr<float>(),
                               dg.data_ptr<float>(), db.data_ptr<float>(), M, D, (int)nwaves, accumulate,
@@ -178,7 +178,7 @@ static void layernorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rst
 static void rmsnorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor rstd, c10::optional<Tensor> dres, Tensor dx,
                         Tensor ws, Tensor dg, int64_t nwaves, bool accumulate) {
   const int D = (int)x.size(-1), M = (int)(x.numel() / D);
-  TORCH_CHECK(ws.numel() >= nwaves * D, "rmsnorm_bwd workspace too small");
+  TORCH_CHECK(ws.numel() >= (2 * (nwaves / 4) + 128) * D, "rmsnorm_bwd workspace too small");
   check_rc(rtdc_rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), rstd.data_ptr<float>(), ptr_or_null(dres),
                             dx.data_ptr(), ws.data_ptr<float>(), dg.data_ptr<float>(), M, D, (int)nwaves,
                             accumulate, cur_stream()),
@@ -186,7 +186,7 @@ static void rmsnorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor rstd, c10::optiona
 }
 static void colsum(Tensor X, int64_t M, int64_t N, int64_t ld, Tensor ws, int64_t nblk, Tensor out,
                    bool accumulate) {
-  TORCH_CHECK(ws.numel() >= nblk * N, "colsum workspace too small");
+  TORCH_CHECK(ws.numel() >= (nblk + 64) * N, "colsum workspace too small");
   check_rc(rtdc_colsum(X.data_ptr(), (int)M, (int)N, (int)ld, ws.data_ptr<float>(), (int)nblk,
                        out.data_ptr<float>(), accumulate, X.scalar_type() == at::kBFloat16, cur_stream()),
            "colsum");

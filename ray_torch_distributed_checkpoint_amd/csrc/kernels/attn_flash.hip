@@ -215,26 +215,35 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
 }
 
 // ------------------------------------------------------------------------------ delta
+// delta[b][h][t] = sum_d O * dO over one head row; G = DH/8 lanes per row (16-B loads,
+// consecutive lanes read consecutive 16 B), reduced with xor shuffles inside the lane group.
+template <int DH>
 __global__ __launch_bounds__(256) void delta_kernel(const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
-                                                   float* __restrict__ delta, int B, int T, int H, int DH) {
-  const long long idx = blockIdx.x * 256LL + threadIdx.x;  // (b, t, h)
-  if (idx >= (long long)B * T * H) return;
-  const int h = (int)(idx % H);
-  const long long bt = idx / H;
-  const int t = (int)(bt % T), b = (int)(bt / T);
-  const bf16_t* o = out + bt * H * DH + h * DH;
-  const bf16_t* d = dout + bt * H * DH + h * DH;
+                                                   float* __restrict__ delta, int B, int T, int H) {
+  constexpr int G = DH / 8;
+  const long long gid = blockIdx.x * 256LL + threadIdx.x;
+  const long long idx = gid / G;  // (b, t, h) row
+  const int part = (int)(gid % G);
   float s = 0.f;
-  for (int c = 0; c < DH; c += 8) {
-    uint4 x = *(const uint4*)(o + c), y = *(const uint4*)(d + c);
-    uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+  if (idx < (long long)B * T * H) {
+    const bf16_t* o = out + idx * DH + part * 8;
+    const bf16_t* d = dout + idx * DH + part * 8;
+    const uint4 x = *(const uint4*)o, y = *(const uint4*)d;
+    const uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       s += __uint_as_float(xa[i] << 16) * __uint_as_float(ya[i] << 16);
       s += __uint_as_float(xa[i] & 0xffff0000u) * __uint_as_float(ya[i] & 0xffff0000u);
     }
   }
-  delta[((long long)b * H + h) * T + t] = s;
+#pragma unroll
+  for (int off = 1; off < G; off <<= 1) s += __shfl_xor(s, off, 64);
+  if (part == 0 && idx < (long long)B * T * H) {
+    const int h = (int)(idx % H);
+    const long long bt = idx / H;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    delta[((long long)b * H + h) * T + t] = s;
+  }
 }
 
 // ------------------------------------------------------------------------------ dK / dV
@@ -436,8 +445,13 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
                               void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st) {
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
   const long long rows = (long long)B * T * H;
-  hipLaunchKernelGGL(fa::delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, (const bf16_t*)out,
-                     (const bf16_t*)dout, delta, B, T, H, Dh);
+  const long long dthreads = rows * (Dh / 8);
+  if (Dh == 64)
+    hipLaunchKernelGGL(fa::delta_kernel<64>, dim3((unsigned)((dthreads + 255) / 256)), dim3(256), 0, st,
+                       (const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
+  else
+    hipLaunchKernelGGL(fa::delta_kernel<128>, dim3((unsigned)((dthreads + 255) / 256)), dim3(256), 0, st,
+                       (const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta;
   a.dqkv = (bf16_t*)dqkv;

@@ -1,0 +1,222 @@
+// 256x256 bf16 MFMA GEMM, 8 waves, counted-vmcnt phase pipeline (gfx950).
+//
+// Same contract, operand layouts (K-major / MN-major), fused epilogues and split-K slabs as
+// gemm_bf16.hip, for large outputs.  What is different is the schedule
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4):
+//
+// * The 256x64 A and B K-tiles are staged as HALF tiles (128 rows x 64 k, 16 KiB, two
+//   global_load_lds_dwordx4 per thread) into 2 LDS buffers (2 x 4 halves = 128 KiB).
+// * Wave w owns a 128x64 output made of four 64x32 quadrants, one per (A half, B half)
+//   pair: rows 64*(w&1) of each A half, columns 32*(w>>1) of each B half.  A K-tile is
+//   4 phases, one quadrant each, in the order (lo,lo) (lo,hi) (hi,lo) (hi,hi) - 16 MFMA
+//   16x16x32 per phase.  A-lo is therefore dead after phase 2, B-lo after phase 3 (its
+//   fragments stay in registers for phase 3), and each half of the NEXT tiles can be
+//   restaged early: one half-tile is issued per phase -
+//       p1: B-lo(t+1)   p2: B-hi(t+1)   p3: A-hi(t+1)   p4: A-lo(t+2)
+//   so every half-tile load has 4-5 phases (>= one K-tile of MFMA work) to land, with three
+//   half-tiles (6 loads) in flight across every barrier: s_waitcnt vmcnt(6), never 0 in
+//   the steady state, and raw s_barrier (a __syncthreads() would drain the DMA queue).
+// * RAW: a half is read one phase after the wait that retires it; WAR: a half is restaged
+//   >= 3 phases after its last ds_read (the reads were retired by lgkmcnt(0) before the
+//   barrier in between).  All LDS lives in ONE __shared__ array (a second object makes
+//   hipcc drain vmcnt before every ds_read).
+#include "gemm_common.h"
+
+namespace rtdc {
+namespace g8 {
+
+constexpr int BM = 256, BN = 256, HALF = 16384;
+
+// outstanding glds instructions allowed (wave-uniform): counted waits are immediates
+__device__ __forceinline__ void wait_vm(int allowed) {
+  if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (allowed >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (allowed >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool AK, bool BKM, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * HALF];  // [buf][A-lo, A-hi, B-lo, B-hi]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wave & 1, wb = wave >> 1;
+
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  int tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  int kb = 0, ke = a.K;
+  if (a.splitk > 1) {
+    const int ktiles = a.K / gemm::BK;
+    const int per = (ktiles + a.splitk - 1) / a.splitk;
+    kb = blockIdx.y * per * gemm::BK;
+    ke = min(a.K, kb + per * gemm::BK);
+  }
+  const int nt = ke > kb ? (ke - kb) / gemm::BK : 0;
+  const int total_ev = 4 * nt;
+
+  Stager<AK, 128, 8> sa0, sa1;
+  Stager<BKM, 128, 8> sb0, sb1;
+  sa0.init(a.A, a.lda, a.M, m0, wave, lane);
+  sa1.init(a.A, a.lda, a.M, m0 + 128, wave, lane);
+  sb0.init(a.B, a.ldb, a.N, n0, wave, lane);
+  sb1.init(a.B, a.ldb, a.N, n0 + 128, wave, lane);
+
+  // event e = 4*tile + kind, kind 0: A-lo, 1: B-lo, 2: B-hi, 3: A-hi (issue order = e order)
+  auto issue = [&](int e) {
+    if (e >= total_ev) return;
+    const int j = e >> 2, kind = e & 3;
+    const int k0 = kb + j * gemm::BK;
+    char* base = smem + (j & 1) * 4 * HALF;
+    if (kind == 0) sa0.issue(k0, base, wave);
+    else if (kind == 1) sb0.issue(k0, base + 2 * HALF, wave);
+    else if (kind == 2) sb1.issue(k0, base + 3 * HALF, wave);
+    else sa1.issue(k0, base + HALF, wave);
+  };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    // prologue: A-lo(0) B-lo(0) B-hi(0) A-hi(0) A-lo(1); phase (0,1) needs events 0 and 1
+#pragma unroll
+    for (int e = 0; e < 5; ++e) issue(e);
+    wait_vm(2 * (min(5, total_ev) - 2));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  bf16x8 fa[4][2], fbl[2][2], fbh[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const char* buf = smem + (t & 1) * 4 * HALF;
+#pragma unroll
+    for (int p = 1; p <= 4; ++p) {
+      // 1. fragments for this phase's quadrant (data retired by an earlier wait + barrier)
+      if (p == 1 || p == 3) {
+        const char* ah = buf + (p == 1 ? 0 : HALF);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[i][ks] = load_frag<AK, 128>(ah, 64 * wa + 16 * i, ks, lane);
+      }
+      if (p == 1) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fbl[j][ks] = load_frag<BKM, 128>(buf + 2 * HALF, 32 * wb + 16 * j, ks, lane);
+      }
+      if (p == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fbh[j][ks] = load_frag<BKM, 128>(buf + 3 * HALF, 32 * wb + 16 * j, ks, lane);
+      }
+      // 2. restage one half-tile of a later K-tile
+      const int e = p < 4 ? 4 * t + 4 + p : 4 * t + 8;
+      issue(e);
+      // 3. retire what the next phase reads (p3 -> p4 reads nothing new)
+      if (p != 3 && (p != 4 || t + 1 < nt)) {
+        const int need = p == 1 ? 4 * t + 2 : (p == 2 ? 4 * t + 3 : 4 * t + 5);
+        wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // 4. one quadrant x K=64
+      const int qa = (p - 1) >> 1, qb = (p - 1) & 1;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (qb == 0)
+              acc[qa][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[j][ks], fa[i][ks], acc[qa][0][i][j], 0, 0, 0);
+            else
+              acc[qa][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbh[j][ks], fa[i][ks], acc[qa][1][i][j], 0, 0, 0);
+          }
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3] of every (quadrant, i, j) fragment ----
+  if (a.splitk > 1) {
+    float* Wp = a.ws + (long long)blockIdx.y * a.M * a.N;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + 128 * qa + 64 * wa + 16 * i + (lane & 15);
+          if (m >= a.M) continue;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int n = n0 + 128 * qb + 32 * wb + 16 * j + 4 * (lane >> 4);
+            if (n >= a.N) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * a.alpha;
+            store4<float>(Wp + (long long)m * a.N + n, v);
+          }
+        }
+    return;
+  }
+  OutT* C = (OutT*)a.C;
+  const OutT* Cin = (const OutT*)a.Cin;
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 128 * qa + 64 * wa + 16 * i + (lane & 15);
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = n0 + 128 * qb + 32 * wb + 16 * j + 4 * (lane >> 4);
+          if (n >= a.N) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * a.alpha;
+          epilogue4<OutT>(a, C, Cin, m, n, v);
+        }
+      }
+}
+
+}  // namespace g8
+}  // namespace rtdc
+
+using namespace rtdc;
+
+// Launch the 8-phase kernel (batch 1, no causal modes).  a->splitk is honoured as set.
+extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st) {
+  const GemmArgs& a = *args;
+  const unsigned tiles = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
+  dim3 grid(tiles, a.splitk > 1 ? a.splitk : 1, 1), block(512);
+#define G8(AK, BKM, T) hipLaunchKernelGGL((g8::gemm8_kernel<AK, BKM, T>), grid, block, 0, st, a)
+  if (out_fp32) {
+    if (a_kmajor && b_kmajor) G8(true, true, float);
+    else if (a_kmajor) G8(true, false, float);
+    else if (!b_kmajor) G8(false, false, float);
+    else G8(false, true, float);
+  } else {
+    if (a_kmajor && b_kmajor) G8(true, true, bf16_t);
+    else if (a_kmajor) G8(true, false, bf16_t);
+    else if (!b_kmajor) G8(false, false, bf16_t);
+    else G8(false, true, bf16_t);
+  }
+#undef G8
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

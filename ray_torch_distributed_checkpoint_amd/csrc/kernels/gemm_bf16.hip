@@ -31,240 +31,10 @@
 //
 // Batching (attention) uses blockIdx.z with a two-level (outer, inner) stride per operand;
 // causal modes skip/limit work for the triangular attention products.
-#include "common.h"
-#include "args.h"
-
-#include <type_traits>
+#include "gemm_common.h"
 
 namespace rtdc {
 
-namespace gemm {
-constexpr int BK = 64;
-}
-
-template <int BM_, int BN_, int WM_, int WN_>
-struct TileCfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
-  static constexpr int NW = WM * WN, NT = 64 * NW;
-  static constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // MFMA tiles per wave
-  static constexpr int A_BYTES = BM * gemm::BK * 2, B_BYTES = BN * gemm::BK * 2;
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "pieces must split evenly over waves");
-};
-
-// ---- LDS image helpers ----------------------------------------------------------------
-// K-major image: ROWS rows x 128 B (64 bf16 of k).  16-B chunk c of row r lives at physical
-// chunk c ^ ((r >> 1) & 7): a ds_read_b128 lane group (16 distinct rows, same logical chunk)
-// then touches 16 distinct 16-B slots of the 256-B bank row.
-__device__ __forceinline__ int kmaj_off(int row, int chunk) {
-  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
-}
-// MN-major image: 64 k-rows x (2*ROWS) B.  Chunk c of k-row kr lives at c ^ f(kr); a 32-lane
-// half of ds_read_b64_tr_b16 reads 8 k-rows {q, 8+q : q < 4} x 2 chunks -> 16 distinct 16-B
-// bank slots.  ROWS >= 128 (k-rows start on the same bank, stride 256/512 B): f < 16 keeps the
-// chunk inside its row.  ROWS = 64 (128-B k-rows, two per bank row: kr&1 already separates
-// halves): f in {0,2,4,6} from bits 1 and 3 of kr.
-template <int ROWS>
-__device__ __forceinline__ int mnmaj_swz(int kr) {
-  if constexpr (ROWS >= 128)
-    return ((kr & 3) | (((kr >> 3) & 1) << 2)) << 1;
-  else
-    return (((kr >> 1) & 1) | (((kr >> 3) & 1) << 1)) << 1;
-}
-
-// Per-lane global sources of one operand tile, computed once per block.
-template <bool KMAJOR, int ROWS, int NW>
-struct Stager {
-  static constexpr int PIECES = ROWS / 8;  // 1 KiB pieces per 64-deep k tile
-  static constexpr int PPW = PIECES / NW;
-  const bf16_t* src[PPW];
-  long long kmul;  // element stride per unit of k
-
-  __device__ __forceinline__ void init(const bf16_t* X, int ld, int rows, int r0, int wave, int lane) {
-#pragma unroll
-    for (int ii = 0; ii < PPW; ++ii) {
-      const int piece = wave * PPW + ii;
-      if constexpr (KMAJOR) {
-        const int row = piece * 8 + (lane >> 3);
-        const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
-        int gr = r0 + row;
-        gr = gr < rows ? gr : rows - 1;
-        src[ii] = X + (long long)gr * ld + lchunk * 8;
-      } else {
-        constexpr int CPR = ROWS / 8;     // 16-B chunks per k-row
-        constexpr int KRP = 1024 / (ROWS * 2);  // k-rows per piece
-        const int kr = piece * KRP + lane / CPR;
-        const int lchunk = (lane % CPR) ^ mnmaj_swz<ROWS>(kr);
-        int gc = r0 + lchunk * 8;
-        gc = gc < rows ? gc : rows - 8;
-        src[ii] = X + (long long)kr * ld + gc;
-      }
-    }
-    kmul = KMAJOR ? 1 : ld;
-  }
-
-  __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
-    const long long koff = (long long)k0 * kmul;
-#pragma unroll
-    for (int ii = 0; ii < PPW; ++ii) {
-      const int piece = wave * PPW + ii;
-      __builtin_amdgcn_global_load_lds((const void*)(src[ii] + koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
-    }
-  }
-};
-
-// ---- implicit-GEMM convolution stagers ---------------------------------------------------
-// Zero source for taps that fall into the padding (global_load_lds needs a real address).
-__device__ __attribute__((aligned(16))) uint4 g_conv_zero[4];
-
-// q = x / d for 0 <= x < 2^24 via the fp32 reciprocal (one correction step is exact there)
-__device__ __forceinline__ int fdivq(int x, int d, float rd) {
-  int q = (int)((float)x * rd);
-  const int r = x - q * d;
-  q += (r < 0) ? -1 : (r >= d ? 1 : 0);
-  return q;
-}
-
-// Mode 1: A (K-major) = im2col(X) gathered on the fly.  A 64-deep k tile lies inside one tap
-// (C % 64 == 0), so row m of the tile is 128 contiguous bytes of X at pixel
-// (b, ho*s - p + kh, wo*s - p + kw), channels c0..c0+63 - exactly the 8 x 16-B pieces the
-// plain K-major stager moves; out-of-image taps read the zero page.
-template <int ROWS, int NW>
-struct ConvStagerK {
-  static constexpr int PIECES = ROWS / 8, PPW = PIECES / NW;
-  const bf16_t* X;
-  int hb[PPW], wb[PPW], pb[PPW], co[PPW];
-  int H, W, C, KW;
-
-  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* Xp, int rows, int r0, int wave, int lane) {
-    X = Xp;
-    H = a.cv_H; W = a.cv_W; C = a.cv_C; KW = a.cv_KW;
-    const float rWo = 1.f / (float)a.cv_Wo, rHo = 1.f / (float)a.cv_Ho;
-#pragma unroll
-    for (int ii = 0; ii < PPW; ++ii) {
-      const int piece = wave * PPW + ii;
-      const int row = piece * 8 + (lane >> 3);
-      const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
-      int gr = r0 + row;
-      gr = gr < rows ? gr : rows - 1;
-      const int q = fdivq(gr, a.cv_Wo, rWo), wo = gr - q * a.cv_Wo;
-      const int b = fdivq(q, a.cv_Ho, rHo), ho = q - b * a.cv_Ho;
-      hb[ii] = ho * a.cv_stride - a.cv_pad;
-      wb[ii] = wo * a.cv_stride - a.cv_pad;
-      pb[ii] = b * H;
-      co[ii] = lchunk * 8;
-    }
-  }
-
-  __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
-    const int tap = k0 / C, c0 = k0 - tap * C, kh = tap / KW, kw = tap - kh * KW;
-#pragma unroll
-    for (int ii = 0; ii < PPW; ++ii) {
-      const int piece = wave * PPW + ii;
-      const int h = hb[ii] + kh, w = wb[ii] + kw;
-      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const bf16_t* src = ok ? X + (size_t)((pb[ii] + h) * W + w) * C + c0 + co[ii] : (const bf16_t*)g_conv_zero;
-      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
-    }
-  }
-};
-
-// Mode 2: B (MN-major) = im2col(X) with k = output pixel, n = tap*C + c (weight gradient
-// dW = dY^T . im2col(X)).  A lane's 16-B chunk has a fixed (tap, c) for the whole loop; its
-// k-row (pixel) advances by 64 per tile and is decomposed with fp32-reciprocal divisions.
-template <int ROWS, int NW>
-struct ConvStagerMN {
-  static constexpr int PIECES = ROWS / 8, PPW = PIECES / NW;
-  static constexpr int CPR = ROWS / 8, KRP = 1024 / (ROWS * 2);
-  const bf16_t* X;
-  int kr[PPW], dh[PPW], dw[PPW], cc[PPW];
-  int H, W, C, Ho, Wo, stride, npix;
-  float rWo, rHo;
-
-  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* Xp, int cols, int c0, int wave, int lane) {
-    X = Xp;
-    H = a.cv_H; W = a.cv_W; C = a.cv_C; Ho = a.cv_Ho; Wo = a.cv_Wo; stride = a.cv_stride; npix = a.cv_npix;
-    rWo = 1.f / (float)Wo;
-    rHo = 1.f / (float)Ho;
-#pragma unroll
-    for (int ii = 0; ii < PPW; ++ii) {
-      const int piece = wave * PPW + ii;
-      kr[ii] = piece * KRP + lane / CPR;
-      const int lchunk = (lane % CPR) ^ mnmaj_swz<ROWS>(kr[ii]);
-      int gc = c0 + lchunk * 8;
-      gc = gc < cols ? gc : cols - 8;
-      const int tap = gc / C, c = gc - tap * C, kh = tap / a.cv_KW, kw = tap - kh * a.cv_KW;
-      dh[ii] = kh - a.cv_pad;
-      dw[ii] = kw - a.cv_pad;
-      cc[ii] = c;
-    }
-  }
-
-  __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
-#pragma unroll
-    for (int ii = 0; ii < PPW; ++ii) {
-      const int piece = wave * PPW + ii;
-      const int pix = k0 + kr[ii];
-      const int q = fdivq(pix, Wo, rWo), wo = pix - q * Wo;
-      const int b = fdivq(q, Ho, rHo), ho = q - b * Ho;
-      const int h = ho * stride + dh[ii], w = wo * stride + dw[ii];
-      const bool ok = pix < npix && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const bf16_t* src = ok ? X + (size_t)((b * H + h) * W + w) * C + cc[ii] : (const bf16_t*)g_conv_zero;
-      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
-    }
-  }
-};
-
-// Fragment for v_mfma_f32_16x16x32_bf16: lane l holds X(row = R0 + (l&15), k = ks*32 + 8(l>>4) + j).
-template <bool KMAJOR, int ROWS>
-__device__ __forceinline__ bf16x8 load_frag(const char* lds_tile, int R0, int ks, int lane) {
-  if constexpr (KMAJOR) {
-    const int row = R0 + (lane & 15);
-    const int chunk = ks * 4 + (lane >> 4);
-    return *(const bf16x8*)(lds_tile + kmaj_off(row, chunk));
-  } else {
-    const int idx = lane & 15, q = idx >> 2, p = idx & 3, g = lane >> 4;
-    const int c = (R0 >> 3) + (p >> 1);
-    bf16x4 v[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kr = ks * 32 + 8 * g + 4 * h + q;
-      const int off = kr * (ROWS * 2) + ((c ^ mnmaj_swz<ROWS>(kr)) << 4) + ((p & 1) << 3);
-      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) bf16x4*)(lds_tile + off));
-    }
-    bf16x8 r;
-    r[0] = v[0][0]; r[1] = v[0][1]; r[2] = v[0][2]; r[3] = v[0][3];
-    r[4] = v[1][0]; r[5] = v[1][1]; r[6] = v[1][2]; r[7] = v[1][3];
-    return r;
-  }
-}
-
-template <typename OutT>
-__device__ __forceinline__ void load4(const OutT* p, float* v);
-template <>
-__device__ __forceinline__ void load4<float>(const float* p, float* v) {
-  f32x4 x = *(const f32x4*)p;
-  v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
-}
-template <>
-__device__ __forceinline__ void load4<bf16_t>(const bf16_t* p, float* v) {
-  uint2 x = *(const uint2*)p;
-  v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
-  v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
-}
-template <typename OutT>
-__device__ __forceinline__ void store4(OutT* p, const float* v);
-template <>
-__device__ __forceinline__ void store4<float>(float* p, const float* v) {
-  f32x4 x = {v[0], v[1], v[2], v[3]};
-  *(f32x4*)p = x;
-}
-template <>
-__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
-  uint2 x = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-  *(uint2*)p = x;
-}
 
 template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0>
 __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
@@ -498,29 +268,36 @@ static void launch_layout(const GemmArgs& a, int cfg, int batch, hipStream_t st)
 
 using namespace rtdc;
 
-// Choose the tile configuration: the largest tile whose grid still fills the chip in whole
-// (or >= 90%-used) waves of 256 CUs.
-static int pick_cfg(const GemmArgs& a, int batch) {
+// Choose the tile configuration.  Measured on MI355X (benchmarks/gemm_bench.py --sweep,
+// random operands, GPT-2 / Llama shapes, profiles/gemm_bench_8ph.jsonl): the 256x256
+// 8-wave counted-vmcnt kernel (cfg 6) beats the 128x128 2-stage kernel on every MN-major-B
+// product (dgrad +13..39 %, wgrad +10..18 % once >= 24 output tiles exist for split-K), and
+// on forward products when the grid quantises well onto 256 CUs or K is long (fc 887 vs 808,
+// mlp_proj 1020 vs 934, lm_head 872 vs 768 TF); at 2.25 waves and K = 768 (qkv) the 128x128
+// tile with 2 blocks/CU still wins (764 vs 703).
+static int pick_cfg(const GemmArgs& a, int batch, bool a_kmajor, bool b_kmajor) {
   if (a.tile_cfg >= 0) return a.tile_cfg;
   if (batch == 1 && a.causal == 0) {
     // 64-wide outputs (Cout = 64 convolutions): a 128x128 tile would idle half its MFMAs
     if (a.N <= 64 && a.M >= 256) return 4;
     if (a.M <= 64 && a.N >= 128) return 5;
+    if (a.M >= 256 && a.N >= 256) {
+      const long long t6 = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+      const long long waves = (t6 + 255) / 256;
+      const double eff = (double)t6 / (double)(waves * 256);
+      if (a_kmajor && b_kmajor) {
+        if (t6 >= 1024 || eff >= 0.95 || a.K >= 2048) return 6;
+      } else if (a_kmajor) {
+        if (t6 >= 128) return 6;
+      } else {
+        if (t6 >= 24) return 6;
+      }
+    }
   }
-  if (batch > 1 || a.causal != 0 || a.M < 256 || a.N < 256) return 0;
-  auto eff = [](long long tiles) {
-    const long long waves = (tiles + 255) / 256;
-    return (double)tiles / (double)(waves * 256);
-  };
-  // Measured (benchmarks/gemm_bench.py --sweep, MI355X): with the 2-stage loop the 256-wide
-  // tiles only win when the per-tile prologue/epilogue is amortised - long K or a huge
-  // output (LM head 16384x50304: 749 vs 646 TF); at K = 768 the 128x128 tile is 10-25 %
-  // faster (qkv 743 vs 586 TF).
-  const long long t3 = ntiles<Cfg256x256>(a);
-  const bool big = a.K >= 4096 || (long long)a.M * a.N >= (1LL << 28);
-  if (big && t3 >= 256 && eff(t3) >= 0.85) return 3;
   return 0;
 }
+
+extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 
 // split-K when the output tiles cannot fill the chip and K is long (weight gradients): aim at
 // ~2 blocks per CU, >= 8 k-tiles per slice, slabs within the workspace.
@@ -537,15 +314,22 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
                               hipStream_t stream) {
   GemmArgs a = *args;
   if (a.K % gemm::BK != 0 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
-  const int cfg = pick_cfg(a, batch);
+  const int cfg = pick_cfg(a, batch, a_kmajor, b_kmajor);
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
   long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
                   : cfg == 2 ? ntiles<Cfg128x256>(a) : cfg == 4 ? ntiles<Cfg256x64>(a)
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
+  if (cfg == 6) {  // 256x256 8-wave counted-vmcnt pipeline (gemm_8ph.hip)
+    if (batch != 1 || a.causal != 0) return 1;
+    tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  }
   if (plain) a.splitk = pick_splitk(a, tiles);
-  if (out_fp32) {
+  if (cfg == 6) {
+    const int rc = rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
+    if (rc) return rc;
+  } else if (out_fp32) {
     if (a_kmajor && b_kmajor) launch_layout<true, true, float>(a, cfg, batch, stream);
     else if (a_kmajor && !b_kmajor) launch_layout<true, false, float>(a, cfg, batch, stream);
     else if (!a_kmajor && !b_kmajor) launch_layout<false, false, float>(a, cfg, batch, stream);

@@ -152,58 +152,119 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
       }
     }
   }
+  // combine the block's 4 waves in LDS (fixed wave order), one partial row per block
+  extern __shared__ float red[];  // [D] dgamma (+ [D] dbeta)
+  const int wv = threadIdx.x >> 6;
+  for (int w = 0; w < 4; ++w) {
+    if (wv == w) {
 #pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
-      float* pg = ws_dg + (long long)gw * D + c * 8;
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pg[e] = adg[i][e];
-      if (!RMS) {
-        float* pb = ws_db + (long long)gw * D + c * 8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) pb[e] = adb[i][e];
+          for (int e = 0; e < 8; ++e) {
+            red[c * 8 + e] = w ? red[c * 8 + e] + adg[i][e] : adg[i][e];
+            if (!RMS) red[D + c * 8 + e] = w ? red[D + c * 8 + e] + adb[i][e] : adb[i][e];
+          }
+        }
       }
     }
+    __syncthreads();
+  }
+  for (int d = threadIdx.x; d < D; d += 256) {
+    ws_dg[(long long)blockIdx.x * D + d] = red[d];
+    if (!RMS) ws_db[(long long)blockIdx.x * D + d] = red[D + d];
   }
 }
 
 // out[d] (+)= sum_w ws[w][d], fixed summation order.  A block owns 64 columns; its 4 waves
 // stride over the W partial rows (coalesced 256-B rows per wave) and combine through LDS,
 // so a 1024 x 768 workspace is 12 blocks x 256 loads per lane instead of 768 serial chains.
+// Sum W partial rows of ws [W][D] -> out[S][D] where block (x, y) reduces rows
+// [y*R, (y+1)*R) of 64 columns; 4 waves stride the rows, combined in LDS in fixed order.
+// Run twice (W -> S -> 1) so every thread keeps only a few independent loads in flight and
+// the reduction order is fixed (deterministic).
 __global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict__ ws, float* __restrict__ out,
-                                                       int W, int D, int accumulate) {
+                                                       int W, int D, int R, int accumulate) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + lane;
-  float s = 0.f;
+  const int r0 = blockIdx.y * R, r1 = min(W, r0 + R);
+  float s0 = 0.f, s1 = 0.f;
   if (d < D) {
-#pragma unroll 4
-    for (int w = wv; w < W; w += 4) s += ws[(long long)w * D + d];
+    int w = r0 + wv;
+    for (; w + 4 < r1; w += 8) {
+      s0 += ws[(long long)w * D + d];
+      s1 += ws[(long long)(w + 4) * D + d];
+    }
+    if (w < r1) s0 += ws[(long long)w * D + d];
   }
-  part[wv][lane] = s;
+  part[wv][lane] = s0 + s1;
   __syncthreads();
   if (wv == 0 && d < D) {
-    const float t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-    out[d] = accumulate ? out[d] + t : t;
+    const float t = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    float* o = out + (long long)blockIdx.y * D + d;
+    *o = (accumulate && gridDim.y == 1) ? *o + t : t;
   }
 }
 
-// Column sums of a bf16 matrix [M][N] (bias gradient): stage 1 per-block partials over a row
-// range, stage 2 = colsum_ws_kernel.  Thread t of block owns columns (blockIdx.y*256+t).
+// ws [W][D] (W partial rows) -> out [D]; tmp holds the S intermediate rows (S*D floats).
+static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, float* out, int accumulate, hipStream_t st) {
+  int S = W / 32;
+  S = S < 1 ? 1 : (S > 64 ? 64 : S);
+  if (S > 1 && tmp) {
+    const int R = (W + S - 1) / S;
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, S), dim3(256), 0, st, ws, tmp, W, D, R, 0);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1), dim3(256), 0, st, (const float*)tmp, out, S, D, S,
+                       accumulate);
+  } else {
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1), dim3(256), 0, st, ws, out, W, D, W, accumulate);
+  }
+}
+
+// Column sums of a [M][N] matrix (bias gradient), stage 1: block (x, y) reduces rows
+// [x*R, (x+1)*R) of columns [y*512, y*512+512): lane = 8 columns (16-B loads for bf16), the 4
+// waves stride the rows and are combined in LDS -> ws[x][N].  Stage 2 = colsum_ws_reduce.
 __device__ __forceinline__ float as_f(bf16_t v) { return bf2f(v); }
 __device__ __forceinline__ float as_f(float v) { return v; }
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ X, int M, int N,
-                                                            int ld, int rows_per_block,
-                                                            float* __restrict__ ws) {
-  const int n = blockIdx.y * 256 + threadIdx.x;
-  if (n >= N) return;
+__device__ __forceinline__ void ld8c(const T* p, float* v);
+template <>
+__device__ __forceinline__ void ld8c<bf16_t>(const bf16_t* p, float* v) { ld8(p, v); }
+template <>
+__device__ __forceinline__ void ld8c<float>(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ X, int M, int N, int ld,
+                                                            int rows_per_block, float* __restrict__ ws) {
+  __shared__ float part[4][512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.y * 512 + lane * 8;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += as_f(X[(long long)r * ld + n]);
-  ws[(long long)blockIdx.x * N + n] = s;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    for (int r = r0 + wv; r < r1; r += 4) {
+      float v[8];
+      if constexpr (VEC) {
+        ld8c<T>(X + (long long)r * ld + c, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = c + e < N ? as_f(X[(long long)r * ld + c + e]) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[wv][lane * 8 + e] = a[e];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 512; j += 256) {
+    const int n = blockIdx.y * 512 + j;
+    if (n < N) ws[(long long)blockIdx.x * N + n] = (part[0][j] + part[1][j]) + (part[2][j] + part[3][j]);
+  }
 }
 
 }  // namespace rtdc
@@ -235,11 +296,16 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
                            float* db, int M, int D, int nwaves, int accumulate, hipStream_t st) {
   if (D % 8 != 0 || nwaves % 4 != 0) return 1;
   const int cpl = (D / 8 + 63) / 64;
-  dim3 grid(nwaves / 4), block(256);
+  const int nblk = nwaves / 4;
+  dim3 grid(nblk), block(256);
+  // ws layout: [nblk][D] dgamma partials | [nblk][D] dbeta partials | 2 x [64][D] level-2 rows
   float* ws_dg = ws;
-  float* ws_db = ws + (long long)nwaves * D;
+  float* ws_db = ws + (long long)nblk * D;
+  float* tmp = ws + 2LL * nblk * D;
+  const size_t lds = (RMS ? 1 : 2) * (size_t)D * sizeof(float);
+  if (lds > 160 * 1024) return 1;
 #define L(C)                                                                                  \
-  hipLaunchKernelGGL((norm_bwd_kernel<C, RMS>), grid, block, 0, st, (const bf16_t*)dy,        \
+  hipLaunchKernelGGL((norm_bwd_kernel<C, RMS>), grid, block, lds, st, (const bf16_t*)dy,       \
                      (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \
                      (bf16_t*)dx, ws_dg, ws_db, M, D)
   if (cpl <= 1) L(1);
@@ -248,9 +314,8 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
   else if (cpl <= 8) L(8);
   else return 1;
 #undef L
-  dim3 g2((D + 63) / 64);
-  hipLaunchKernelGGL(colsum_ws_kernel, g2, block, 0, st, ws_dg, dg, nwaves, D, accumulate);
-  if (!RMS) hipLaunchKernelGGL(colsum_ws_kernel, g2, block, 0, st, ws_db, db, nwaves, D, accumulate);
+  colsum_ws_reduce(ws_dg, nblk, D, tmp, dg, accumulate, st);
+  if (!RMS) colsum_ws_reduce(ws_db, nblk, D, tmp + 64LL * D, db, accumulate, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -277,13 +342,17 @@ extern "C" int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, co
 }
 extern "C" int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out,
                            int accumulate, int is_bf16, hipStream_t st) {
+  // ws: [nblk][N] partials followed by [64][N] level-2 rows
+  const bool vec = N % 8 == 0 && ld % 8 == 0;
   const int rpb = (M + nblk - 1) / nblk;
-  dim3 grid(nblk, (N + 255) / 256), block(256);
-  if (is_bf16)
-    hipLaunchKernelGGL((colsum_partial_kernel<bf16_t>), grid, block, 0, st, (const bf16_t*)X, M, N, ld, rpb, ws);
-  else
-    hipLaunchKernelGGL((colsum_partial_kernel<float>), grid, block, 0, st, (const float*)X, M, N, ld, rpb, ws);
-  hipLaunchKernelGGL(colsum_ws_kernel, dim3((N + 63) / 64), block, 0, st, (const float*)ws, out, nblk, N,
-                     accumulate);
+  dim3 grid(nblk, (N + 511) / 512), block(256);
+#define CS(T, V) hipLaunchKernelGGL((colsum_partial_kernel<T, V>), grid, block, 0, st, (const T*)X, M, N, ld, rpb, ws)
+  if (is_bf16) {
+    if (vec) CS(bf16_t, true); else CS(bf16_t, false);
+  } else {
+    if (vec) CS(float, true); else CS(float, false);
+  }
+#undef CS
+  colsum_ws_reduce(ws, nblk, N, ws + (long long)nblk * N, out, accumulate, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

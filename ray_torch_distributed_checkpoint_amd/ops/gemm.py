@@ -14,7 +14,7 @@ from ._ext import gpu_ext
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
 CAUSAL_NONE, CAUSAL_SKIP_UPPER, CAUSAL_K_UPTO_M, CAUSAL_K_FROM_M = 0, 1, 2, 3
 
-_COLSUM_BLOCKS = 128
+_COLSUM_BLOCKS = 256
 SPLITK_MAX_OUT = 200 * 128 * 128  # outputs that fill < 200 tiles of 128x128
 SPLITK_WS_ELEMS = 48 << 20       # 192 MiB fp32 slab workspace cap
 _ws_cache: dict = {}
@@ -80,8 +80,8 @@ def colsum(x2d: torch.Tensor, out=None, accumulate=False):
     M, N = x2d.shape
     if out is None:
         out = torch.empty((N,), dtype=torch.float32, device=x2d.device)
-    nblk = min(_COLSUM_BLOCKS, max(1, M // 16))
-    ws = workspace(x2d.device, nblk * N, "colsum")
+    nblk = min(_COLSUM_BLOCKS, max(1, M // 64))
+    ws = workspace(x2d.device, (nblk + 64) * N, "colsum")
     gpu_ext().colsum(x2d, M, N, x2d.stride(0), ws, nblk, out, accumulate)
     return out
 

@@ -10,7 +10,13 @@ from .shadow import shadow_of
 
 
 def _bwd_waves(M: int) -> int:
-    return max(4, min(1024, (M + 3) // 4 * 4))
+    # up to 4096 waves (4 blocks of 4 waves per CU) for latency hiding; the kernel combines
+    # each block's 4 waves, so the partial workspace is (waves / 4) rows
+    return max(4, min(4096, (M + 3) // 4 * 4))
+
+
+def _bwd_ws_elems(nw: int, D: int) -> int:
+    return (2 * (nw // 4) + 2 * 64) * D
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -33,7 +39,7 @@ class _LayerNorm(torch.autograd.Function):
         D = xc.shape[-1]
         M = xc.numel() // D
         nw = _bwd_waves(M)
-        wsp = G.workspace(xc.device, 2 * nw * D, "ln_bwd")
+        wsp = G.workspace(xc.device, _bwd_ws_elems(nw, D), "ln_bwd")
         dx = torch.empty_like(xc)
         dg = torch.empty(D, dtype=torch.float32, device=xc.device)
         db = torch.empty(D, dtype=torch.float32, device=xc.device)
@@ -60,7 +66,7 @@ class _RMSNorm(torch.autograd.Function):
         D = xc.shape[-1]
         M = xc.numel() // D
         nw = _bwd_waves(M)
-        wsp = G.workspace(xc.device, nw * D, "rms_bwd")
+        wsp = G.workspace(xc.device, _bwd_ws_elems(nw, D), "rms_bwd")
         dx = torch.empty_like(xc)
         dg = torch.empty(D, dtype=torch.float32, device=xc.device)
         gpu_ext().rmsnorm_bwd(dy.contiguous(), xc, ws, rstd, None, dx, wsp, dg, nw, False)
