@@ -96,7 +96,7 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
                       int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool a_kmajor, bool b_kmajor,
                       int64_t batch, int64_t batch_inner, int64_t sA0, int64_t sA1, int64_t sB0, int64_t sB1,
                       int64_t sC0, int64_t sC1, double alpha, double beta, int64_t act, int64_t causal,
-                      c10::optional<Tensor> ws, int64_t tile_cfg) {
+                      c10::optional<Tensor> ws, int64_t tile_cfg, c10::optional<Tensor> alpha_dev) {
   check_dev(A, "A");
   check_dev(B, "B");
   check_dev(C, "C");
@@ -122,6 +122,11 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
   a.ws = ws.has_value() ? ws->data_ptr<float>() : nullptr;
   a.ws_elems = ws.has_value() ? ws->numel() : 0;
   a.tile_cfg = (int)tile_cfg;
+  if (alpha_dev.has_value()) {
+    TORCH_CHECK(alpha_dev->scalar_type() == at::kFloat && alpha_dev->numel() == 1 && alpha_dev->is_cuda(),
+                "alpha_dev must be a 1-element fp32 GPU tensor");
+    a.alpha_dev = alpha_dev->data_ptr<float>();
+  }
   TORCH_CHECK(!(act == 2) || a.aux_out, "gelu forward needs aux_out");
   TORCH_CHECK(!(act == 3 || act == 4) || a.aux_in, "activation backward needs aux_in");
   check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream()),

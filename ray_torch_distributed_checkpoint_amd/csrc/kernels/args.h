@@ -18,6 +18,7 @@ struct GemmArgs {
   long long sA0, sA1, sB0, sB1, sC0, sC1;
   int batch_inner;
   float alpha, beta;
+  const float* alpha_dev;  // optional device scalar multiplied into alpha (upstream loss grad)
   int act;        // 0 none, 1 relu, 2 gelu_tanh, 3 *gelu'(aux_in), 4 *relu'(aux_in)
   int causal;     // 0 none, 1 skip tiles with n0 > m_last, 2 k < m0+BM, 3 k >= m0
   int bias_type;  // 0 none, 1 bf16, 2 fp32

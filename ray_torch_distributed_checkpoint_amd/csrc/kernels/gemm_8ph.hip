@@ -151,6 +151,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
   }
 
   // ---- epilogue: lane holds C[m][n..n+3] of every (quadrant, i, j) fragment ----
+  const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
   if (a.splitk > 1) {
     float* Wp = a.ws + (long long)blockIdx.y * a.M * a.N;
 #pragma unroll
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
             if (n >= a.N) continue;
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * a.alpha;
+            for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
             store4<float>(Wp + (long long)m * a.N + n, v);
           }
         }
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
           if (n >= a.N) continue;
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * a.alpha;
+          for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
           epilogue4<OutT>(a, C, Cin, m, n, v);
         }
       }

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
   }
 #undef BUF_A
 #undef BUF_B
+  const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
 
   if (a.splitk > 1) {
     // raw fp32 partial slab (alpha applied); epilogue happens in the reduce kernel
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
         if (n >= a.N) continue;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha;
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
         store4<float>(W + (long long)m * a.N + n, v);
       }
     }
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
       if (n >= a.N) continue;
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha;
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
       if (a.bias_type == 1) {
         float bb[4];
         load4<bf16_t>((const bf16_t*)a.bias + n, bb);
@@ -301,10 +302,10 @@ extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajo
 
 // split-K when the output tiles cannot fill the chip and K is long (weight gradients): aim at
 // ~2 blocks per CU, >= 8 k-tiles per slice, slabs within the workspace.
-static int pick_splitk(const GemmArgs& a, long long tiles) {
+static int pick_splitk(const GemmArgs& a, long long tiles, int target_blocks = 512) {
   const int ktiles = a.K / gemm::BK;
   if (!a.ws || tiles >= 200 || ktiles < 32) return 1;
-  int s = (int)((256 * 2 + tiles - 1) / tiles);
+  int s = (int)((target_blocks + tiles - 1) / tiles);
   s = s > 128 ? 128 : s;
   while (s > 1 && (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems)) --s;
   return s;
@@ -325,6 +326,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     if (batch != 1 || a.causal != 0) return 1;
     tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
   }
+  // the 8-phase kernel runs one 512-thread block per CU: ~one block per CU of slices
   if (plain) a.splitk = pick_splitk(a, tiles);
   if (cfg == 6) {
     const int rc = rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);

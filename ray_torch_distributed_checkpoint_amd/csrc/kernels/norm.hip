@@ -185,9 +185,12 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
 // Run twice (W -> S -> 1) so every thread keeps only a few independent loads in flight and
 // the reduction order is fixed (deterministic).
 __global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict__ ws, float* __restrict__ out,
-                                                       int W, int D, int R, int accumulate) {
+                                                       int W, int D, int R, int accumulate, long long ws_z,
+                                                       long long out_z) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  ws += blockIdx.z * ws_z;  // z = independent reductions batched into one launch
+  out += blockIdx.z * out_z;
   const int d = blockIdx.x * 64 + lane;
   const int r0 = blockIdx.y * R, r1 = min(W, r0 + R);
   float s0 = 0.f, s1 = 0.f;
@@ -208,17 +211,21 @@ __global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict_
   }
 }
 
-// ws [W][D] (W partial rows) -> out [D]; tmp holds the S intermediate rows (S*D floats).
-static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, float* out, int accumulate, hipStream_t st) {
+// nz independent reductions ws + z*ws_z [W][D] (W partial rows) -> out + z*out_z [D];
+// tmp holds nz x S intermediate rows (nz * 64 * D floats).
+static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, float* out, int accumulate, hipStream_t st,
+                             int nz = 1, long long ws_z = 0, long long out_z = 0) {
   int S = W / 32;
   S = S < 1 ? 1 : (S > 64 ? 64 : S);
   if (S > 1 && tmp) {
     const int R = (W + S - 1) / S;
-    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, S), dim3(256), 0, st, ws, tmp, W, D, R, 0);
-    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1), dim3(256), 0, st, (const float*)tmp, out, S, D, S,
-                       accumulate);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, S, nz), dim3(256), 0, st, ws, tmp, W, D, R, 0, ws_z,
+                       64LL * D);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1, nz), dim3(256), 0, st, (const float*)tmp, out, S, D, S,
+                       accumulate, 64LL * D, out_z);
   } else {
-    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1), dim3(256), 0, st, ws, out, W, D, W, accumulate);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1, nz), dim3(256), 0, st, ws, out, W, D, W, accumulate,
+                       ws_z, out_z);
   }
 }
 
@@ -314,8 +321,8 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
   else if (cpl <= 8) L(8);
   else return 1;
 #undef L
-  colsum_ws_reduce(ws_dg, nblk, D, tmp, dg, accumulate, st);
-  if (!RMS) colsum_ws_reduce(ws_db, nblk, D, tmp + 64LL * D, db, accumulate, st);
+  if (RMS) colsum_ws_reduce(ws_dg, nblk, D, tmp, dg, accumulate, st);
+  else colsum_ws_reduce(ws_dg, nblk, D, tmp, dg, accumulate, st, 2, (long long)nblk * D, ((long long)(uintptr_t)db - (long long)(uintptr_t)dg) / (long long)sizeof(float));
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -84,8 +84,12 @@ class Block(nn.Module):
         self.mlp = MLP(cfg)
 
     def forward(self, x):
-        x = self.attn(self.ln_1(x), residual=x)
-        return self.mlp(self.ln_2(x), residual=x)
+        # the residual stream passes through each LayerNorm so its gradient is summed inside
+        # the norm's backward kernel (no separate add of the two branches' gradients)
+        h, x = self.ln_1(x, passthrough=True)
+        x = self.attn(h, residual=x)
+        h, x = self.ln_2(x, passthrough=True)
+        return self.mlp(h, residual=x)
 
 
 class GPT2(nn.Module):

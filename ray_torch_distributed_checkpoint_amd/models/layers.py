@@ -64,8 +64,10 @@ class LayerNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(dim))
         self.bias = nn.Parameter(torch.zeros(dim))
 
-    def forward(self, x):
-        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+    def forward(self, x, passthrough: bool = False):
+        """passthrough=True -> (LN(x), x): use the second output as the residual so its
+        gradient is folded into the norm's backward kernel."""
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, passthrough=passthrough)
 
 
 class RMSNorm(nn.Module):
@@ -74,8 +76,8 @@ class RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(dim))
 
-    def forward(self, x):
-        return ops.rms_norm(x, self.weight, self.eps)
+    def forward(self, x, passthrough: bool = False):
+        return ops.rms_norm(x, self.weight, self.eps, passthrough=passthrough)
 
 
 class Embedding(nn.Module):

@@ -94,8 +94,10 @@ class TransformerBlock(nn.Module):
         self.feed_forward = FeedForward(cfg)
 
     def forward(self, x):
-        x = self.attention(self.attention_norm(x), residual=x)
-        return self.feed_forward(self.ffn_norm(x), residual=x)
+        h, x = self.attention_norm(x, passthrough=True)
+        x = self.attention(h, residual=x)
+        h, x = self.ffn_norm(x, passthrough=True)
+        return self.feed_forward(h, residual=x)
 
 
 class Llama(nn.Module):

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext
+from .gradbuf import grad_target
 from .shadow import shadow_of
 
 
@@ -76,6 +77,7 @@ class _Conv2d(torch.autograd.Function):
             y = torch.empty((M, Cout), dtype=torch.bfloat16, device=x.device)
             gpu_ext().conv_gemm(x, wm, y, 1, M, Cout, K, K, Ho, Wo, KW, stride, pad, None)
             ctx.save_for_backward(x, wm)
+            ctx.w = w
             ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, K, M, M, "implicit")
             return y.view(B, Ho, Wo, Cout)
         Kp = _ceil(K, 64)
@@ -91,6 +93,7 @@ class _Conv2d(torch.autograd.Function):
         wm = _weight_matrix(w, Kp)
         y = G.linear_fwd(cols, wm)  # [Mp, Cout]
         ctx.save_for_backward(cols, wm)
+        ctx.w = w
         ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp, M, Mp, "direct" if direct else "cols")
         return y[:M].view(B, Ho, Wo, Cout)
 
@@ -109,7 +112,9 @@ class _Conv2d(torch.autograd.Function):
                 dwm = torch.empty((Cout, K), dtype=torch.float32, device=dy.device)
                 ws = G.workspace(dy.device, G.SPLITK_WS_ELEMS, "splitk")
                 gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws)
-                dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2).contiguous()
+                dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2)
+                tw = grad_target(ctx.w)
+                dw = tw.copy_(dw) if tw is not None else dw.contiguous()
             if ctx.needs_input_grad[0]:
                 if stride == 1 and _implicit_ok(Cout, B * H * W):
                     # stride-1 dgrad is itself a convolution of dY with the flipped, transposed
@@ -127,7 +132,9 @@ class _Conv2d(torch.autograd.Function):
         cols = saved
         if ctx.needs_input_grad[1]:
             dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
-            dw = dwm[:, :K].view(Cout, KH, KW, C).permute(0, 3, 1, 2).contiguous()
+            dw = dwm[:, :K].view(Cout, KH, KW, C).permute(0, 3, 1, 2)
+            tw = grad_target(ctx.w)
+            dw = tw.copy_(dw) if tw is not None else dw.contiguous()
         if ctx.needs_input_grad[0]:
             dcols = G.linear_dgrad(dy2, wm)  # [Mp, Kp] bf16
             if mode == "direct":
@@ -181,6 +188,7 @@ class _BatchNorm(torch.autograd.Function):
         gpu_ext().bn_fwd(x, res, y, mean, rstd, weight, bias, running_mean if training else None,
                          running_var if training else None, eps, momentum, training, relu, ws, nblk)
         ctx.save_for_backward(x, y if relu else None, mean, rstd, weight)
+        ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.has_res = residual is not None
         return y
@@ -193,8 +201,12 @@ class _BatchNorm(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        w, b = ctx.params
+        dgamma, dbeta = grad_target(w), grad_target(b)
+        if dgamma is None:
+            dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        if dbeta is None:
+            dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
         gpu_ext().bn_bwd(dy, y if ctx.relu else x, x, mean, rstd, weight, dx, dres, dgamma, dbeta, ctx.relu, ws, nblk)
@@ -289,6 +301,7 @@ class _Classifier(torch.autograd.Function):
         y = G.linear_fwd(xp, wp.contiguous(), bias=bp.contiguous())
         ctx.save_for_backward(xp, wp)
         ctx.meta = (Bn, N, Np, Mp)
+        ctx.params = (w, b)
         return y[:Bn, :N].contiguous()
 
     @staticmethod
@@ -297,9 +310,15 @@ class _Classifier(torch.autograd.Function):
         Bn, N, Np, Mp = ctx.meta
         dyp = torch.zeros((Mp, Np), dtype=torch.bfloat16, device=dy.device)
         dyp[:Bn, :N].copy_(dy)
+        w, b = ctx.params
         dx = G.linear_dgrad(dyp, wp)[:Bn] if ctx.needs_input_grad[0] else None
         dw = G.linear_wgrad(dyp, xp)[:N] if ctx.needs_input_grad[1] else None
         db = G.colsum(dyp)[:N] if ctx.needs_input_grad[2] else None
+        tw, tb = grad_target(w), grad_target(b)
+        if dw is not None and tw is not None:
+            dw = tw.copy_(dw)
+        if db is not None and tb is not None:
+            db = tb.copy_(db)
         return dx, dw, db
 
 

@@ -10,6 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from ._ext import gpu_ext
+from .gradbuf import grad_target
 from .shadow import shadow_of
 
 
@@ -23,6 +24,7 @@ class _Embedding(torch.autograd.Function):
         gpu_ext().embed_fwd(idx_c, shadow_of(wte), shadow_of(wpe) if wpe is not None else None, out, T)
         ctx.save_for_backward(idx_c)
         ctx.shapes = (wte.shape, None if wpe is None else wpe.shape)
+        ctx.params = (wte, wpe)
         return out
 
     @staticmethod
@@ -30,10 +32,13 @@ class _Embedding(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         B, T = idx.shape
         wte_shape, wpe_shape = ctx.shapes
-        dwte = torch.zeros(wte_shape, dtype=torch.float32, device=idx.device)
+        wte, wpe = ctx.params
+        dwte = grad_target(wte)
+        dwte = torch.zeros(wte_shape, dtype=torch.float32, device=idx.device) if dwte is None else dwte.zero_()
         dwpe = None
         if wpe_shape is not None:
-            dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device)
+            dwpe = grad_target(wpe)
+            dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device) if dwpe is None else dwpe.zero_()
         sidx, perm = torch.sort(idx.reshape(-1), stable=True)
         gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False)
         return None, dwte, dwpe

@@ -32,7 +32,7 @@ def workspace(device, numel: int, tag: str = "ws") -> torch.Tensor:
 
 def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, Cin=None, bias=None,
               aux_in=None, aux_out=None, alpha=1.0, beta=0.0, act=ACT_NONE, causal=CAUSAL_NONE,
-              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0), tile_cfg=-1):
+              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0), tile_cfg=-1, alpha_dev=None):
     sA0, sA1, sB0, sB1, sC0, sC1 = strides
     ws = None
     if act == ACT_NONE and bias is None and causal == CAUSAL_NONE and batch == 1 and M * N <= SPLITK_MAX_OUT:
@@ -40,7 +40,7 @@ def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, 
         ws = workspace(C.device, min(16 * M * N, SPLITK_WS_ELEMS), "splitk")
     gpu_ext().gemm_bf16(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
                         batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act, causal,
-                        ws, tile_cfg)
+                        ws, tile_cfg, alpha_dev)
     return C
 
 
@@ -55,23 +55,23 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     return y
 
 
-def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0):
-    """dx[M,K] = dy[M,N] @ w[N,K]  (optionally * act'(aux_in))."""
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None):
+    """dx[M,K] = alpha (* alpha_dev[0]) * dy[M,N] @ w[N,K]  (optionally * act'(aux_in))."""
     M, N = dy.shape
     K = w.shape[1]
     dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
-    gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha)
+    gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev)
     return dx
 
 
-def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0):
-    """dw[N,K] (fp32) = dy[M,N]^T @ x[M,K]."""
+def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0, alpha_dev=None):
+    """dw[N,K] (fp32) = alpha (* alpha_dev[0]) * dy[M,N]^T @ x[M,K]."""
     M, N = dy.shape
     K = x2d.shape[1]
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
     gemm_bf16(dy, x2d, out, N, K, M, N, K, K, False, False, Cin=out if accumulate else None,
-              beta=1.0 if accumulate else 0.0, alpha=alpha)
+              beta=1.0 if accumulate else 0.0, alpha=alpha, alpha_dev=alpha_dev)
     return out
 
 

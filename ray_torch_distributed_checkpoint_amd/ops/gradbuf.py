@@ -1,0 +1,28 @@
+"""Where a native backward writes a parameter gradient.
+
+With a FlatParamSpace in "fresh" mode (after `zero_grad(set_to_none=True)`) a parameter's
+first gradient contribution of the step is written by the producing kernel straight into
+the parameter's slice of the flat gradient buffer; torch's AccumulateGrad sees `p.grad is
+None` and adopts that tensor as `p.grad` without a copy (the stealing path of
+torch/csrc/autograd/functions/accumulate_grad.h), so there is neither an add kernel nor a
+memset of the buffer per step, and the DDP buckets / fused optimizer find the gradient in
+place.  A second contribution in the same step (tied weights) gets a fresh tensor and is
+added by autograd as usual; anything that ends up outside the buffer is folded back by the
+DDP hook / `FlatParamSpace.ensure_grad_views`.
+"""
+from __future__ import annotations
+
+import torch
+
+
+def grad_target(p: torch.Tensor | None) -> torch.Tensor | None:
+    """The flat-buffer view to write p's gradient into, or None (allocate normally)."""
+    if p is None:
+        return None
+    sp = getattr(p, "_rtdc_space", None)
+    if sp is None or sp.grad is None or not sp.fresh or p.grad is not None:
+        return None
+    if getattr(p, "_rtdc_claim", -1) == sp.step_id:
+        return None  # already handed out this step (second use of a tied weight)
+    p._rtdc_claim = sp.step_id
+    return sp.grad_view(p)

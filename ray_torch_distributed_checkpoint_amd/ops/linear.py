@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext
+from .gradbuf import grad_target
 from .shadow import shadow_of
 
 
@@ -42,6 +43,7 @@ class _LinearBF16(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.has_res = residual is not None
         ctx.in_shape = x.shape
+        ctx.params = (w, b)
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -52,9 +54,10 @@ class _LinearBF16(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dpre = _relu_mask_bwd(dy2, y) if ctx.relu else dy2
+        w, b = ctx.params
         dx = G.linear_dgrad(dpre, ws).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
-        dw = G.linear_wgrad(dpre, x2) if ctx.needs_input_grad[1] else None
-        db = G.colsum(dpre) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dw = G.linear_wgrad(dpre, x2, out=grad_target(w)) if ctx.needs_input_grad[1] else None
+        db = G.colsum(dpre, out=grad_target(b)) if ctx.has_b and ctx.needs_input_grad[2] else None
         dres = dy if ctx.has_res else None
         return dx, dw, db, dres, None
 
@@ -71,6 +74,7 @@ class _LinearF32(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_b = b is not None
         ctx.in_shape = x.shape
+        ctx.bias = b
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -86,10 +90,12 @@ class _LinearF32(torch.autograd.Function):
             G.gemm_f32(dpre, w, dx, M, K, N, N, 1, K, 1, K)
             dx = dx.view(ctx.in_shape)
         if ctx.needs_input_grad[1]:
-            dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+            dw = grad_target(w)
+            if dw is None:
+                dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
             G.gemm_f32(dpre, x2, dw, N, K, M, 1, N, K, 1, K)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = G.colsum(dpre)
+            db = G.colsum(dpre, out=grad_target(ctx.bias))
         return dx, dw, db, None
 
 
@@ -126,6 +132,7 @@ class _FusedMLP(torch.autograd.Function):
         ctx.save_for_backward(x2, wfs, wps, pre, g)
         ctx.has_res = residual is not None
         ctx.in_shape = x.shape
+        ctx.params = (w_fc, b_fc, w_proj, b_proj)
         return y.view(x.shape)
 
     @staticmethod
@@ -135,11 +142,12 @@ class _FusedMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, C)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dw_proj = G.linear_wgrad(dy2, g)
-        db_proj = G.colsum(dy2)
+        w_fc, b_fc, w_proj, b_proj = ctx.params
+        dw_proj = G.linear_wgrad(dy2, g, out=grad_target(w_proj))
+        db_proj = G.colsum(dy2, out=grad_target(b_proj))
         dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_GELU_BWD, aux_in=pre)
-        dw_fc = G.linear_wgrad(dpre, x2)
-        db_fc = G.colsum(dpre)
+        dw_fc = G.linear_wgrad(dpre, x2, out=grad_target(w_fc))
+        db_fc = G.colsum(dpre, out=grad_target(b_fc))
         dx = G.linear_dgrad(dpre, wfs).view(ctx.in_shape)
         return dx, dw_fc, db_fc, dw_proj, db_proj, (dy if ctx.has_res else None)
 

@@ -6,6 +6,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext
+from .gradbuf import grad_target
 from .shadow import shadow_of
 
 _tables: dict = {}
@@ -79,6 +80,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         res2 = residual.reshape(-1, C) if residual is not None else None
         y = G.linear_fwd(h, w2s, residual=res2)
         ctx.save_for_backward(x2, w13s, w2s, gu, h)
+        ctx.params = (w13, w2)
         ctx.has_res = residual is not None
         ctx.in_shape = x.shape
         return y.view(x.shape)
@@ -90,11 +92,12 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, C)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dw2 = G.linear_wgrad(dy2, h)
+        w13, w2 = ctx.params
+        dw2 = G.linear_wgrad(dy2, h, out=grad_target(w2))
         dh = G.linear_dgrad(dy2, w2s)
         dgu = torch.empty_like(gu)
         gpu_ext().swiglu_bwd(gu, dh, dgu)
-        dw13 = G.linear_wgrad(dgu, x2)
+        dw13 = G.linear_wgrad(dgu, x2, out=grad_target(w13))
         dx = G.linear_dgrad(dgu, w13s).view(ctx.in_shape)
         return dx, dw13, dw2, (dy if ctx.has_res else None)
 

@@ -6,6 +6,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext
+from .gradbuf import grad_target
 from .shadow import shadow_of
 
 
@@ -20,8 +21,13 @@ def _bwd_ws_elems(nw: int, D: int) -> int:
 
 
 class _LayerNorm(torch.autograd.Function):
+    """y = LN(x).  With passthrough=True also returns x itself (the residual stream): its
+    gradient arrives as a second output gradient and is added inside the backward kernel
+    (dres) instead of by a separate autograd add."""
+
     @staticmethod
-    def forward(ctx, x, w, b, eps):
+    def forward(ctx, x, w, b, eps, passthrough=False):
+        ctx.set_materialize_grads(False)
         D = x.shape[-1]
         xc = x.contiguous()
         M = xc.numel() // D
@@ -31,25 +37,34 @@ class _LayerNorm(torch.autograd.Function):
         ws, bs = shadow_of(w), shadow_of(b)
         gpu_ext().layernorm_fwd(xc, ws, bs, y, mean, rstd, eps)
         ctx.save_for_backward(xc, ws, mean, rstd)
-        return y
+        ctx.params = (w, b)
+        return (y, xc) if passthrough else y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dpass=None):
         xc, ws, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(xc)
         D = xc.shape[-1]
         M = xc.numel() // D
         nw = _bwd_waves(M)
         wsp = G.workspace(xc.device, _bwd_ws_elems(nw, D), "ln_bwd")
         dx = torch.empty_like(xc)
-        dg = torch.empty(D, dtype=torch.float32, device=xc.device)
-        db = torch.empty(D, dtype=torch.float32, device=xc.device)
-        gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, None, dx, wsp, dg, db, nw, False)
-        return dx, dg, db, None
+        w, b = ctx.params
+        dg, db = grad_target(w), grad_target(b)
+        if dg is None or db is None:
+            dgb = torch.empty((2, D), dtype=torch.float32, device=xc.device)
+            dg = dgb[0] if dg is None else dg
+            db = dgb[1] if db is None else db
+        dres = dpass.contiguous() if dpass is not None else None
+        gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, dres, dx, wsp, dg, db, nw, False)
+        return dx, dg, db, None, None
 
 
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, eps):
+    def forward(ctx, x, w, eps, passthrough=False):
+        ctx.set_materialize_grads(False)
         D = x.shape[-1]
         xc = x.contiguous()
         M = xc.numel() // D
@@ -58,30 +73,40 @@ class _RMSNorm(torch.autograd.Function):
         ws = shadow_of(w)
         gpu_ext().rmsnorm_fwd(xc, ws, y, rstd, eps)
         ctx.save_for_backward(xc, ws, rstd)
-        return y
+        ctx.w = w
+        return (y, xc) if passthrough else y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dpass=None):
         xc, ws, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(xc)
         D = xc.shape[-1]
         M = xc.numel() // D
         nw = _bwd_waves(M)
         wsp = G.workspace(xc.device, _bwd_ws_elems(nw, D), "rms_bwd")
         dx = torch.empty_like(xc)
-        dg = torch.empty(D, dtype=torch.float32, device=xc.device)
-        gpu_ext().rmsnorm_bwd(dy.contiguous(), xc, ws, rstd, None, dx, wsp, dg, nw, False)
-        return dx, dg, None
+        dg = grad_target(ctx.w)
+        if dg is None:
+            dg = torch.empty(D, dtype=torch.float32, device=xc.device)
+        dres = dpass.contiguous() if dpass is not None else None
+        gpu_ext().rmsnorm_bwd(dy.contiguous(), xc, ws, rstd, dres, dx, wsp, dg, nw, False)
+        return dx, dg, None, None
 
 
-def layer_norm(x, w, b, eps=1e-5):
+def layer_norm(x, w, b, eps=1e-5, passthrough=False):
+    """LayerNorm over the last axis; passthrough=True returns (y, x) with the residual-stream
+    gradient fused into the backward kernel."""
     if not x.is_cuda or x.dtype != torch.bfloat16:
-        return F.layer_norm(x, (x.shape[-1],), w.to(x.dtype), b.to(x.dtype), eps)
-    return _LayerNorm.apply(x, w, b, eps)
+        y = F.layer_norm(x, (x.shape[-1],), w.to(x.dtype), b.to(x.dtype), eps)
+        return (y, x) if passthrough else y
+    return _LayerNorm.apply(x, w, b, eps, passthrough)
 
 
-def rms_norm(x, w, eps=1e-5):
+def rms_norm(x, w, eps=1e-5, passthrough=False):
     if not x.is_cuda or x.dtype != torch.bfloat16:
         xf = x.float()
         y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
-        return (y * w.float()).to(x.dtype)
-    return _RMSNorm.apply(x, w, eps)
+        y = (y * w.float()).to(x.dtype)
+        return (y, x) if passthrough else y
+    return _RMSNorm.apply(x, w, eps, passthrough)

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext
+from .gradbuf import grad_target
 from .shadow import shadow_of
 
 IGNORE_INDEX = -100
@@ -61,16 +62,16 @@ class _LMHeadXent(torch.autograd.Function):
                        1.0 / n_valid, IGNORE_INDEX)
         ctx.save_for_backward(x2, ws, logits)
         ctx.in_shape = x.shape
+        ctx.w = w
         return loss.sum() / n_valid
 
     @staticmethod
     def backward(ctx, g):
         x2, ws, dlogits = ctx.saved_tensors
-        dx = G.linear_dgrad(dlogits, ws)
-        dw = G.linear_wgrad(dlogits, x2)
-        gs = g.to(torch.float32)
-        dx.mul_(gs.to(dx.dtype))
-        dw.mul_(gs)
+        # the upstream loss gradient is applied as a device-side alpha inside both GEMMs
+        gs = g.detach().to(torch.float32).reshape(1).contiguous()
+        dx = G.linear_dgrad(dlogits, ws, alpha_dev=gs)
+        dw = G.linear_wgrad(dlogits, x2, out=grad_target(ctx.w), alpha_dev=gs)
         return dx.view(ctx.in_shape), dw, None, None, None
 
 

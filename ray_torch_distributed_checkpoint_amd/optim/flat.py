@@ -43,12 +43,19 @@ class FlatParamSpace:
         self.params = uniq
         self.device = torch.device(device) if device is not None else uniq[0].device
         self.segments: list[Segment] = []
+        # "fresh" gradient mode (zero_grad(set_to_none=True)): p.grad is None until the first
+        # contribution of the step, which the native backward writes straight into the flat
+        # view (ops.gradbuf.grad_target); AccumulateGrad then adopts that view without a copy
+        # or an add, and no memset of the buffer is needed.
+        self.fresh = False
+        self.step_id = 0
         off = 0
         for i, p in enumerate(uniq):
             assert p.dtype == torch.float32, "FlatParamSpace holds fp32 master parameters"
             self.segments.append(Segment(i, off, p.numel(), tuple(p.shape)))
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
+        self._seg_of = {id(p): s for p, s in zip(uniq, self.segments)}
         self.data = torch.zeros(off, dtype=torch.float32, device=self.device)
         with torch.no_grad():
             for p, s in zip(uniq, self.segments):
@@ -72,10 +79,13 @@ class FlatParamSpace:
         return buf[s.offset:s.offset + s.numel].view(s.shape)
 
     def segment_of(self, p) -> Segment:
-        for q, s in zip(self.params, self.segments):
-            if q is p:
-                return s
-        raise KeyError("parameter not in this space")
+        s = self._seg_of.get(id(p))
+        if s is None or self.params[s.index] is not p:
+            raise KeyError("parameter not in this space")
+        return s
+
+    def grad_view(self, p) -> torch.Tensor:
+        return self.view(self.grad, self.segment_of(p))
 
     def refresh_shadows(self):
         if self.shadow is None:
@@ -86,27 +96,37 @@ class FlatParamSpace:
         for p, s in zip(self.params, self.segments):
             bind_shadow(p, self.view(self.shadow, s))
 
-    def zero_grad(self):
-        if self.grad is not None:
-            self.grad.zero_()
-            for p, s in zip(self.params, self.segments):
-                v = self.view(self.grad, s)
-                if p.grad is None or p.grad.data_ptr() != v.data_ptr():
-                    p.grad = v
+    def zero_grad(self, set_to_none: bool = False):
+        if self.grad is None:
+            return
+        if set_to_none:
+            for p in self.params:
+                p.grad = None
+            self.fresh = True
+            self.step_id += 1
+            return
+        self.fresh = False
+        self.grad.zero_()
+        for p, s in zip(self.params, self.segments):
+            v = self.view(self.grad, s)
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
 
     def ensure_grad_views(self):
         """Re-attach grads that were replaced (e.g. zero_grad(set_to_none=True))."""
         if self.grad is None:
             return
+        base = self.grad.data_ptr()
         for p, s in zip(self.params, self.segments):
-            v = self.view(self.grad, s)
             g = p.grad
+            if g is not None and g.data_ptr() == base + 4 * s.offset:
+                continue
+            v = self.view(self.grad, s)
             if g is None:
                 v.zero_()
-                p.grad = v
-            elif g.data_ptr() != v.data_ptr():
+            else:
                 v.copy_(g)
-                p.grad = v
+            p.grad = v
 
     def chunk_table(self, params_subset, decay_flags) -> tuple[torch.Tensor, int]:
         """int64 [nchunks, 2] rows of (start, len | decay<<32) for the native optimizer kernels."""

@@ -87,7 +87,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = True):
         if self._space is not None and self._space.grad is not None:
-            self._space.zero_grad()
+            self._space.zero_grad(set_to_none=set_to_none)
         else:
             super().zero_grad(set_to_none=set_to_none)
 
