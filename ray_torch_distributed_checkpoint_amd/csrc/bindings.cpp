@@ -10,6 +10,7 @@
 
 #include "kernels/args.h"
 #include "runtime/ckpt_engine.cpp"
+#include "runtime/reducer.cpp"
 
 using torch::Tensor;
 namespace py = pybind11;
@@ -461,6 +462,22 @@ static py::tuple plan_layout(const py::list& arcs) {
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  py::class_<rtdc_ddp::GradBucketEngine>(m, "GradBucketEngine")
+      .def(py::init([](at::Tensor flat, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
+                       std::vector<std::pair<int64_t, int64_t>> seg, py::object pg, bool use_avg, double post_scale) {
+             auto cpg = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
+             return new rtdc_ddp::GradBucketEngine(flat, std::move(bounds), std::move(param_bucket), std::move(seg),
+                                                   cpg, use_avg, post_scale);
+           }),
+           py::arg("flat_grad"), py::arg("bounds"), py::arg("param_bucket"), py::arg("segments"),
+           py::arg("process_group"), py::arg("use_avg"), py::arg("post_scale"))
+      .def("mark_ready", &rtdc_ddp::GradBucketEngine::mark_ready)
+      .def("finalize", &rtdc_ddp::GradBucketEngine::finalize)
+      .def("num_buckets", &rtdc_ddp::GradBucketEngine::num_buckets)
+      .def("launched", &rtdc_ddp::GradBucketEngine::launched)
+      .def("steps", &rtdc_ddp::GradBucketEngine::steps)
+      .def("bucket_bytes", &rtdc_ddp::GradBucketEngine::bucket_bytes);
+
   m.doc() = "MI355X (gfx950) kernels and native checkpoint engine";
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_f32", &gemm_f32);

@@ -1,0 +1,109 @@
+// Native gradient-bucket engine for data-parallel training (the MI355X-native counterpart of
+// c10d's C++ Reducer, T/include/torch/csrc/distributed/c10d/reducer.hpp:30-31,135,279,329,499,523).
+//
+// The gradients of all parameters live in ONE flat fp32 buffer (optim/flat.py).  A bucket is
+// a contiguous [lo, hi) slice of it, fixed at construction (static plan in backward order:
+// a small first bucket, then `bucket_cap` buckets - see parallel/ddp.py for the sizing
+// rationale for 7 xGMI links).  Per step:
+//   * mark_ready(p) is called from each parameter's post-accumulate-grad hook; it counts the
+//     bucket down and launches every bucket whose turn has come, strictly in bucket order
+//     (identical collective order on every rank - no rendezvous needed),
+//   * the all-reduce runs IN PLACE on the slice on the process group's own stream (RCCL over
+//     xGMI; averaging folded into the collective with ReduceOp::AVG), overlapped with the
+//     rest of the backward pass - no copy-in/copy-out, no pre-divide kernel,
+//   * finalize() (queued at the end of backward) launches what is left (parameters that got
+//     no gradient), waits for every Work - which on RCCL makes the current stream wait, not
+//     the host - applies the 1/world post-scale for backends without AVG (gloo), and resets.
+// Bucket bookkeeping is lock-free single-threaded state: autograd invokes the hooks from
+// one engine thread per device.
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Work.hpp>
+
+namespace rtdc_ddp {
+
+class GradBucketEngine {
+ public:
+  // seg: per parameter (offset, numel) inside flat_grad, same order as param_bucket
+  GradBucketEngine(at::Tensor flat_grad, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
+                   std::vector<std::pair<int64_t, int64_t>> seg, c10::intrusive_ptr<c10d::ProcessGroup> pg,
+                   bool use_avg, double post_scale)
+      : flat_(std::move(flat_grad)), bounds_(std::move(bounds)), param_bucket_(std::move(param_bucket)),
+        seg_(std::move(seg)), pg_(std::move(pg)), use_avg_(use_avg), post_scale_(post_scale) {
+    TORCH_CHECK(seg_.size() == param_bucket_.size(), "one segment per parameter");
+    TORCH_CHECK(bounds_.size() >= 2, "need at least one bucket");
+    const size_t nb = bounds_.size() - 1;
+    expected_.assign(nb, 0);
+    for (int64_t b : param_bucket_) {
+      TORCH_CHECK(b >= 0 && (size_t)b < nb, "bad bucket index");
+      expected_[b] += 1;
+    }
+    pending_ = expected_;
+    works_.resize(nb);
+    launched_.assign(nb, false);
+    marked_.assign(param_bucket_.size(), false);
+  }
+
+  void mark_ready(int64_t param_idx) {
+    TORCH_CHECK(param_idx >= 0 && (size_t)param_idx < param_bucket_.size(), "bad parameter index");
+    if (marked_[param_idx]) return;  // a second gradient of the same parameter this step
+    marked_[param_idx] = true;
+    pending_[param_bucket_[param_idx]] -= 1;
+    launch_ready();
+  }
+
+  void finalize() {
+    // parameters that produced no gradient this step contribute zeros (their slots may hold
+    // a previous step's values when gradients are written in place): only unlaunched
+    // buckets can contain them
+    for (size_t i = 0; i < marked_.size(); ++i)
+      if (!marked_[i]) flat_.slice(0, seg_[i].first, seg_[i].first + seg_[i].second).zero_();
+    while (next_ < works_.size()) launch(next_++);
+    {
+      pybind11::gil_scoped_release nogil;
+      for (auto& w : works_)
+        if (w) w->wait();
+    }
+    if (!use_avg_ && post_scale_ != 1.0) flat_.mul_(post_scale_);
+    for (auto& w : works_) w.reset();
+    pending_ = expected_;
+    std::fill(launched_.begin(), launched_.end(), false);
+    std::fill(marked_.begin(), marked_.end(), false);
+    next_ = 0;
+    ++steps_;
+  }
+
+  int64_t num_buckets() const { return (int64_t)works_.size(); }
+  int64_t steps() const { return steps_; }
+  int64_t launched() const { return (int64_t)next_; }
+  std::vector<int64_t> bucket_bytes() const {
+    std::vector<int64_t> out;
+    for (size_t b = 0; b + 1 < bounds_.size(); ++b) out.push_back((bounds_[b + 1] - bounds_[b]) * 4);
+    return out;
+  }
+
+ private:
+  void launch_ready() {
+    while (next_ < works_.size() && pending_[next_] <= 0) launch(next_++);
+  }
+
+  void launch(size_t b) {
+    std::vector<at::Tensor> t{flat_.slice(0, bounds_[b], bounds_[b + 1])};
+    c10d::AllreduceOptions opts;
+    opts.reduceOp = use_avg_ ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
+    works_[b] = pg_->allreduce(t, opts);
+    launched_[b] = true;
+  }
+
+  at::Tensor flat_;
+  std::vector<int64_t> bounds_, param_bucket_, expected_, pending_;
+  std::vector<std::pair<int64_t, int64_t>> seg_;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  bool use_avg_;
+  double post_scale_;
+  std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  std::vector<bool> launched_, marked_;
+  size_t next_ = 0;
+  int64_t steps_ = 0;
+};
+
+}  // namespace rtdc_ddp

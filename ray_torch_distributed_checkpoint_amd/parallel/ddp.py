@@ -25,6 +25,7 @@ MI355X:
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -110,9 +111,31 @@ class DistributedDataParallel(nn.Module):
         self._require_sync = True
         self._callback_queued = False
         self._hooks = []
+        self._pidx = {id(p): i for i, p in enumerate(self.space.params)}
+        self._engine = None
         if self.world_size > 1:
+            self._engine = self._native_engine(process_group)
             for p in self.space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+
+    def _native_engine(self, process_group):
+        """C++ bucket engine (csrc/runtime/reducer.cpp); RTDC_DDP_ENGINE=python keeps the
+        Python reference implementation of the same protocol."""
+        if os.environ.get("RTDC_DDP_ENGINE", "native") == "python":
+            return None
+        from ..ops._ext import ext
+
+        mod = ext()
+        if mod is None or not hasattr(mod, "GradBucketEngine"):
+            return None
+        for a, b in zip(self.buckets, self.buckets[1:]):
+            assert a.end == b.start, "buckets must tile the flat gradient buffer"
+        bounds = [b.start for b in self.buckets] + [self.buckets[-1].end]
+        param_bucket = [self._bucket_of[id(p)].index for p in self.space.params]
+        segs = [(s.offset, s.numel) for s in self.space.segments]
+        pg = process_group if process_group is not None else dist.distributed_c10d._get_default_group()
+        return mod.GradBucketEngine(self.space.grad, bounds, param_bucket, segs, pg, self._use_avg,
+                                    1.0 / self.world_size)
 
     # ------------------------------------------------------------------ buffers
     def _sync_buffers(self):
@@ -162,6 +185,9 @@ class DistributedDataParallel(nn.Module):
                 with torch.no_grad():
                     seg_view.copy_(g)
                 p.grad = seg_view
+        if self._engine is not None:
+            self._engine.mark_ready(self._pidx[id(p)])
+            return
         b = self._bucket_of[id(p)]
         b.pending -= 1
         self._launch_ready()
@@ -178,6 +204,10 @@ class DistributedDataParallel(nn.Module):
             self._next += 1
 
     def _finalize(self):
+        self._callback_queued = False
+        if self._engine is not None:
+            self._engine.finalize()
+            return
         # params that produced no gradient this step: zero-filled grads, still reduced
         while self._next < len(self.buckets):
             b = self.buckets[self._next]

@@ -8,7 +8,8 @@ import torch.distributed as dist
 from tests import mp_util
 
 
-def _ddp_equiv(rank, world, seed):
+def _ddp_equiv(rank, world, seed, engine="native"):
+    os.environ["RTDC_DDP_ENGINE"] = engine
     from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
 
     torch.manual_seed(seed)
@@ -21,6 +22,7 @@ def _ddp_equiv(rank, world, seed):
     ours = DistributedDataParallel(ours_m, bucket_cap_mb=0.01, first_bucket_mb=0.005)
     ref = torch.nn.parallel.DistributedDataParallel(ref_m)
     assert len(ours.buckets) > 1
+    assert (ours._engine is not None) == (engine == "native")
     opt_o = torch.optim.SGD(ours.parameters(), lr=0.1, momentum=0.9)
     opt_r = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
     g = torch.Generator().manual_seed(100 + rank)
@@ -38,6 +40,47 @@ def _ddp_equiv(rank, world, seed):
 def test_ddp_matches_torch_ddp():
     out = mp_util.run(_ddp_equiv, 2, 0)
     assert max(out) < 1e-5, out
+
+
+def test_ddp_python_engine_matches_torch_ddp():
+    out = mp_util.run(_ddp_equiv, 2, 1, "python")
+    assert max(out) < 1e-5, out
+
+
+def _ddp_unused(rank, world):
+    """A parameter without a gradient in a step contributes zeros (in-place gradient mode)."""
+    from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    m = torch.nn.ModuleDict({"a": torch.nn.Linear(8, 8), "b": torch.nn.Linear(8, 8)})
+
+    class Net(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, x, use_b):
+            y = self.m["a"](x)
+            return self.m["b"](y) if use_b else y
+
+    net = DistributedDataParallel(Net(m), bucket_cap_mb=0.0005, first_bucket_mb=0.0002)
+    opt = FusedSGD(net.parameters(), lr=0.1)
+    x = torch.randn(4, 8) * (rank + 1)
+    net(x, True).sum().backward()
+    opt.step()
+    opt.zero_grad()
+    w_before = m["b"].weight.detach().clone()
+    net(x, False).sum().backward()
+    gb = m["b"].weight.grad
+    ok = gb is None or float(gb.abs().max()) == 0.0
+    opt.step()
+    return ok and torch.equal(w_before, m["b"].weight.detach())
+
+
+def test_ddp_unused_parameter_zero_grad():
+    out = mp_util.run(_ddp_unused, 2)
+    assert all(out), out
 
 
 def _sampler(rank, world):
