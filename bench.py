@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--no-ckpt", action="store_true")
     ap.add_argument("--ckpt-dir", default=None)
+    ap.add_argument("--ckpt-scope", default="full", choices=["full", "model"],
+                    help="full = model + optimizer train state (default); model = weights only")
     ap.add_argument("--overlap-steps", type=int, default=5)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (multi-rank rehearsal on 1 GPU)")
     args = ap.parse_args()
@@ -229,9 +231,26 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
 
     from ray_torch_distributed_checkpoint_amd.checkpoint.state_dict import get_state_dict, set_state_dict
 
+    scope = args.ckpt_scope
+
     def state():
         msd, osd = get_state_dict(model, opt)
-        return {"model": msd, "optim": osd, "step": 1}
+        return {"model": msd, "optim": osd, "step": 1} if scope == "full" else {"model": msd, "step": 1}
+
+    def nbytes_of(sd):
+        if torch.is_tensor(sd):
+            return sd.numel() * sd.element_size()
+        if isinstance(sd, dict):
+            return sum(nbytes_of(v) for v in sd.values())
+        return 0
+
+    # the box's scratch disk bounds what one rank can write (Llama-3-8B full train state is
+    # 96 GB on one GPU, 12 GB per rank at 8): fall back to the model shard if it does not fit
+    free = shutil.disk_usage(base).free
+    if scope == "full" and nbytes_of(state()) / max(world, 1) * 1.15 > free:
+        scope = "model"
+    if nbytes_of(state()) / max(world, 1) * 1.15 > free:
+        return {"ckpt_skipped": f"state larger than free disk ({free / 1e9:.0f} GB)"}
 
     # ---- async save overlapped with training steps
     torch.cuda.synchronize()
@@ -253,6 +272,8 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     nbytes = torch.tensor([float(h.nbytes)], device=dev)
     if world > 1:
         dist.all_reduce(nbytes)
+    if rank == 0:
+        shutil.rmtree(path, ignore_errors=True)  # keep one checkpoint on disk at a time
     # ---- blocking save (nothing overlapped) for the pure write bandwidth
     path2 = path + "_sync"
     if rank == 0:
@@ -270,7 +291,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     t3 = time.perf_counter()
     sd = state()
     dcp.load(sd, path2)
-    set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd["optim"])
+    set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -293,6 +314,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
         "ckpt_write_GBps": round(total / max(t_sync, 1e-9) / 1e9, 3),
         "ms_per_step_during_async_save": round(overlap_ms, 3),
         "ckpt_format": "torch.distributed.checkpoint (.metadata + __r_0.distcp), native engine",
+        "ckpt_scope": "model + optimizer + step" if scope == "full" else "model + step",
     }
 
 
