@@ -51,7 +51,7 @@ int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* o
 int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe, int B, int T,
                    int D, int accumulate_wpe, hipStream_t st);
 int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
-                 unsigned long long offset, int is_bf16, hipStream_t st);
+                 unsigned long long offset, const long long* off_dev, int is_bf16, hipStream_t st);
 int rtdc_relu_dropout(const void* h, void* y, const void* dy, void* dx, long long n, float p,
                       unsigned long long seed, unsigned long long offset, int backward, int is_bf16,
                       hipStream_t st);
@@ -261,8 +261,11 @@ static void embed_bwd(Tensor sidx, Tensor perm, Tensor dout, Tensor dwte, c10::o
                           (float*)ptr_or_null(dwpe), (int)B, (int)T, D, accumulate_wpe, cur_stream()),
            "embed_bwd");
 }
-static void dropout(Tensor x, Tensor y, double p, uint64_t seed, uint64_t offset) {
+static void dropout(Tensor x, Tensor y, double p, uint64_t seed, uint64_t offset, c10::optional<Tensor> off_dev) {
+  TORCH_CHECK(!off_dev.has_value() || (off_dev->scalar_type() == at::kLong && off_dev->is_cuda()),
+              "dropout: off_dev must be an int64 GPU tensor");
   check_rc(rtdc_dropout(x.data_ptr(), y.data_ptr(), (long long)x.numel(), (float)p, seed, offset,
+                        off_dev.has_value() ? (const long long*)off_dev->data_ptr<int64_t>() : nullptr,
                         x.scalar_type() == at::kBFloat16, cur_stream()),
            "dropout");
 }

@@ -93,8 +93,10 @@ template <> __device__ __forceinline__ void stx<bf16_t>(bf16_t* p, long long i, 
 
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long long n, float p,
-                                                     unsigned long long seed, unsigned long long offset) {
+                                                     unsigned long long seed, unsigned long long offset,
+                                                     const long long* __restrict__ off_dev) {
   const float scale = 1.f / (1.f - p);
+  if (off_dev) offset += (unsigned long long)*off_dev;  // graph replay: per-step base on device
   for (long long q = blockIdx.x * 256LL + threadIdx.x; q * 4 < n; q += gridDim.x * 256LL) {
     uint4 r = Philox::gen(seed, 0, offset + q);
     uint32_t rr[4] = {r.x, r.y, r.z, r.w};
@@ -170,15 +172,16 @@ extern "C" int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const vo
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// off_dev (optional): device-resident counter base added to `offset` (hipGraph replays)
 extern "C" int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
-                            unsigned long long offset, int is_bf16, hipStream_t st) {
+                            unsigned long long offset, const long long* off_dev, int is_bf16, hipStream_t st) {
   const unsigned g = ew_grid((n + 3) / 4);
   if (is_bf16)
     hipLaunchKernelGGL((dropout_kernel<bf16_t>), dim3(g), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y, n, p,
-                       seed, offset);
+                       seed, offset, off_dev);
   else
     hipLaunchKernelGGL((dropout_kernel<float>), dim3(g), dim3(256), 0, st, (const float*)x, (float*)y, n, p,
-                       seed, offset);
+                       seed, offset, off_dev);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

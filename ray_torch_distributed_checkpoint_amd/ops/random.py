@@ -11,10 +11,35 @@ import threading
 
 
 class PhiloxStream:
+    """In graph mode (a captured hipGraph step, utils/graphs.py) the counter base lives in a
+    device int64 (`device_base`): kernels add it to the step-relative offsets recorded at
+    capture time, and the captured step ends with `base += consumed`, so every replay draws
+    fresh masks while the host never runs."""
+
     def __init__(self, seed: int = 0x5EED, offset: int = 0):
         self.seed = int(seed) & ((1 << 64) - 1)
         self.offset = int(offset)
         self._lock = threading.Lock()
+        self._base = None  # device counter base in graph mode
+
+    def device_base(self):
+        return self._base
+
+    def enter_graph_mode(self, device) -> None:
+        import torch
+
+        self._base = torch.tensor([self.offset], dtype=torch.int64, device=device)
+        self.offset = 0
+
+    def end_graph_step(self) -> None:
+        """Called inside the capture after the step's last dropout: advance the device base."""
+        self._base.add_(self.offset)
+        self.offset = 0
+
+    def exit_graph_mode(self) -> None:
+        if self._base is not None:
+            self.offset = int(self._base.item()) + self.offset
+            self._base = None
 
     def reserve(self, numel: int) -> tuple[int, int]:
         """Reserve counters for `numel` elements; returns (seed, offset)."""
@@ -25,11 +50,16 @@ class PhiloxStream:
         return self.seed, off
 
     def state_dict(self) -> dict:
-        return {"seed": self.seed, "offset": self.offset}
+        off = self.offset if self._base is None else int(self._base.item()) + self.offset
+        return {"seed": self.seed, "offset": off}
 
     def load_state_dict(self, sd: dict) -> None:
         self.seed = int(sd["seed"])
-        self.offset = int(sd["offset"])
+        if self._base is not None:
+            self._base.fill_(int(sd["offset"]))
+            self.offset = 0
+        else:
+            self.offset = int(sd["offset"])
 
 
 _default = PhiloxStream()

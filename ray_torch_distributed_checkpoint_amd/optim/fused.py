@@ -137,6 +137,9 @@ class FusedAdamW(_FlatOptimizer):
             with torch.enable_grad():
                 loss = closure()
         if self._use_native():
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedAdamW computes bias corrections on the host per step: not graph-capturable "
+                                   "(use eager steps, or FusedSGD inside utils.graphs.CapturedStep)")
             sp = self._ensure_space()
             sp.ensure_grad_views()
             ext = gpu_ext()

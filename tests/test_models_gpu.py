@@ -122,3 +122,58 @@ def test_llama_tiny_matches_reference_and_trains():
         opt.step()
         losses.append(l.item())
     assert losses[-1] < losses[0] - 1.0, losses
+
+
+def test_toy_mlp_hipgraph_step_matches_eager():
+    """Whole-step hipGraph capture (utils/graphs.py) of the toy model: replays reproduce the
+    eager steps bit for bit, dropout masks included (device-side Philox base)."""
+    import torch.nn.functional as F
+
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.models import NeuralNetwork
+    from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
+    from ray_torch_distributed_checkpoint_amd.utils.graphs import CapturedStep
+
+    torch.manual_seed(0)
+    base = NeuralNetwork()
+    xs = torch.randn(12, 16, 1, 28, 28, device="cuda")
+    ys = torch.randint(0, 10, (12, 16), device="cuda")
+
+    def run(graph):
+        m = copy.deepcopy(base).cuda()
+        opt = FusedSGD(m.parameters(), lr=1e-2, momentum=0.9)
+        ops.manual_seed(77)
+        x, y = xs[0].clone(), ys[0].clone()
+
+        def step():
+            opt.zero_grad()
+            loss = ops.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+        losses = []
+        if graph:
+            cs = CapturedStep(step, warmup=3)  # the 3 warm-up steps consume batch 0
+            for i in range(3):
+                x.copy_(xs[0])
+                y.copy_(ys[0])
+            for i in range(3, 12):
+                x.copy_(xs[i])
+                y.copy_(ys[i])
+                losses.append(cs.replay().clone())
+            cs.close()
+        else:
+            for i in range(12):
+                x.copy_(xs[0] if i < 3 else xs[i])
+                y.copy_(ys[0] if i < 3 else ys[i])
+                lo = step()
+                if i >= 3:
+                    losses.append(lo)
+        return torch.stack(losses), [p.detach().clone() for p in m.parameters()], ops.default_stream().state_dict()
+
+    le, pe, se = run(False)
+    lg, pg, sg = run(True)
+    assert torch.equal(le, lg), (le, lg)
+    assert all(torch.equal(a, b) for a, b in zip(pe, pg))
+    assert se == sg
