@@ -1,0 +1,74 @@
+"""Causal flash attention microbenchmark (native fwd/bwd vs torch SDPA) on the GPT-2-small and
+Llama-3-8B shapes; random operands, one process, interleaved repetitions.
+
+    python benchmarks/attn_bench.py [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention  # noqa: E402
+
+SHAPES = [("gpt2", 16, 1024, 12, 12, 64), ("llama8b", 1, 2048, 32, 8, 128), ("llama8b_b4", 4, 2048, 32, 8, 128)]
+
+
+def timeit(fn, reps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    for name, B, T, H, Hkv, Dh in SHAPES:
+        W = (H + 2 * Hkv) * Dh
+        qkv = (torch.randn(B, T, W, device="cuda") * 0.5).bfloat16().requires_grad_(True)
+        flops_f = 2 * 2 * B * H * T * T * Dh / 2  # causal
+        y = causal_attention(qkv, H, Hkv)
+        dy = torch.randn_like(y)
+        t_f = min(timeit(lambda: causal_attention(qkv, H, Hkv), args.reps) for _ in range(3))
+
+        def fb():
+            out = causal_attention(qkv, H, Hkv)
+            out.backward(dy)
+
+        t_fb = min(timeit(fb, args.reps) for _ in range(3))
+        q = qkv.detach()[..., : H * Dh].view(B, T, H, Dh).transpose(1, 2).contiguous().requires_grad_(True)
+        k = qkv.detach()[..., H * Dh:(H + Hkv) * Dh].view(B, T, Hkv, Dh).transpose(1, 2)
+        v = qkv.detach()[..., (H + Hkv) * Dh:].view(B, T, Hkv, Dh).transpose(1, 2)
+        k = k.repeat_interleave(H // Hkv, 1).contiguous().requires_grad_(True)
+        v = v.repeat_interleave(H // Hkv, 1).contiguous().requires_grad_(True)
+        t_sf = min(timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True), args.reps) for _ in range(3))
+        do = torch.randn(B, H, T, Dh, device="cuda", dtype=torch.bfloat16)
+
+        def sfb():
+            F.scaled_dot_product_attention(q, k, v, is_causal=True).backward(do)
+
+        t_sfb = min(timeit(sfb, args.reps) for _ in range(3))
+        print(json.dumps({"shape": name, "B": B, "T": T, "H": H, "Hkv": Hkv, "Dh": Dh,
+                          "fwd_us": round(t_f * 1e6, 1), "fwd_TF": round(flops_f / t_f / 1e12, 1),
+                          "bwd_us": round((t_fb - t_f) * 1e6, 1),
+                          "bwd_TF": round(2.5 * flops_f / (t_fb - t_f) / 1e12, 1),
+                          "sdpa_fwd_us": round(t_sf * 1e6, 1), "sdpa_fwd_TF": round(flops_f / t_sf / 1e12, 1),
+                          "sdpa_bwd_us": round((t_sfb - t_sf) * 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

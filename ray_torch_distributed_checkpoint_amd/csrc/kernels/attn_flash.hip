@@ -24,6 +24,8 @@
 // Requires T % 64 == 0 and Dh in {64, 128}.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace rtdc {
 namespace fa {
 
@@ -212,6 +214,147 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
     *(uint2*)(orow + 16 * d + 4 * g) = v;
   }
   if (g == 0) a.lse[(long long)bh * a.T + myq] = (m + log2f(l)) / LOG2E;
+}
+
+// Forward, 32 query rows per wave (block = 128 rows): every K fragment read from LDS feeds
+// two S MFMAs and every V fragment two P.V MFMAs, halving LDS bytes per FLOP - with 16 rows
+// per wave the loop is LDS-read bound (8 waves/CU x 16 KiB per 64-key tile vs 128 B/clk),
+// with 32 it balances against the MFMA pipe.  Same accumulator-as-operand layout as above.
+template <int DH>
+__global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2, QG = 2, BQ2 = 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K[2], V[2]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = a.T / BQ2;
+  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest (longest causal prefix) blocks first
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int grp = a.H / a.Hkv, kvh = h / grp;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const int qcol = h * DH, kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int q0w = qb * BQ2 + wave * 32;  // this wave: rows [q0w, q0w + 32)
+  int myq[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) myq[qg] = q0w + 16 * qg + (lane & 15);
+  const float c = a.scale * LOG2E;
+
+  bf16x8 qf[QG][KS];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = gload8(base + (long long)myq[qg] * W + qcol + ks * 32 + g * 8);
+
+  f32x4 o[QG][DT];
+  float m[QG], l[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    m[qg] = -INFINITY;
+    l[qg] = 0.f;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[qg][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (2 + (s)) * TILE)
+  const int nkb = (qb + 1) * (BQ2 / BKV);
+  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
+  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) {
+      stage<DH>(base, W, (kb + 1) * BKV, kcol, KT(cur ^ 1), wave, lane);
+      stage<DH>(base, W, (kb + 1) * BKV, vcol, VT(cur ^ 1), wave, lane);
+    }
+    // keys of this tile all after this wave's last row: nothing to add (barriers still run)
+    if (kb * BKV <= q0w + 31) {
+      const char* kt = KT(cur);
+      const char* vt = VT(cur);
+      f32x4 sc[QG][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) sc[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 kf = frag_rows<DH>(kt, 16 * t, ks, lane);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) sc[qg][t] = mfma(kf, qf[qg][ks], sc[qg][t]);
+        }
+      }
+      const bool diag = (kb * BKV + BKV - 1 > q0w);
+      bf16x8 pp[QG][2];
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = sc[qg][t][r] * c;
+            if (diag) {
+              const int key = kb * BKV + 16 * t + 4 * g + r;
+              if (key > myq[qg]) v = -INFINITY;
+            }
+            sc[qg][t][r] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[qg], mx);
+        const float alpha = exp2f(m[qg] - mn);
+        m[qg] = mn;
+        float ps = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = exp2f(sc[qg][t][r] - mn);
+            sc[qg][t][r] = pv;
+            ps += pv;
+          }
+        l[qg] = l[qg] * alpha + ps;
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[qg][d][r] *= alpha;
+        pp[qg][0] = pack_pair(sc[qg][0], sc[qg][1]);
+        pp[qg][1] = pack_pair(sc[qg][2], sc[qg][3]);
+      }
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        const bf16x8 v0 = frag_cols<DH>(vt, 0, 16 * d, lane);
+        const bf16x8 v1 = frag_cols<DH>(vt, 32, 16 * d, lane);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) {
+          o[qg][d] = mfma(v0, pp[qg][0], o[qg][d]);
+          o[qg][d] = mfma(v1, pp[qg][1], o[qg][d]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef KT
+#undef VT
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    float lt = l[qg];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.f / lt;
+    bf16_t* orow = a.out + ((long long)b * a.T + myq[qg]) * C + h * DH;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      const uint2 v = make_uint2(pack_bf2(o[qg][d][0] * inv, o[qg][d][1] * inv),
+                                 pack_bf2(o[qg][d][2] * inv, o[qg][d][3] * inv));
+      *(uint2*)(orow + 16 * d + 4 * g) = v;
+    }
+    if (g == 0) a.lse[(long long)bh * a.T + myq[qg]] = (m[qg] + log2f(lt)) / LOG2E;
+  }
 }
 
 // ------------------------------------------------------------------------------ delta
@@ -435,9 +578,19 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.lse = lse;
   a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
-  dim3 grid(T / 64, B * H), block(256);
-  if (Dh == 64) hipLaunchKernelGGL(fa::fwd_kernel<64>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(fa::fwd_kernel<128>, grid, block, 0, st, a);
+  // measured (benchmarks/attn_bench.py): 32 rows/wave wins at Dh = 128 (Llama: 101 vs 108 us,
+  // 365 vs 401 us), 16 rows/wave at Dh = 64 (GPT-2: 100 vs 109 us); RTDC_FA_FWD=1|2 forces one
+  static const int forced = getenv("RTDC_FA_FWD") ? atoi(getenv("RTDC_FA_FWD")) : 0;
+  const int variant = forced ? forced : (Dh == 128 ? 2 : 1);
+  if (variant == 2 && T % 128 == 0) {  // 32 rows per wave
+    dim3 grid(T / 128, B * H), block(256);
+    if (Dh == 64) hipLaunchKernelGGL(fa::fwd2_kernel<64>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(fa::fwd2_kernel<128>, grid, block, 0, st, a);
+  } else {
+    dim3 grid(T / 64, B * H), block(256);
+    if (Dh == 64) hipLaunchKernelGGL(fa::fwd_kernel<64>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(fa::fwd_kernel<128>, grid, block, 0, st, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
