@@ -300,15 +300,29 @@ static int pick_cfg(const GemmArgs& a, int batch, bool a_kmajor, bool b_kmajor) 
 
 extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 
-// split-K when the output tiles cannot fill the chip and K is long (weight gradients): aim at
-// ~2 blocks per CU, >= 8 k-tiles per slice, slabs within the workspace.
-static int pick_splitk(const GemmArgs& a, long long tiles, int target_blocks = 512) {
+// Split-K for long-K / few-tile products (weight gradients): choose the slice count s that
+// minimises a wave-quantised time model
+//     T(s) = ceil(tiles*s / slots) * ceil(ktiles / s) * t_ktile  +  s * M*N * 8 B / HBM
+// (slots = concurrent blocks on 256 CUs, t_ktile = one block's time per 64-deep k-tile, the
+// second term the fp32 slab write + reduce read).  Grid sizes just past a multiple of the
+// slots cost a whole extra wave (e.g. 27 tiles x 19 slices = 513 blocks = 3 waves of 1-block-
+// per-CU work), so the quantisation term matters more than "about 2 blocks per CU".
+static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, double t_ktile_us = 1.8) {
   const int ktiles = a.K / gemm::BK;
   if (!a.ws || tiles >= 200 || ktiles < 32) return 1;
-  int s = (int)((target_blocks + tiles - 1) / tiles);
-  s = s > 128 ? 128 : s;
-  while (s > 1 && (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems)) --s;
-  return s;
+  const double slab_us = (double)a.M * a.N * 8.0 / 4.0e6;  // bytes / (4 TB/s) in us
+  int best = 1;
+  double best_t = 1e30;
+  for (int s = 1; s <= 128; ++s) {
+    if (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems) break;
+    const long long waves = (tiles * s + slots - 1) / slots;
+    const double t = (double)waves * (double)((ktiles + s - 1) / s) * t_ktile_us + (s > 1 ? s * slab_us : 0.0);
+    if (t < best_t - 1e-9) {
+      best_t = t;
+      best = s;
+    }
+  }
+  return best;
 }
 
 extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
@@ -326,8 +340,8 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     if (batch != 1 || a.causal != 0) return 1;
     tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
   }
-  // the 8-phase kernel runs one 512-thread block per CU: ~one block per CU of slices
-  if (plain) a.splitk = pick_splitk(a, tiles);
+  // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
+  if (plain) a.splitk = cfg == 6 ? pick_splitk(a, tiles, 256, 1.8) : pick_splitk(a, tiles);
   if (cfg == 6) {
     const int rc = rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
     if (rc) return rc;
