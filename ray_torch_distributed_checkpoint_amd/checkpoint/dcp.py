@@ -151,6 +151,9 @@ class AsyncSave:
             self._h = None
         if self.write_s is None:
             self.write_s = time.perf_counter() - self.t_start
+        if getattr(self, "_verify", None):
+            _verify_written(self._verify)
+            self._verify = None
         return self.write_s
 
     def _finish(self):
@@ -168,6 +171,19 @@ class AsyncSave:
         if w > 1:
             dist.barrier(group=self.pg)
         return self
+
+
+def _verify_written(entries) -> None:
+    """RTDC_CKPT_VERIFY=1 debug mode: read every tensor record this rank wrote
+    back from disk and compare it byte for byte with the snapshot that was staged."""
+    for path, base, size, t in entries:
+        off, n = _zip_data_record(path, base, size)
+        with open(path, "rb") as f:
+            f.seek(off)
+            disk = f.read(n)
+        host = t.detach().contiguous().cpu().reshape(-1).view(torch.uint8).numpy().tobytes()
+        if disk != host:
+            raise IOError(f"checkpoint verify failed: {path}@{off} ({n} bytes) differs from the staged tensor")
 
 
 def write_metadata(checkpoint_id: str, md: Metadata):
@@ -247,12 +263,18 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
         pass
     handle = None
     nbytes = sum(it.nbytes for it in mine)
+    verify = []
     if mine:
         arcs = _archives_for(mine, with_ptrs=True)
         path = os.path.join(checkpoint_id, f"__{rank}_0.distcp")
         handle = torchsave.submit_files([(path, fsync, crc, arcs)], [it.tensor for it in mine if it.tensor is not None],
                                         nbytes, ready)
-    return AsyncSave(checkpoint_id, handle, metadata, rank, t0, time.perf_counter() - t0, nbytes, process_group)
+        if os.environ.get("RTDC_CKPT_VERIFY", "0") == "1":
+            _, lay = ext.plan_layout(_archives_for(mine, with_ptrs=False))
+            verify = [(path, base, size, it.tensor) for it, (base, size, _r) in zip(mine, lay) if it.kind == "tensor"]
+    h = AsyncSave(checkpoint_id, handle, metadata, rank, t0, time.perf_counter() - t0, nbytes, process_group)
+    h._verify = verify
+    return h
 
 
 def save(state_dict: dict, checkpoint_id: str, process_group=None, **kw) -> AsyncSave:

@@ -113,10 +113,30 @@ class DistributedDataParallel(nn.Module):
         self._hooks = []
         self._pidx = {id(p): i for i, p in enumerate(self.space.params)}
         self._engine = None
+        self._check = os.environ.get("RTDC_COLLECTIVE_CHECK", "0") == "1"
+        self._steps = 0
         if self.world_size > 1:
+            self._verify_plan_across_ranks()
             self._engine = self._native_engine(process_group)
             for p in self.space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+
+    def _agree(self, value: int, what: str) -> None:
+        """All ranks must hold the same integer (MIN == MAX all-reduce); raise otherwise."""
+        t = torch.tensor([value, -value], dtype=torch.int64, device=self.space.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.process_group)
+        if int(t[0].item()) != -int(t[1].item()):
+            raise RuntimeError(f"DDP {what} differs across ranks (rank {dist.get_rank(self.process_group)} has "
+                               f"{value}): collectives would deadlock or mix unrelated buffers")
+
+    def _verify_plan_across_ranks(self) -> None:
+        """Parameter shapes + bucket plan fingerprint identical on every rank (the role of torch
+        DDP's _verify_param_shape_across_processes)."""
+        import zlib
+
+        desc = ";".join(f"{tuple(s.shape)}@{s.offset}" for s in self.space.segments)
+        desc += "|" + ",".join(f"{b.start}-{b.end}" for b in self.buckets)
+        self._agree(zlib.crc32(desc.encode()) & 0x7FFFFFFF, "parameter/bucket plan")
 
     def _native_engine(self, process_group):
         """C++ bucket engine (csrc/runtime/reducer.cpp); RTDC_DDP_ENGINE=python keeps the
@@ -205,8 +225,11 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._callback_queued = False
+        self._steps += 1
         if self._engine is not None:
             self._engine.finalize()
+            if self._check:  # RTDC_COLLECTIVE_CHECK=1: desync detector (one tiny all-reduce per step)
+                self._agree(self._steps * 1000003 + self._engine.launched() + len(self.buckets), "step sequence")
             return
         # params that produced no gradient this step: zero-filled grads, still reduced
         while self._next < len(self.buckets):
