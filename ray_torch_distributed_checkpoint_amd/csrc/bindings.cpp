@@ -67,7 +67,8 @@ int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho,
                 int pad, int K, int Kp, hipStream_t st);
 int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, long long N, int C, float eps, float momentum, int training,
-                int relu, float* ws, int nblk, hipStream_t st);
+                int relu, float* ws, int nblk, const float* pmean, const float* pm2, int p_nblk, int p_R,
+                hipStream_t st);
 int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
                 void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu, float* ws, int nblk,
                 hipStream_t st);
@@ -317,8 +318,11 @@ static void swiglu_bwd(Tensor gu, Tensor dh, Tensor dgu) {
 //   mode 1: C[npix, N] bf16 = im2col(X) . other[N, K]^T          (other K-major, ld = ld_other)
 //   mode 2: C[M, N]    fp32 = other[K, M]^T . im2col(X)           (other = dY, MN-major, ld = ld_other)
 // X is NHWC [B, H, W, Cx]; the window is KH x KW (K = KH*KW*Cx in mode 1, N in mode 2).
-static void conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K, int64_t ld_other,
-                      int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad, c10::optional<Tensor> ws) {
+// stats_mean/stats_m2 (mode 1, optional): fused BatchNorm statistics per output row tile,
+// [ceil(M/128)][N] fp32; returns the rows per statistics tile (128 or 256).
+static int64_t conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K,
+                         int64_t ld_other, int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad,
+                         c10::optional<Tensor> ws, c10::optional<Tensor> stats_mean, c10::optional<Tensor> stats_m2) {
   check_dev(X, "X");
   check_dev(other, "other");
   TORCH_CHECK(X.is_contiguous() && X.dim() == 4 && X.scalar_type() == at::kBFloat16, "conv_gemm: X must be NHWC bf16");
@@ -349,7 +353,16 @@ static void conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M,
   a.cv_H = (int)X.size(1); a.cv_W = (int)X.size(2); a.cv_C = (int)X.size(3);
   a.cv_Ho = (int)Ho; a.cv_Wo = (int)Wo; a.cv_KW = (int)KW; a.cv_stride = (int)stride; a.cv_pad = (int)pad;
   a.cv_npix = (int)npix;
+  const int64_t bm = N <= 64 ? 256 : 128;
+  if (stats_mean.has_value()) {
+    TORCH_CHECK(mode == 1 && stats_m2.has_value(), "conv_gemm: statistics need mode 1 and both buffers");
+    TORCH_CHECK(stats_mean->numel() >= ((M + bm - 1) / bm) * N && stats_m2->numel() >= ((M + bm - 1) / bm) * N,
+                "conv_gemm: statistics buffers too small");
+    a.stats_mean = stats_mean->data_ptr<float>();
+    a.stats_m2 = stats_m2->data_ptr<float>();
+  }
   check_rc(rtdc_conv_gemm(&a, (int)mode, cur_stream()), "conv_gemm");
+  return bm;
 }
 
 // x: NHWC bf16 [B,H,W,C]; cols: [B*Ho*Wo, Kp] with K = KH*KW*C real columns (rest zero).
@@ -372,7 +385,8 @@ static void col2im(Tensor dcols, Tensor dx, int64_t Ho, int64_t Wo, int64_t KH, 
 }
 static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta,
                    c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var, double eps, double momentum,
-                   bool training, bool relu, Tensor ws, int64_t nblk) {
+                   bool training, bool relu, Tensor ws, int64_t nblk, c10::optional<Tensor> pmean,
+                   c10::optional<Tensor> pm2, int64_t p_R) {
   const int64_t C = x.size(-1), N = x.numel() / C;
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "bn_fwd: contiguous tensors expected");
   TORCH_CHECK(!training || ws.numel() >= 2 * nblk * C, "bn_fwd: workspace too small");
@@ -380,7 +394,10 @@ static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, T
                        gamma.data_ptr<float>(), beta.data_ptr<float>(),
                        running_mean.has_value() ? running_mean->data_ptr<float>() : nullptr,
                        running_var.has_value() ? running_var->data_ptr<float>() : nullptr, N, (int)C, (float)eps,
-                       (float)momentum, training, relu, ws.data_ptr<float>(), (int)nblk, cur_stream()),
+                       (float)momentum, training, relu, ws.data_ptr<float>(), (int)nblk,
+                       pmean.has_value() ? pmean->data_ptr<float>() : nullptr,
+                       pm2.has_value() ? pm2->data_ptr<float>() : nullptr,
+                       pmean.has_value() ? (int)pmean->size(0) : 0, (int)p_R, cur_stream()),
            "bn_fwd");
 }
 static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor dx,

@@ -31,6 +31,10 @@ struct GemmArgs {
   // X [B][cv_H][cv_W][cv_C] through a KHxKW window (stride, pad) over a cv_Ho x cv_Wo grid of
   // cv_npix output pixels.  Mode 1: A(m = pixel, k = tap*C + c), mode 2: B(k = pixel, n = tap*C + c).
   int cv_H, cv_W, cv_C, cv_Ho, cv_Wo, cv_KW, cv_stride, cv_pad, cv_npix;
+  // optional fused BatchNorm statistics of the (bf16-rounded) output, mode 1 only:
+  // per row-tile t and column n: mean and M2 over the tile's rows -> [tiles_m][N] each
+  float* stats_mean;
+  float* stats_m2;
 };
 
 // fp32 MFMA GEMM (gemm_f32.hip)

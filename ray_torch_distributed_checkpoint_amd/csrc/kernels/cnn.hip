@@ -490,11 +490,17 @@ extern "C" int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// pmean/pm2 (optional): per-row-block statistics already computed by the producer (the
+// convolution GEMM epilogue, blocks of pR rows): the statistics pass over x is skipped.
 extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma,
                            const float* beta, float* running_mean, float* running_var, long long N, int C, float eps,
-                           float momentum, int training, int relu, float* ws, int nblk, hipStream_t st) {
+                           float momentum, int training, int relu, float* ws, int nblk, const float* pmean,
+                           const float* pm2, int p_nblk, int p_R, hipStream_t st) {
   if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
-  if (training) {
+  if (training && pmean) {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(64), 0, st, pmean, pm2, p_nblk, N, p_R, C, eps, momentum, mean,
+                       rstd, running_mean, running_var);
+  } else if (training) {
     const int R = (int)((N + nblk - 1) / nblk);
     hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)nullptr,
                        (const bf16_t*)nullptr, (const float*)nullptr, (const float*)nullptr, N, C, R, 0, ws,

@@ -36,6 +36,73 @@
 namespace rtdc {
 
 
+// Per-column (mean, M2) of this block's output tile - the BatchNorm statistics of a
+// convolution output computed in the GEMM epilogue instead of by a separate pass over the
+// activation (values rounded to bf16 exactly as stored).  Each lane sums v and v^2 over its
+// TM rows, an xor-shuffle tree sums the 16 lanes that share a column, the WM waves that
+// share a column are added in LDS in fixed order, and the tile's (mean, M2) = (S/n,
+// Q - S^2/n) (a 128/256-row tile keeps the one-pass cancellation small; tiles are then
+// merged with Chan's formula by the BatchNorm finalize kernel).  Deterministic.
+template <class CFG>
+__device__ __forceinline__ void conv_tile_stats(const GemmArgs& a, const f32x4 (&acc)[CFG::TM][CFG::TN], float alpha,
+                                                int m0, int n0, int wm, int wn, int lane, char* smem) {
+  constexpr int TM = CFG::TM, TN = CFG::TN, WM = CFG::WM, BN = CFG::BN, BM = CFG::BM;
+  float* sh = (float*)smem;  // [WM][BN][2]
+  __syncthreads();          // staging buffers are free (the k-loop ended with a barrier)
+  float s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = bf2f(f2bf(acc[i][j][r] * alpha));
+        s1[j][r] += v;
+        s2[j][r] += v * v;
+      }
+  }
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] += __shfl_xor(s1[j][r], off, 64);
+        s2[j][r] += __shfl_xor(s2[j][r], off, 64);
+      }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * (TN * 16) + j * 16 + 4 * (lane >> 4) + r;
+        sh[(wm * BN + col) * 2] = s1[j][r];
+        sh[(wm * BN + col) * 2 + 1] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  const int tile = m0 / BM;
+  const float n = (float)min(BM, a.M - m0);
+  for (int col = threadIdx.x; col < BN; col += CFG::NT) {
+    const int nn = n0 + col;
+    if (nn >= a.N) continue;
+    float S = 0.f, Q = 0.f;
+    for (int w = 0; w < WM; ++w) {
+      S += sh[(w * BN + col) * 2];
+      Q += sh[(w * BN + col) * 2 + 1];
+    }
+    const float mean = S / n;
+    a.stats_mean[(long long)tile * a.N + nn] = mean;
+    a.stats_m2[(long long)tile * a.N + nn] = fmaxf(Q - S * mean, 0.f);
+  }
+}
+
 template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0>
 __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
   using namespace gemm;
@@ -91,11 +158,12 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  using SA = std::conditional_t<GM == 1, ConvStagerK<BM, NW>, Stager<AK, BM, NW>>;
+  // GM 1: gathered A (implicit-GEMM convolution); 3: the same plus fused BatchNorm statistics
+  using SA = std::conditional_t<GM == 1 || GM == 3, ConvStagerK<BM, NW>, Stager<AK, BM, NW>>;
   using SB = std::conditional_t<GM == 2, ConvStagerMN<BN, NW>, Stager<BKM, BN, NW>>;
   SA sa;
   SB sb;
-  if constexpr (GM == 1) sa.init(a, A, a.M, m0, wave, lane);
+  if constexpr (GM == 1 || GM == 3) sa.init(a, A, a.M, m0, wave, lane);
   else sa.init(A, a.lda, a.M, m0, wave, lane);
   if constexpr (GM == 2) sb.init(a, B, a.N, n0, wave, lane);
   else sb.init(B, a.ldb, a.N, n0, wave, lane);
@@ -209,6 +277,7 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
       store4<OutT>(C + off, v);
     }
   }
+  if constexpr (GM == 3) conv_tile_stats<CFG>(a, acc, alpha, m0, n0, wm, wn, lane, smem);
 }
 
 // out[m][n] = sum_s ws[s][m][n] (+ beta * Cin[m][n]); fixed slice order.
@@ -382,10 +451,16 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
   a.splitk = 1;
   if (mode == 1) {
     if (a.M != a.cv_npix) return 1;
-    if (a.N <= 64) launch_cfg<Cfg256x64, true, true, bf16_t, 1>(a, 1, stream);
-    else launch_cfg<Cfg128x128, true, true, bf16_t, 1>(a, 1, stream);
+    // stats rows are per BM-row tile: 256 (256x64 tiles) or 128
+    if (a.stats_mean) {
+      if (a.N <= 64) launch_cfg<Cfg256x64, true, true, bf16_t, 3>(a, 1, stream);
+      else launch_cfg<Cfg128x128, true, true, bf16_t, 3>(a, 1, stream);
+    } else {
+      if (a.N <= 64) launch_cfg<Cfg256x64, true, true, bf16_t, 1>(a, 1, stream);
+      else launch_cfg<Cfg128x128, true, true, bf16_t, 1>(a, 1, stream);
+    }
   } else if (mode == 2) {
-    if (a.K < a.cv_npix) return 1;
+    if (a.K < a.cv_npix || a.stats_mean) return 1;
     const bool narrow = a.M <= 64;
     a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a));
     if (narrow) launch_cfg<Cfg64x256, false, false, float, 2>(a, 1, stream);

@@ -55,7 +55,9 @@ class Conv2d(nn.Module):
         nn.init.kaiming_normal_(self.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x):
-        return cnn.conv2d(x, self.weight, self.stride, self.pad)
+        # every convolution of the network feeds a BatchNorm: its statistics come out of the
+        # GEMM epilogue (training mode), the BN then skips its own pass over the activation
+        return cnn.conv2d(x, self.weight, self.stride, self.pad, bn_stats=self.training)
 
     def extra_repr(self):
         o, i, k, _ = self.weight.shape

@@ -63,7 +63,7 @@ def _implicit_ok(C: int, M: int) -> bool:
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad):
+    def forward(ctx, x, w, stride, pad, bn_stats=False):
         B, H, W, C = x.shape
         Cout, Cin, KH, KW = w.shape
         assert Cin == C, (x.shape, w.shape)
@@ -75,11 +75,20 @@ class _Conv2d(torch.autograd.Function):
             # implicit GEMM: the MFMA kernel gathers im2col(x) tiles straight from NHWC x
             wm = _weight_matrix(w, K)
             y = torch.empty((M, Cout), dtype=torch.bfloat16, device=x.device)
-            gpu_ext().conv_gemm(x, wm, y, 1, M, Cout, K, K, Ho, Wo, KW, stride, pad, None)
+            smean = sm2 = None
+            if bn_stats:  # BatchNorm statistics fused into the GEMM epilogue (per 128/256-row tile)
+                nt = (M + 127) // 128
+                smean = torch.empty((nt, Cout), dtype=torch.float32, device=x.device)
+                sm2 = torch.empty((nt, Cout), dtype=torch.float32, device=x.device)
+            bm = gpu_ext().conv_gemm(x, wm, y, 1, M, Cout, K, K, Ho, Wo, KW, stride, pad, None, smean, sm2)
             ctx.save_for_backward(x, wm)
             ctx.w = w
             ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, K, M, M, "implicit")
-            return y.view(B, Ho, Wo, Cout)
+            out = y.view(B, Ho, Wo, Cout)
+            if bn_stats:
+                ntiles = (M + bm - 1) // bm
+                ctx.stats = (smean[:ntiles], sm2[:ntiles], bm)
+            return out
         Kp = _ceil(K, 64)
         Mp = _ceil(M, 64)
         direct = KH == 1 and KW == 1 and stride == 1 and pad == 0 and K == Kp and M == Mp
@@ -111,7 +120,7 @@ class _Conv2d(torch.autograd.Function):
             if ctx.needs_input_grad[1]:
                 dwm = torch.empty((Cout, K), dtype=torch.float32, device=dy.device)
                 ws = G.workspace(dy.device, G.SPLITK_WS_ELEMS, "splitk")
-                gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws)
+                gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws, None, None)
                 dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2)
                 tw = grad_target(ctx.w)
                 dw = tw.copy_(dw) if tw is not None else dw.contiguous()
@@ -123,12 +132,12 @@ class _Conv2d(torch.autograd.Function):
                     dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                     Kt = KH * KW * Cout
                     gpu_ext().conv_gemm(dy, s, dx.view(B * H * W, C), 1, B * H * W, C, Kt, Kt, H, W, KW, 1,
-                                        KH - 1 - pad, None)
+                                        KH - 1 - pad, None, None, None)
                 else:
                     dcols = G.linear_dgrad(dy2, wm)  # [Mp, K]
                     dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                     gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
-            return dx, dw, None, None
+            return dx, dw, None, None, None
         cols = saved
         if ctx.needs_input_grad[1]:
             dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
@@ -142,7 +151,7 @@ class _Conv2d(torch.autograd.Function):
             else:
                 dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                 gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def shadow_of_w(ctx, wm, Cout, C, KH, KW):
@@ -156,11 +165,17 @@ def conv2d_ref(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) 
     return y.permute(0, 2, 3, 1).contiguous()
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
-    """NHWC convolution (no bias): x [B, H, W, Cin] -> [B, Ho, Wo, Cout]; w [Cout, Cin, KH, KW]."""
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, bn_stats: bool = False) -> torch.Tensor:
+    """NHWC convolution (no bias): x [B, H, W, Cin] -> [B, Ho, Wo, Cout]; w [Cout, Cin, KH, KW].
+    bn_stats=True also computes the per-channel BatchNorm statistics of the output inside the
+    GEMM epilogue; `batch_norm` on exactly this tensor then skips its statistics pass."""
     if not x.is_cuda or x.dtype != torch.bfloat16:
         return conv2d_ref(x, w, stride, pad)
-    return _Conv2d.apply(x, w, stride, pad)
+    y = _Conv2d.apply(x, w, stride, pad, bn_stats)
+    st = getattr(y.grad_fn, "stats", None) if y.grad_fn is not None else None
+    if st is not None:
+        y._rtdc_bn_stats = st  # (mean [tiles, C], M2 [tiles, C], rows per tile)
+    return y
 
 
 def _bn_blocks(N: int, C: int) -> int:
@@ -175,18 +190,24 @@ class _BatchNorm(torch.autograd.Function):
         x = x.contiguous()
         N = x.numel() // C
         y = torch.empty_like(x)
+        pmean = pm2 = None
+        p_rows = 0
         if training:
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             rstd = torch.empty(C, dtype=torch.float32, device=x.device)
             nblk = _bn_blocks(N, C)
             ws = G.workspace(x.device, 2 * nblk * C, "bn")
+            st = getattr(x, "_rtdc_bn_stats", None)
+            if st is not None and st[0].shape[1] == C and st[0].shape[0] == (N + st[2] - 1) // st[2]:
+                pmean, pm2, p_rows = st
         else:
             mean = running_mean.float()
             rstd = torch.rsqrt(running_var.float() + eps)
             nblk, ws = 1, G.workspace(x.device, 2 * C, "bn")
         res = residual.contiguous() if residual is not None else None
         gpu_ext().bn_fwd(x, res, y, mean, rstd, weight, bias, running_mean if training else None,
-                         running_var if training else None, eps, momentum, training, relu, ws, nblk)
+                         running_var if training else None, eps, momentum, training, relu, ws, nblk, pmean, pm2,
+                         p_rows)
         ctx.save_for_backward(x, y if relu else None, mean, rstd, weight)
         ctx.params = (weight, bias)
         ctx.relu = relu

@@ -163,7 +163,7 @@ def _bf16_emulated_grads(model, x, t):
     from ray_torch_distributed_checkpoint_amd.ops import cnn
 
     oc, ob = cnn.conv2d, cnn.batch_norm
-    R.cnn.conv2d = lambda x_, w, s=1, p=0: oc(x_, w.bfloat16().float(), s, p).bfloat16().float()
+    R.cnn.conv2d = lambda x_, w, s=1, p=0, bn_stats=False: oc(x_, w.bfloat16().float(), s, p).bfloat16().float()
     R.cnn.batch_norm = lambda *a, **k: ob(*a, **k).bfloat16().float()
     try:
         F.cross_entropy(model(x), t).backward()
@@ -206,3 +206,23 @@ def test_resnet18_matches_reference_and_trains():
         opt.step()
         losses.append(l.item())
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+@pytest.mark.parametrize("B,H,C,Cout,s", [(4, 28, 64, 64, 1), (2, 14, 128, 256, 2), (2, 13, 64, 128, 1)])
+def test_conv_fused_bn_statistics(B, H, C, Cout, s):
+    """BatchNorm statistics computed in the implicit-GEMM epilogue == the separate pass."""
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(B + H + Cout)
+    x = (torch.randn(B, H, H, C, device=DEV) + 0.7).to(torch.bfloat16)
+    w = torch.randn(Cout, C, 3, 3, device=DEV) * 0.1
+    y = cnn.conv2d(x, w.requires_grad_(True), s, 1, bn_stats=True)
+    assert getattr(y, "_rtdc_bn_stats", None) is not None
+    g, b = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
+    rm1, rv1 = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    out_fused = cnn.batch_norm(y, g, b, rm1, rv1, True, relu=True)
+    out_ref = cnn.batch_norm(y.detach().clone(), g, b, rm2, rv2, True, relu=True)
+    _close(out_fused, out_ref, 0.01, "y")
+    _close(rm1, rm2, 1e-4, "running_mean")
+    _close(rv1, rv2, 1e-4, "running_var")
