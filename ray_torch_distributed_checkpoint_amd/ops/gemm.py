@@ -15,8 +15,8 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
 CAUSAL_NONE, CAUSAL_SKIP_UPPER, CAUSAL_K_UPTO_M, CAUSAL_K_FROM_M = 0, 1, 2, 3
 
 _COLSUM_BLOCKS = 256
-SPLITK_MAX_OUT = 200 * 128 * 128  # outputs that fill < 200 tiles of 128x128
-SPLITK_WS_ELEMS = 48 << 20       # 192 MiB fp32 slab workspace cap
+SPLITK_MAX_OUT = 200 * 256 * 256  # outputs that fill < 200 tiles of 256x256 (e.g. Llama-8B at 2k tokens/GPU)
+SPLITK_WS_ELEMS = 64 << 20        # 256 MiB fp32 slab workspace cap
 _ws_cache: dict = {}
 
 
