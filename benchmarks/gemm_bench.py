@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--sweep", action="store_true", help="also time forced tile configurations (all layouts)")
-    ap.add_argument("--cfgs", default="0,3,6", help="tile configurations for --sweep")
+    ap.add_argument("--cfgs", default="0,6,7", help="tile configurations for --sweep")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []

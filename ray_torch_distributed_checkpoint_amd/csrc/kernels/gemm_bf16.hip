@@ -351,23 +351,37 @@ static int pick_cfg(const GemmArgs& a, int batch, bool a_kmajor, bool b_kmajor) 
     // 64-wide outputs (Cout = 64 convolutions): a 128x128 tile would idle half its MFMAs
     if (a.N <= 64 && a.M >= 256) return 4;
     if (a.M <= 64 && a.N >= 128) return 5;
-    if (a.M >= 256 && a.N >= 256) {
+    if (a.M >= 256 && a.N >= 192) {
+      // 8-wave counted-vmcnt kernel, 256x256 (cfg 6) or 256x192 (cfg 7) tiles: the 192-wide
+      // tile when it quantises onto the 256 CUs clearly better (N = 768: 256 vs 192 tiles)
+      auto eff_of = [](long long t) { return (double)t / (double)(((t + 255) / 256) * 256); };
       const long long t6 = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
-      const long long waves = (t6 + 255) / 256;
-      const double eff = (double)t6 / (double)(waves * 256);
+      const long long t7 = (long long)((a.M + 255) / 256) * ((a.N + 191) / 192);
+      // measured (profiles/gemm_bench_v4_256x192.jsonl): the 192-wide tile wins for forward
+      // products with one wave of tiles or long K (mlp_proj 1132 vs 983 TF, attn_proj 700 vs
+      // 654), for short-K dgrads (+2..4 %); it loses on long-K dgrad (LM head 943 vs 1059)
+      // and qkv forward (737 vs 778 for 128x128), where per-tile efficiency outweighs the
+      // better wave quantisation
+      const bool better7 = eff_of(t7) > eff_of(t6) + 0.05;
+      const bool use7 = better7 && ((a_kmajor && b_kmajor && (t7 <= 256 || a.K >= 2048)) ||
+                                    (a_kmajor && !b_kmajor && a.K <= 4096));
+      const long long t = use7 ? t7 : t6;
+      const double eff = use7 ? eff_of(t7) : eff_of(t6);
+      const int big = use7 ? 7 : 6;
       if (a_kmajor && b_kmajor) {
-        if (t6 >= 1024 || eff >= 0.95 || a.K >= 2048) return 6;
+        if (t >= 1024 || eff >= 0.95 || a.K >= 2048) return big;
       } else if (a_kmajor) {
-        if (t6 >= 128) return 6;
+        if (t >= 128) return big;
       } else {
-        if (t6 >= 24) return 6;
+        if (t >= 24) return big;
       }
     }
   }
   return 0;
 }
 
-extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
+extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
+                                 hipStream_t st);
 
 // Split-K for long-K / few-tile products (weight gradients): choose the slice count s that
 // minimises a wave-quantised time model
@@ -405,14 +419,14 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
                   : cfg == 2 ? ntiles<Cfg128x256>(a) : cfg == 4 ? ntiles<Cfg256x64>(a)
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
-  if (cfg == 6) {  // 256x256 8-wave counted-vmcnt pipeline (gemm_8ph.hip)
+  if (cfg == 6 || cfg == 7) {  // 256x256 / 256x192 8-wave counted-vmcnt pipeline (gemm_8ph.hip)
     if (batch != 1 || a.causal != 0) return 1;
-    tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+    tiles = (long long)((a.M + 255) / 256) * ((a.N + (cfg == 7 ? 191 : 255)) / (cfg == 7 ? 192 : 256));
   }
   // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
-  if (plain) a.splitk = cfg == 6 ? pick_splitk(a, tiles, 256, 1.8) : pick_splitk(a, tiles);
-  if (cfg == 6) {
-    const int rc = rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
+  if (plain) a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : 1.8) : pick_splitk(a, tiles);
+  if (cfg == 6 || cfg == 7) {
+    const int rc = rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, cfg == 7 ? 192 : 256, stream);
     if (rc) return rc;
   } else if (out_fp32) {
     if (a_kmajor && b_kmajor) launch_layout<true, true, float>(a, cfg, batch, stream);

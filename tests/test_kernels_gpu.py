@@ -365,7 +365,7 @@ def test_ckpt_engine_writes_torch_loadable(tmp_path):
         assert torch.equal(got[k], sd[k].cpu())
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)])
 def test_gemm_tile_configs(cfg, a_k, b_k):
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
