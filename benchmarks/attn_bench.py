@@ -35,9 +35,12 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default=None)
     args = ap.parse_args()
     torch.manual_seed(0)
     for name, B, T, H, Hkv, Dh in SHAPES:
+        if args.only and name != args.only:
+            continue
         W = (H + 2 * Hkv) * Dh
         qkv = (torch.randn(B, T, W, device="cuda") * 0.5).bfloat16().requires_grad_(True)
         flops_f = 2 * 2 * B * H * T * T * Dh / 2  # causal
