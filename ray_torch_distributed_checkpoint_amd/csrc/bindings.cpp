@@ -49,7 +49,7 @@ int rtdc_softmax_bwd(const void* P, const void* dP, void* dS, long long rows, in
 int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int ntok, int T, int D,
                    hipStream_t st);
 int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe, int B, int T,
-                   int D, int accumulate_wpe, hipStream_t st);
+                   int D, int accumulate_wpe, int accumulate_wte, hipStream_t st);
 int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
                  unsigned long long offset, const long long* off_dev, int is_bf16, hipStream_t st);
 int rtdc_relu_dropout(const void* h, void* y, const void* dy, void* dx, long long n, float p,
@@ -255,11 +255,11 @@ static void embed_fwd(Tensor idx, Tensor wte, c10::optional<Tensor> wpe, Tensor 
 }
 // sidx / perm: stably sorted token ids and their original positions (deterministic backward)
 static void embed_bwd(Tensor sidx, Tensor perm, Tensor dout, Tensor dwte, c10::optional<Tensor> dwpe, int64_t B,
-                      int64_t T, bool accumulate_wpe) {
+                      int64_t T, bool accumulate_wpe, bool accumulate_wte) {
   const int D = (int)dwte.size(1);
   TORCH_CHECK(sidx.is_contiguous() && perm.is_contiguous() && sidx.numel() == B * T, "embed_bwd: bad sort arrays");
   check_rc(rtdc_embed_bwd(sidx.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
-                          (float*)ptr_or_null(dwpe), (int)B, (int)T, D, accumulate_wpe, cur_stream()),
+                          (float*)ptr_or_null(dwpe), (int)B, (int)T, D, accumulate_wpe, accumulate_wte, cur_stream()),
            "embed_bwd");
 }
 static void dropout(Tensor x, Tensor y, double p, uint64_t seed, uint64_t offset, c10::optional<Tensor> off_dev) {
@@ -514,7 +514,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
   m.def("embed_fwd", &embed_fwd);
-  m.def("embed_bwd", &embed_bwd);
+  m.def("embed_bwd", &embed_bwd, py::arg("sidx"), py::arg("perm"), py::arg("dout"), py::arg("dwte"), py::arg("dwpe"),
+        py::arg("B"), py::arg("T"), py::arg("accumulate_wpe"), py::arg("accumulate_wte") = false);
   m.def("dropout", &dropout);
   m.def("relu_dropout", &relu_dropout);
   m.def("flash_fwd", &flash_fwd);

@@ -12,7 +12,7 @@
 // columns per 16-lane group).
 //
 //   fwd     : block = 64 query rows (4 waves x 16) of one (b, h); K/V tiles of 64 keys
-//             double-buffered in LDS by global_load_lds; online softmax in the log2 domain;
+//             streamed through LDS by global_load_lds; online softmax in the log2 domain;
 //             writes O and the row log-sum-exp.
 //   bwd_dkdv: block = 64 keys (4 waves x 16) of one (b, kv-head); loops over the query
 //             blocks at or after the diagonal and over the q-heads of the GQA group; keeps
@@ -22,6 +22,20 @@
 //             bitwise reproducible (MI355X_MICROARCH.md §Global float atomics).
 //   delta   : D[b,h,t] = sum_d dO * O (the softmax-backward row term).
 // Requires T % 64 == 0 and Dh in {64, 128}.
+//
+// Pipelining (all three loops): the streamed tiles (K/V for fwd and dQ; Q, dO and the 64
+// LSE / delta values of a query block for dK/dV) go through an NS-slot LDS ring with NS-1
+// tiles in flight.  Every streamed byte arrives by global_load_lds; the operands a wave keeps
+// in registers are loaded - and waited for - before the loop, so no ordinary load sits
+// between a DMA and its wait (hipcc waits vmcnt(0) at the first use of an ordinary load while
+// a DMA is in flight: cdna_hip_programming.md §5 "Pipelining across barriers").  A step ends
+// with a counted `s_waitcnt vmcnt(n)` that retires exactly the next tile (n = the DMA
+// instructions of the tiles issued after it) and a raw s_barrier (a __syncthreads() would
+// drain the DMA queue).  The tile of step j+NS-1 is issued at the top of step j into the slot
+// that step j-1 read, which every wave has left: its reads completed (lgkmcnt(0)) before the
+// barrier that closed step j-1.  All LDS is one __shared__ array.
+// NS (ring slots) is chosen at launch (fa_ns below): LDS per block grows with NS and sets how
+// many blocks share a CU, so deeper rings trade occupancy for DMA depth.
 #include "common.h"
 
 #include <cstdlib>
@@ -53,6 +67,7 @@ __device__ __forceinline__ int toff(int row, int chunk) {
 
 // global -> LDS copy of rows [r0, r0+64) (row stride ld elements, column offset col0) by all
 // 4 waves: 1 KiB global_load_lds pieces, swizzle applied on the source address.
+// DH/32 DMA instructions per wave.
 template <int DH>
 __device__ __forceinline__ void stage(const bf16_t* base, long long ld, int r0, int col0, char* tile, int wave,
                                       int lane) {
@@ -77,25 +92,47 @@ __device__ __forceinline__ bf16x8 frag_rows(const char* tile, int R0, int ks, in
 }
 
 // MFMA operand with rows = tile columns [d0, d0+16), k = tile rows in the accumulator order
-// kbase + 16(j>>2) + 4g + (j&3)  (two ds_read_b64_tr_b16)
+// kbase + 16(j>>2) + 4g + (j&3): two transposing reads (ds_read_b64_tr_b16), issued as asm
+// (common.h ds_tr16 protocol: lgkm_wait0() then tr_use() before the MFMA reads them)
 template <int DH>
-__device__ __forceinline__ bf16x8 frag_cols(const char* tile, int kbase, int d0, int lane) {
+__device__ __forceinline__ TrPair frag_cols_tr(const char* tile, int kbase, int d0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  bf16x4 v[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = kbase + 16 * h + 4 * g + q;
-    const int off = toff<DH>(row, (d0 >> 3) + (p >> 1)) + ((p & 1) << 3);
-    v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(tile + off));
-  }
-  bf16x8 r;
-  r[0] = v[0][0]; r[1] = v[0][1]; r[2] = v[0][2]; r[3] = v[0][3];
-  r[4] = v[1][0]; r[5] = v[1][1]; r[6] = v[1][2]; r[7] = v[1][3];
-  return r;
+  TrPair f;
+  f.lo = ds_tr16(tile + toff<DH>(kbase + 4 * g + q, (d0 >> 3) + (p >> 1)) + ((p & 1) << 3));
+  f.hi = ds_tr16(tile + toff<DH>(kbase + 16 + 4 * g + q, (d0 >> 3) + (p >> 1)) + ((p & 1) << 3));
+  return f;
 }
 
 // 16-B global load of row `row` columns [c, c+8) -> bf16x8
 __device__ __forceinline__ bf16x8 gload8(const bf16_t* p) { return *(const bf16x8*)p; }
+
+// make the compiler retire an ordinary load HERE (its own s_waitcnt before this use), not at
+// the first use inside the DMA loop
+__device__ __forceinline__ void settle(const bf16x8& x) { asm volatile("" ::"v"(__builtin_bit_cast(f32x4, x))); }
+__device__ __forceinline__ void settle(float x) { asm volatile("" ::"v"(x)); }
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n: rounded DOWN to an encoded immediate
+// (waiting for more of the in-flight DMA than needed is always safe).
+#define RTDC_FA_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+__device__ __forceinline__ void wait_vm_upto(int n) {
+  if (n >= 18) RTDC_FA_VM(18);
+  else if (n >= 16) RTDC_FA_VM(16);
+  else if (n >= 10) RTDC_FA_VM(10);
+  else if (n >= 9) RTDC_FA_VM(9);
+  else if (n >= 8) RTDC_FA_VM(8);
+  else if (n >= 5) RTDC_FA_VM(5);
+  else if (n >= 4) RTDC_FA_VM(4);
+  else RTDC_FA_VM(0);
+}
+#undef RTDC_FA_VM
+
+// close a pipeline step: this wave's LDS reads retired, then the block barrier (raw: the
+// DMA in flight stays in flight)
+__device__ __forceinline__ void step_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // two accumulator tiles (rows 16*(2s) and 16*(2s+1)) -> one bf16 B operand
 __device__ __forceinline__ bf16x8 pack_pair(const f32x4& a, const f32x4& b) {
@@ -110,10 +147,10 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 }
 
 // ------------------------------------------------------------------------------ forward
-template <int DH>
+template <int DH, int NS>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
-  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K[2], V[2]
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2, PER = DH / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE];  // K[NS], V[NS]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -127,28 +164,34 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
   const int q0w = qb * BQ + wave * 16;
   const int myq = q0w + (lane & 15);
   const float c = a.scale * LOG2E;
+  const int nkb = qb + 1;
 
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (NS + (s)) * TILE)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkb) {
+      stage<DH>(base, W, s * BKV, kcol, KT(s), wave, lane);
+      stage<DH>(base, W, s * BKV, vcol, VT(s), wave, lane);
+    }
   bf16x8 qf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) settle(qf[ks]);
+  step_barrier();
 
   f32x4 o[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
-#define KT(s) (smem + (s) * TILE)
-#define VT(s) (smem + (2 + (s)) * TILE)
-  const int nkb = qb + 1;
-  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
-  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nkb) {
-      stage<DH>(base, W, (kb + 1) * BKV, kcol, KT(cur ^ 1), wave, lane);
-      stage<DH>(base, W, (kb + 1) * BKV, vcol, VT(cur ^ 1), wave, lane);
+    const int cur = kb % NS;
+    if (kb + NS - 1 < nkb) {
+      const int nx = (kb + NS - 1) % NS;
+      stage<DH>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
+      stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
     }
     const char* kt = KT(cur);
     const char* vt = VT(cur);
@@ -195,12 +238,22 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
       for (int r = 0; r < 4; ++r) o[d][r] *= alpha;
     const bf16x8 p0 = pack_pair(s[0], s[1]), p1 = pack_pair(s[2], s[3]);
 #pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      o[d] = mfma(frag_cols<DH>(vt, 0, 16 * d, lane), p0, o[d]);
-      o[d] = mfma(frag_cols<DH>(vt, 32, 16 * d, lane), p1, o[d]);
+    for (int d0 = 0; d0 < DT; d0 += DB) {
+      TrPair vq[DB][2];
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        vq[d][0] = frag_cols_tr<DH>(vt, 0, 16 * (d0 + d), lane);
+        vq[d][1] = frag_cols_tr<DH>(vt, 32, 16 * (d0 + d), lane);
+      }
+      lgkm_wait0();
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        o[d0 + d] = mfma(tr_use(vq[d][0]), p0, o[d0 + d]);
+        o[d0 + d] = mfma(tr_use(vq[d][1]), p1, o[d0 + d]);
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (kb + 1 < nkb) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    step_barrier();
   }
 #undef KT
 #undef VT
@@ -217,13 +270,12 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
 }
 
 // Forward, 32 query rows per wave (block = 128 rows): every K fragment read from LDS feeds
-// two S MFMAs and every V fragment two P.V MFMAs, halving LDS bytes per FLOP - with 16 rows
-// per wave the loop is LDS-read bound (8 waves/CU x 16 KiB per 64-key tile vs 128 B/clk),
-// with 32 it balances against the MFMA pipe.  Same accumulator-as-operand layout as above.
-template <int DH>
+// two S MFMAs and every V fragment two P.V MFMAs, halving LDS bytes per FLOP.  Same
+// accumulator-as-operand layout and the same DMA ring as fwd_kernel.
+template <int DH, int NS>
 __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
-  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2, QG = 2, BQ2 = 128;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K[2], V[2]
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2, QG = 2, BQ2 = 128, PER = DH / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE];  // K[NS], V[NS]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -239,12 +291,26 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) myq[qg] = q0w + 16 * qg + (lane & 15);
   const float c = a.scale * LOG2E;
+  const int nkb = (qb + 1) * (BQ2 / BKV);
 
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (NS + (s)) * TILE)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkb) {
+      stage<DH>(base, W, s * BKV, kcol, KT(s), wave, lane);
+      stage<DH>(base, W, s * BKV, vcol, VT(s), wave, lane);
+    }
   bf16x8 qf[QG][KS];
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = gload8(base + (long long)myq[qg] * W + qcol + ks * 32 + g * 8);
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) settle(qf[qg][ks]);
+  step_barrier();
 
   f32x4 o[QG][DT];
   float m[QG], l[QG];
@@ -256,18 +322,12 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
     for (int d = 0; d < DT; ++d) o[qg][d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-#define KT(s) (smem + (s) * TILE)
-#define VT(s) (smem + (2 + (s)) * TILE)
-  const int nkb = (qb + 1) * (BQ2 / BKV);
-  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
-  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nkb) {
-      stage<DH>(base, W, (kb + 1) * BKV, kcol, KT(cur ^ 1), wave, lane);
-      stage<DH>(base, W, (kb + 1) * BKV, vcol, VT(cur ^ 1), wave, lane);
+    const int cur = kb % NS;
+    if (kb + NS - 1 < nkb) {
+      const int nx = (kb + NS - 1) % NS;
+      stage<DH>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
+      stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
     }
     // keys of this tile all after this wave's last row: nothing to add (barriers still run)
     if (kb * BKV <= q0w + 31) {
@@ -325,18 +385,27 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
         pp[qg][1] = pack_pair(sc[qg][2], sc[qg][3]);
       }
 #pragma unroll
-      for (int d = 0; d < DT; ++d) {
-        const bf16x8 v0 = frag_cols<DH>(vt, 0, 16 * d, lane);
-        const bf16x8 v1 = frag_cols<DH>(vt, 32, 16 * d, lane);
+      for (int d0 = 0; d0 < DT; d0 += DB) {
+        TrPair vq[DB][2];
 #pragma unroll
-        for (int qg = 0; qg < QG; ++qg) {
-          o[qg][d] = mfma(v0, pp[qg][0], o[qg][d]);
-          o[qg][d] = mfma(v1, pp[qg][1], o[qg][d]);
+        for (int d = 0; d < DB; ++d) {
+          vq[d][0] = frag_cols_tr<DH>(vt, 0, 16 * (d0 + d), lane);
+          vq[d][1] = frag_cols_tr<DH>(vt, 32, 16 * (d0 + d), lane);
+        }
+        lgkm_wait0();
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const bf16x8 v0 = tr_use(vq[d][0]), v1 = tr_use(vq[d][1]);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) {
+            o[qg][d0 + d] = mfma(v0, pp[qg][0], o[qg][d0 + d]);
+            o[qg][d0 + d] = mfma(v1, pp[qg][1], o[qg][d0 + d]);
+          }
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (kb + 1 < nkb) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    step_barrier();
   }
 #undef KT
 #undef VT
@@ -390,11 +459,14 @@ __global__ __launch_bounds__(256) void delta_kernel(const bf16_t* __restrict__ o
 }
 
 // ------------------------------------------------------------------------------ dK / dV
-template <int DH>
+// Ring slot = Q tile | dO tile | LSE[64] | delta[64] of one (q-head, q-block) step.  The 512 B
+// of row constants come by DMA as well (waves 0-1: LSE halves, waves 2-3: delta halves, 8
+// lanes x 16 B each), so every wave issues the same DH/16 + 1 DMA instructions per step.
+template <int DH, int NS>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
-  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // Q[2], dO[2]
-  __shared__ float s_lse[2][64], s_del[2][64];
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2;
+  constexpr int STG = 2 * TILE + 512, PER = DH / 16 + 1;
+  __shared__ __attribute__((aligned(16))) char smem[NS * STG];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -410,40 +482,49 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
   const int mykey = k0w + (lane & 15);
   const float c = a.scale * LOG2E;
 
+  const int nq = nkb - kb;     // q blocks at/after the diagonal
+  const int total = nq * grp;  // steps over (q-head in group, q block)
+  const float* rowsrc = wave < 2 ? (const float*)a.lse : a.delta;
+  const int rowoff = 32 * (wave & 1) + 4 * (lane & 7);
+  const int rowdst = 2 * TILE + 256 * (wave >> 1) + 128 * (wave & 1);
+  auto issue = [&](int it) {
+    char* st = smem + (it % NS) * STG;
+    const int gi = it / nq, qb = kb + it % nq;
+    const int h = kvh * grp + gi;
+    stage<DH>(base, W, qb * BQ, h * DH, st, wave, lane);
+    stage<DH>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
+    const float* src = rowsrc + ((long long)b * a.H + h) * a.T + qb * BQ + rowoff;
+    if (lane < 8) __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(st + rowdst), 16, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < total) issue(s);
+
   bf16x8 kf[KS], vf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     kf[ks] = gload8(base + (long long)mykey * W + kcol + ks * 32 + g * 8);
     vf[ks] = gload8(base + (long long)mykey * W + vcol + ks * 32 + g * 8);
   }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    settle(kf[ks]);
+    settle(vf[ks]);
+  }
+  step_barrier();
+
   f32x4 dk[DT], dv[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) dk[d] = dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#define QT(s) (smem + (s) * TILE)
-#define OT(s) (smem + (2 + (s)) * TILE)
-  const int nq = nkb - kb;     // q blocks at/after the diagonal
-  const int total = nq * grp;  // iterations over (q-head in group, q block)
-  auto issue = [&](int it, int buf) {
-    const int gi = it / nq, qb = kb + it % nq;
-    const int h = kvh * grp + gi;
-    stage<DH>(base, W, qb * BQ, h * DH, QT(buf), wave, lane);
-    stage<DH>(dob, C, qb * BQ, h * DH, OT(buf), wave, lane);
-    if (threadIdx.x < 64) {
-      const long long r = ((long long)b * a.H + h) * a.T + qb * BQ + threadIdx.x;
-      s_lse[buf][threadIdx.x] = a.lse[r] * LOG2E;
-      s_del[buf][threadIdx.x] = a.delta[r];
-    }
-  };
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   for (int it = 0; it < total; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < total) issue(it + 1, cur ^ 1);
+    if (it + NS - 1 < total) issue(it + NS - 1);
+    const char* st = smem + (it % NS) * STG;
+    const char* qt = st;
+    const char* ot = st + TILE;
+    const float* lse_s = (const float*)(st + 2 * TILE);
+    const float* del_s = lse_s + 64;
     const int qb = kb + it % nq;
-    const char* qt = QT(cur);
-    const char* ot = OT(cur);
     const bool diag = (qb == kb);
     f32x4 p[4], ds[4];
 #pragma unroll
@@ -457,26 +538,36 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * t + 4 * g + r;
-        float pv = exp2f(sacc[r] * c - s_lse[cur][ql]);
+        float pv = exp2f(sacc[r] * c - lse_s[ql] * LOG2E);
         if (diag && qb * BQ + ql < mykey) pv = 0.f;
         p[t][r] = pv;
-        ds[t][r] = pv * (dpacc[r] - s_del[cur][ql]);
+        ds[t][r] = pv * (dpacc[r] - del_s[ql]);
       }
     }
     const bf16x8 p0 = pack_pair(p[0], p[1]), p1 = pack_pair(p[2], p[3]);
     const bf16x8 d0 = pack_pair(ds[0], ds[1]), d1 = pack_pair(ds[2], ds[3]);
 #pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      dv[d] = mfma(frag_cols<DH>(ot, 0, 16 * d, lane), p0, dv[d]);
-      dv[d] = mfma(frag_cols<DH>(ot, 32, 16 * d, lane), p1, dv[d]);
-      dk[d] = mfma(frag_cols<DH>(qt, 0, 16 * d, lane), d0, dk[d]);
-      dk[d] = mfma(frag_cols<DH>(qt, 32, 16 * d, lane), d1, dk[d]);
+    for (int e0 = 0; e0 < DT; e0 += DB) {
+      TrPair fo[DB][2], fq[DB][2];
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        fo[d][0] = frag_cols_tr<DH>(ot, 0, 16 * (e0 + d), lane);
+        fo[d][1] = frag_cols_tr<DH>(ot, 32, 16 * (e0 + d), lane);
+        fq[d][0] = frag_cols_tr<DH>(qt, 0, 16 * (e0 + d), lane);
+        fq[d][1] = frag_cols_tr<DH>(qt, 32, 16 * (e0 + d), lane);
+      }
+      lgkm_wait0();
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        dv[e0 + d] = mfma(tr_use(fo[d][0]), p0, dv[e0 + d]);
+        dv[e0 + d] = mfma(tr_use(fo[d][1]), p1, dv[e0 + d]);
+        dk[e0 + d] = mfma(tr_use(fq[d][0]), d0, dk[e0 + d]);
+        dk[e0 + d] = mfma(tr_use(fq[d][1]), d1, dk[e0 + d]);
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (it + 1 < total) wait_vm_upto(PER * (min(it + NS - 1, total - 1) - it - 1));
+    step_barrier();
   }
-#undef QT
-#undef OT
   bf16_t* krow = a.dqkv + ((long long)b * a.T + mykey) * W;
 #pragma unroll
   for (int d = 0; d < DT; ++d) {
@@ -487,10 +578,10 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
 }
 
 // ------------------------------------------------------------------------------ dQ
-template <int DH>
+template <int DH, int NS>
 __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
-  constexpr int KS = DH / 32, DT = DH / 16, TILE = 64 * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K[2], V[2]
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2, PER = DH / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE];  // K[NS], V[NS]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -504,30 +595,42 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
   const int myq = qb * BQ + wave * 16 + (lane & 15);
   const float c = a.scale * LOG2E;
   const long long r = (long long)bh * a.T + myq;
-  const float lse2 = a.lse[r] * LOG2E, del = a.delta[r];
+  const int nkb = qb + 1;
 
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (NS + (s)) * TILE)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkb) {
+      stage<DH>(base, W, s * BKV, kcol, KT(s), wave, lane);
+      stage<DH>(base, W, s * BKV, vcol, VT(s), wave, lane);
+    }
   bf16x8 qf[KS], of[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
     of[ks] = gload8(a.dout + ((long long)b * a.T + myq) * C + h * DH + ks * 32 + g * 8);
   }
+  const float lse2 = a.lse[r] * LOG2E, del = a.delta[r];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    settle(qf[ks]);
+    settle(of[ks]);
+  }
+  settle(lse2);
+  settle(del);
+  step_barrier();
+
   f32x4 dq[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#define KT(s) (smem + (s) * TILE)
-#define VT(s) (smem + (2 + (s)) * TILE)
-  const int nkb = qb + 1;
-  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
-  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nkb) {
-      stage<DH>(base, W, (kb + 1) * BKV, kcol, KT(cur ^ 1), wave, lane);
-      stage<DH>(base, W, (kb + 1) * BKV, vcol, VT(cur ^ 1), wave, lane);
+    const int cur = kb % NS;
+    if (kb + NS - 1 < nkb) {
+      const int nx = (kb + NS - 1) % NS;
+      stage<DH>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
+      stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
     }
     const char* kt = KT(cur);
     const char* vt = VT(cur);
@@ -551,12 +654,22 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     }
     const bf16x8 d0 = pack_pair(ds[0], ds[1]), d1 = pack_pair(ds[2], ds[3]);
 #pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      dq[d] = mfma(frag_cols<DH>(kt, 0, 16 * d, lane), d0, dq[d]);
-      dq[d] = mfma(frag_cols<DH>(kt, 32, 16 * d, lane), d1, dq[d]);
+    for (int e0 = 0; e0 < DT; e0 += DB) {
+      TrPair fk[DB][2];
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        fk[d][0] = frag_cols_tr<DH>(kt, 0, 16 * (e0 + d), lane);
+        fk[d][1] = frag_cols_tr<DH>(kt, 32, 16 * (e0 + d), lane);
+      }
+      lgkm_wait0();
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        dq[e0 + d] = mfma(tr_use(fk[d][0]), d0, dq[e0 + d]);
+        dq[e0 + d] = mfma(tr_use(fk[d][1]), d1, dq[e0 + d]);
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (kb + 1 < nkb) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    step_barrier();
   }
 #undef KT
 #undef VT
@@ -572,24 +685,44 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
 
 using namespace rtdc;
 
+// ring depth: RTDC_FA_NS = 2 | 3 | 4 at Dh = 64.  Measured on GPT-2 shapes (B16 T1024 H12,
+// benchmarks/attn_bench.py): NS 2 / 3 / 4 = fwd 108 / 113 / 135 us, bwd 285 / 335 / 357 us -
+// every extra slot costs a co-resident block per CU (32 / 48 / 64 KiB of LDS per block), and
+// at these 8-16-step loops occupancy hides more HBM latency than a deeper ring.  Dh = 128
+// stays at 2 (a third slot leaves one block per CU).
+static int fa_ns(int Dh) {
+  static const int forced = getenv("RTDC_FA_NS") ? atoi(getenv("RTDC_FA_NS")) : 0;
+  if (Dh == 128) return 2;
+  return forced >= 2 && forced <= 4 ? forced : 2;
+}
+
+#define FA_DISPATCH(KERNEL, DH, NSV, GRID, ARGS)                                                        \
+  do {                                                                                                   \
+    if ((NSV) == 4) hipLaunchKernelGGL((KERNEL<DH, (DH == 64 ? 4 : 2)>), GRID, dim3(256), 0, st, ARGS); \
+    else if ((NSV) == 3) hipLaunchKernelGGL((KERNEL<DH, (DH == 64 ? 3 : 2)>), GRID, dim3(256), 0, st, ARGS); \
+    else hipLaunchKernelGGL((KERNEL<DH, 2>), GRID, dim3(256), 0, st, ARGS);                              \
+  } while (0)
+
 extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, int Hkv, int Dh,
                               float scale, hipStream_t st) {
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.lse = lse;
   a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
-  // measured (benchmarks/attn_bench.py): 32 rows/wave wins at Dh = 128 (Llama: 101 vs 108 us,
-  // 365 vs 401 us), 16 rows/wave at Dh = 64 (GPT-2: 100 vs 109 us); RTDC_FA_FWD=1|2 forces one
+  // measured (benchmarks/attn_bench.py, before the DMA ring): 32 rows/wave wins at Dh = 128
+  // (Llama: 101 vs 108 us), 16 rows/wave at Dh = 64 (GPT-2: 100 vs 109 us); RTDC_FA_FWD=1|2
+  // forces one
   static const int forced = getenv("RTDC_FA_FWD") ? atoi(getenv("RTDC_FA_FWD")) : 0;
   const int variant = forced ? forced : (Dh == 128 ? 2 : 1);
+  const int ns = fa_ns(Dh);
   if (variant == 2 && T % 128 == 0) {  // 32 rows per wave
-    dim3 grid(T / 128, B * H), block(256);
-    if (Dh == 64) hipLaunchKernelGGL(fa::fwd2_kernel<64>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(fa::fwd2_kernel<128>, grid, block, 0, st, a);
+    dim3 grid(T / 128, B * H);
+    if (Dh == 64) FA_DISPATCH(fa::fwd2_kernel, 64, ns, grid, a);
+    else FA_DISPATCH(fa::fwd2_kernel, 128, ns, grid, a);
   } else {
-    dim3 grid(T / 64, B * H), block(256);
-    if (Dh == 64) hipLaunchKernelGGL(fa::fwd_kernel<64>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(fa::fwd_kernel<128>, grid, block, 0, st, a);
+    dim3 grid(T / 64, B * H);
+    if (Dh == 64) FA_DISPATCH(fa::fwd_kernel, 64, ns, grid, a);
+    else FA_DISPATCH(fa::fwd_kernel, 128, ns, grid, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
@@ -609,13 +742,14 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   a.qkv = (const bf16_t*)qkv; a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta;
   a.dqkv = (bf16_t*)dqkv;
   a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
-  dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H), block(256);
+  dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H);
+  const int ns = fa_ns(Dh);
   if (Dh == 64) {
-    hipLaunchKernelGGL(fa::bwd_dkdv_kernel<64>, g1, block, 0, st, a);
-    hipLaunchKernelGGL(fa::bwd_dq_kernel<64>, g2, block, 0, st, a);
+    FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
+    FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
   } else {
-    hipLaunchKernelGGL(fa::bwd_dkdv_kernel<128>, g1, block, 0, st, a);
-    hipLaunchKernelGGL(fa::bwd_dq_kernel<128>, g2, block, 0, st, a);
+    FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
+    FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -16,6 +16,36 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
+// ---- transposing LDS read (ds_read_b64_tr_b16) as inline asm ---------------------------
+// The __builtin_amdgcn_ds_read_tr16_b64 form makes hipcc (ROCm 7.2) emit `s_waitcnt
+// vmcnt(0)` in front of every such read while any global_load_lds is in flight (checked in the
+// .s: one full drain of the DMA pipeline per group of transposing reads), which serialises
+// every DMA-fed loop that reads an MN-major / transposed operand.  The asm form is invisible
+// to hipcc's wait bookkeeping, so the protocol is explicit (cdna_hip_programming.md §5.7):
+// issue with ds_tr16(), retire with lgkm_wait0(), then pass each result through tr_use()
+// (an asm that names the registers, so no consumer is scheduled above the wait) before any
+// other use.  LDS ops return in order; an lgkmcnt(0) also covers hipcc's own LDS ops.
+struct TrPair {
+  bf16x4 lo, hi;
+};
+
+__device__ __forceinline__ bf16x4 ds_tr16(const char* p) {
+  bf16x4 r;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ bf16x8 tr_use(TrPair& f) {
+  asm volatile("" : "+v"(f.lo), "+v"(f.hi));
+  bf16x8 r;
+  r[0] = f.lo[0]; r[1] = f.lo[1]; r[2] = f.lo[2]; r[3] = f.lo[3];
+  r[4] = f.hi[0]; r[5] = f.hi[1]; r[6] = f.hi[2]; r[7] = f.hi[3];
+  return r;
+}
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }

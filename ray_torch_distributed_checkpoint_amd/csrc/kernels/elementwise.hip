@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 __global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ sidx,
                                                            const int64_t* __restrict__ perm,
                                                            const bf16_t* __restrict__ dout,
-                                                           float* __restrict__ dwte, int ntok, int D) {
+                                                           float* __restrict__ dwte, int ntok, int D,
+                                                           int accumulate) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= ntok) return;
@@ -63,6 +64,11 @@ __global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __res
       for (int q = 0; q < 8; ++q) acc[q] += g[q];
     }
     float* o = dwte + row * D + c;
+    if (accumulate) {  // second use of a tied table: add into the gradient already there
+      const float4 a0 = *(const float4*)o, a1 = *(const float4*)(o + 4);
+      acc[0] += a0.x; acc[1] += a0.y; acc[2] += a0.z; acc[3] += a0.w;
+      acc[4] += a1.x; acc[5] += a1.y; acc[6] += a1.z; acc[7] += a1.w;
+    }
     *(float4*)o = make_float4(acc[0], acc[1], acc[2], acc[3]);
     *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   }
@@ -161,11 +167,11 @@ extern "C" int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* w
 // sidx/perm: token ids stably sorted and their original positions (dwte rows that no token
 // uses are left untouched: the caller zero-fills).
 extern "C" int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe,
-                              int B, int T, int D, int accumulate_wpe, hipStream_t st) {
+                              int B, int T, int D, int accumulate_wpe, int accumulate_wte, hipStream_t st) {
   if (D % 8 != 0) return 1;
   const int ntok = B * T;
   hipLaunchKernelGGL(embed_bwd_wte_kernel, dim3((ntok + 3) / 4), dim3(256), 0, st, sidx, perm, (const bf16_t*)dout,
-                     dwte, ntok, D);
+                     dwte, ntok, D, accumulate_wte);
   if (dwpe)
     hipLaunchKernelGGL(embed_bwd_wpe_kernel, dim3(T, (D + 255) / 256), dim3(256), 0, st, (const bf16_t*)dout,
                        dwpe, B, T, D, accumulate_wpe);

@@ -79,25 +79,20 @@ struct Half96Stager {
   }
 };
 
-// fragment of a 96-row half: rows (= n) R0..R0+15, k-slice ks (same lane contract as load_frag)
+// fragment of a 96-row half: rows (= n) R0..R0+15, k-slice ks (same lane contract as
+// load_fragx: MN-major through the asm transposing read)
 template <bool KMAJOR>
-__device__ __forceinline__ bf16x8 load_frag96(const char* tile, int R0, int ks, int lane) {
+__device__ __forceinline__ typename Frag<KMAJOR>::T load_frag96(const char* tile, int R0, int ks, int lane) {
   if constexpr (KMAJOR) {
     return load_frag<true, 96>(tile, R0, ks, lane);
   } else {
     const int idx = lane & 15, q = idx >> 2, p = idx & 3, g = lane >> 4;
     const int c = (R0 >> 3) + (p >> 1);
-    bf16x4 v[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kr = ks * 32 + 8 * g + 4 * h + q;
-      const int off = kr * 192 + (((c + rot96(kr)) % 12) << 4) + ((p & 1) << 3);
-      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(tile + off));
-    }
-    bf16x8 r;
-    r[0] = v[0][0]; r[1] = v[0][1]; r[2] = v[0][2]; r[3] = v[0][3];
-    r[4] = v[1][0]; r[5] = v[1][1]; r[6] = v[1][2]; r[7] = v[1][3];
-    return r;
+    const int kr0 = ks * 32 + 8 * g + q, kr1 = kr0 + 4;
+    TrPair f;
+    f.lo = ds_tr16(tile + kr0 * 192 + (((c + rot96(kr0)) % 12) << 4) + ((p & 1) << 3));
+    f.hi = ds_tr16(tile + kr1 * 192 + (((c + rot96(kr1)) % 12) << 4) + ((p & 1) << 3));
+    return f;
   }
 }
 
@@ -187,12 +182,16 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
 #pragma unroll
     for (int p = 1; p <= 4; ++p) {
       // 1. fragments for this phase's quadrant (data retired by an earlier wait + barrier)
+      // fragments of this phase (MN-major ones as asm TrPair halves, turned into MFMA operands
+      // after the lgkmcnt wait below)
+      typename Frag<AK>::T ra[TMQ][2];
+      typename Frag<BKM>::T rb[TNQ][2];
       if (p == 1 || p == 3) {
         const char* ah = buf + (p == 1 ? 0 : HALF);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-          for (int i = 0; i < TMQ; ++i) fa[i][ks] = load_frag<AK, 128>(ah, SA * wa + 16 * i, ks, lane);
+          for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(ah, SA * wa + 16 * i, ks, lane);
       }
       if (p == 1 || p == 2) {
         const char* bh = buf + 2 * HALF + (p == 1 ? 0 : BHALF);
@@ -200,11 +199,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int j = 0; j < TNQ; ++j) {
-            bf16x8 f;
-            if constexpr (BN == 256) f = load_frag<BKM, 128>(bh, SB * wb + 16 * j, ks, lane);
-            else f = load_frag96<BKM>(bh, SB * wb + 16 * j, ks, lane);
-            if (p == 1) fbl[j][ks] = f;
-            else fbh[j][ks] = f;
+            if constexpr (BN == 256) rb[j][ks] = load_fragx<BKM, 128>(bh, SB * wb + 16 * j, ks, lane);
+            else rb[j][ks] = load_frag96<BKM>(bh, SB * wb + 16 * j, ks, lane);
           }
       }
       // 2. restage one half-tile of a later K-tile
@@ -218,6 +214,21 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (p == 1 || p == 3) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < TMQ; ++i) fa[i][ks] = fval(ra[i][ks]);
+      }
+      if (p == 1 || p == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            if (p == 1) fbl[j][ks] = fval(rb[j][ks]);
+            else fbh[j][ks] = fval(rb[j][ks]);
+          }
+      }
       // 4. one quadrant x K=64
       const int qa = (p - 1) >> 1, qb = (p - 1) & 1;
       __builtin_amdgcn_s_setprio(1);
@@ -282,6 +293,205 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
       }
 }
 
+// ---- persistent variant: one block per CU walks its tiles; the K-tile event stream runs on
+// across tile boundaries, so the next tile's first half-tiles are in flight while this tile
+// finishes, and its epilogue stores drain under the next tile's first MFMA phases.
+//
+// Block b owns tiles b, b + G, b + 2G, ... (G = gridDim.x, a multiple of 8 when the grid is
+// persistent, so all of a block's tiles stay on its XCD under tile_coords' XCD remap).  Global
+// K-tile index g = s*nt + t (s = the block's tile sequence number); event e = 4g + kind; LDS
+// buffer g & 1: gemm8_kernel's steady-state schedule, unchanged, over one long K loop.  What
+// changes at a tile boundary (g = the last K-tile of tile s):
+//   * the stagers switch to tile s+1 right before phase 4 of K-tile g-1 (the first issue of an
+//     event of the next tile: A-lo(g+1));
+//   * phase 4 of g retires through A-hi(g+1) (vmcnt(2) instead of vmcnt(6)): everything the
+//     next tile's phases 1-3 read is in LDS before the epilogue, so phases 1 and 2 of K-tile
+//     g+1 need no wait, and the stores issued in between are first waited on in phase 4 of
+//     g+1, three phases of MFMA work later.  No load/store completion order is assumed: every
+//     wait counts only the loads issued after the one it needs, so outstanding stores can
+//     make a wait longer, never let it pass early (CDNA4 vmcnt counts stores too);
+//   * accumulators are re-zeroed after the epilogue.
+template <bool AK, bool BKM, typename OutT, int BN = 256>
+__global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
+  constexpr int BH = BN / 2, WA = BN == 256 ? 2 : 4, WB = 8 / WA;
+  constexpr int SA = 128 / WA, SB = BH / WB, TMQ = SA / 16, TNQ = SB / 16;
+  constexpr int BHALF = BH * 128, BUF = 2 * HALF + 2 * BHALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024];
+  char* junk = smem + 2 * BUF;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wave % WA, wb = wave / WA;
+
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int my_tiles = b < ntiles ? (ntiles - b + G - 1) / G : 0;
+  const int nt = a.K / gemm::BK;  // >= 2 (host-checked)
+  const int total_kt = my_tiles * nt;
+  const int total_ev = 4 * total_kt;
+  if (total_kt == 0) return;
+
+  Stager<AK, 128, 8> sa0, sa1;
+  using SBT = std::conditional_t<BN == 256, Stager<BKM, 128, 8>, Half96Stager<BKM>>;
+  SBT sb0, sb1;
+  auto stage_tile = [&](int s) {
+    int tm, tn;
+    tile_coords(b + s * G, tiles_m, tiles_n, tm, tn);
+    sa0.init(a.A, a.lda, a.M, tm * BM, wave, lane);
+    sa1.init(a.A, a.lda, a.M, tm * BM + 128, wave, lane);
+    sb0.init(a.B, a.ldb, a.N, tn * BN, wave, lane);
+    sb1.init(a.B, a.ldb, a.N, tn * BN + BH, wave, lane);
+  };
+  // issue event e whose K-tile index inside its own tile is j (stagers point at that tile)
+  auto issue = [&](int e, int j) {
+    if (e >= total_ev) return;
+    const int kind = e & 3;
+    const int k0 = j * gemm::BK;
+    char* base = smem + ((e >> 2) & 1) * BUF;
+    if (kind == 0) sa0.issue(k0, base, wave);
+    else if (kind == 3) sa1.issue(k0, base + HALF, wave);
+    else if constexpr (BN == 256) {
+      if (kind == 1) sb0.issue(k0, base + 2 * HALF, wave);
+      else sb1.issue(k0, base + 3 * HALF, wave);
+    } else {
+      if (kind == 1) sb0.issue(k0, base + 2 * HALF, junk);
+      else sb1.issue(k0, base + 2 * HALF + BHALF, junk);
+    }
+  };
+
+  f32x4 acc[2][2][TMQ][TNQ];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile(0);
+  // prologue: A-lo(0) B-lo(0) B-hi(0) A-hi(0) A-lo(1) of the first tile (nt >= 2)
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  issue(4, 1);
+  wait_vm(6);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
+  OutT* C = (OutT*)a.C;
+  const OutT* Cin = (const OutT*)a.Cin;
+
+  bf16x8 fa[TMQ][2], fbl[TNQ][2], fbh[TNQ][2];
+  for (int s = 0; s < my_tiles; ++s) {
+    int tm, tn;
+    tile_coords(b + s * G, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const bool more = s + 1 < my_tiles;
+    for (int t = 0; t < nt; ++t) {
+      const int g = s * nt + t;
+      const char* buf = smem + (g & 1) * BUF;
+      const bool first = t == 0 && s > 0;  // its phase 1-2 data was retired before the epilogue
+      const bool last = t == nt - 1;
+#pragma unroll
+      for (int p = 1; p <= 4; ++p) {
+        // fragments of this phase (MN-major ones as asm TrPair halves, turned into MFMA operands
+        // after the lgkmcnt wait below)
+        typename Frag<AK>::T ra[TMQ][2];
+        typename Frag<BKM>::T rb[TNQ][2];
+        if (p == 1 || p == 3) {
+          const char* ah = buf + (p == 1 ? 0 : HALF);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(ah, SA * wa + 16 * i, ks, lane);
+        }
+        if (p == 1 || p == 2) {
+          const char* bh = buf + 2 * HALF + (p == 1 ? 0 : BHALF);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < TNQ; ++j) {
+              if constexpr (BN == 256) rb[j][ks] = load_fragx<BKM, 128>(bh, SB * wb + 16 * j, ks, lane);
+              else rb[j][ks] = load_frag96<BKM>(bh, SB * wb + 16 * j, ks, lane);
+            }
+        }
+        // restage: p1-p3 -> K-tile t+1 (the next tile's K-tile 0 when t is the last),
+        //          p4    -> A-lo of K-tile t+2
+        if (p == 4 && t == nt - 2 && more) stage_tile(s + 1);
+        if (p < 4) issue(4 * g + 4 + p, last ? 0 : t + 1);
+        else issue(4 * g + 8, t + 2 < nt ? t + 2 : t + 2 - nt);
+        // retire what later phases read
+        if (p == 1 || p == 2) {
+          if (!first) {
+            const int e = 4 * g + 4 + p, need = 4 * g + 1 + p;
+            wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
+          }
+        } else if (p == 4 && g + 1 < total_kt) {
+          const int e = 4 * g + 8;
+          const int need = last ? 4 * g + 7 : 4 * g + 5;  // A-hi(g+1) ahead of an epilogue
+          wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (p == 1 || p == 3) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < TMQ; ++i) fa[i][ks] = fval(ra[i][ks]);
+        }
+        if (p == 1 || p == 2) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < TNQ; ++j) {
+              if (p == 1) fbl[j][ks] = fval(rb[j][ks]);
+              else fbh[j][ks] = fval(rb[j][ks]);
+            }
+        }
+        const int qa = (p - 1) >> 1, qb = (p - 1) & 1;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+            for (int j = 0; j < TNQ; ++j) {
+              if (qb == 0)
+                acc[qa][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[j][ks], fa[i][ks], acc[qa][0][i][j], 0, 0, 0);
+              else
+                acc[qa][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbh[j][ks], fa[i][ks], acc[qa][1][i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // ---- epilogue of tile s (its stores drain under tile s+1's first phases)
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i) {
+          const int m = m0 + 128 * qa + SA * wa + 16 * i + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            const int n = n0 + BH * qb + SB * wb + 16 * j + 4 * (lane >> 4);
+            if (m < a.M && n < a.N) {
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
+              epilogue4<OutT>(a, C, Cin, m, n, v);
+            }
+            acc[qa][qb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+  }
+}
+
 }  // namespace g8
 }  // namespace rtdc
 
@@ -311,5 +521,45 @@ extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajo
     else G8(false, true, bf16_t);
   }
 #undef G8
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+static int g_num_cus = 0;
+
+// Persistent launch (gemm8p_kernel): grid = min(tiles, #CUs rounded down to a multiple of 8);
+// plain (non split-K) products with K >= 128 only.
+extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
+                                  hipStream_t st) {
+  const GemmArgs& a = *args;
+  if (a.splitk > 1 || a.K < 2 * gemm::BK) return 1;
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cus = n;
+  }
+  const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
+  long long gsz = (g_num_cus / 8) * 8;
+  if (gsz < 8) gsz = 8;
+  if (tiles < gsz) gsz = tiles;
+  dim3 grid((unsigned)gsz, 1, 1), block(512);
+#define G8P(AK, BKM, T)                                                                             \
+  do {                                                                                              \
+    if (bn == 192) hipLaunchKernelGGL((g8::gemm8p_kernel<AK, BKM, T, 192>), grid, block, 0, st, a); \
+    else hipLaunchKernelGGL((g8::gemm8p_kernel<AK, BKM, T, 256>), grid, block, 0, st, a);           \
+  } while (0)
+  if (out_fp32) {
+    if (a_kmajor && b_kmajor) G8P(true, true, float);
+    else if (a_kmajor) G8P(true, false, float);
+    else if (!b_kmajor) G8P(false, false, float);
+    else G8P(false, true, float);
+  } else {
+    if (a_kmajor && b_kmajor) G8P(true, true, bf16_t);
+    else if (a_kmajor) G8P(true, false, bf16_t);
+    else if (!b_kmajor) G8P(false, false, bf16_t);
+    else G8P(false, true, bf16_t);
+  }
+#undef G8P
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

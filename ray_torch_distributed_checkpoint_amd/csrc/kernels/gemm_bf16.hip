@@ -33,6 +33,8 @@
 // causal modes skip/limit work for the triangular attention products.
 #include "gemm_common.h"
 
+#include <cstdlib>
+
 namespace rtdc {
 
 
@@ -188,17 +190,24 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
     const char* tB = BUF_B(cur);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[TM], fb[TN];
+      typename Frag<AK>::T fa[TM];
+      typename Frag<BKM>::T fb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = load_frag<AK, BM>(tA, wm * (TM * 16) + i * 16, ks, lane);
+      for (int i = 0; i < TM; ++i) fa[i] = load_fragx<AK, BM>(tA, wm * (TM * 16) + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = load_frag<BKM, BN>(tB, wn * (TN * 16) + j * 16, ks, lane);
+      for (int j = 0; j < TN; ++j) fb[j] = load_fragx<BKM, BN>(tB, wn * (TN * 16) + j * 16, ks, lane);
+      if constexpr (!AK || !BKM) lgkm_wait0();  // asm transposing reads (gemm_common.h)
+      bf16x8 va[TM], vb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) va[i] = fval(fa[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) vb[j] = fval(fb[j]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[j], va[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -382,6 +391,22 @@ static int pick_cfg(const GemmArgs& a, int batch, bool a_kmajor, bool b_kmajor) 
 
 extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
                                  hipStream_t st);
+extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
+                                  hipStream_t st);
+
+// Persistent 8-wave kernel (gemm_8ph.hip gemm8p_kernel) for plain-K (no split-K) products with
+// more tiles than CUs: the next tile's loads and this tile's epilogue overlap MFMA work instead
+// of costing a prologue/epilogue bubble per tile (K = 768 GPT-2 products: 12 K-tiles per tile).
+// K-major x K-major only: the MN-major variants exceed 256 VGPRs with the persistent state.
+// RTDC_GEMM_PERSIST=0 disables it.
+static bool persist_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_GEMM_PERSIST");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
 
 // Split-K for long-K / few-tile products (weight gradients): choose the slice count s that
 // minimises a wave-quantised time model
@@ -419,14 +444,20 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
                   : cfg == 2 ? ntiles<Cfg128x256>(a) : cfg == 4 ? ntiles<Cfg256x64>(a)
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
-  if (cfg == 6 || cfg == 7) {  // 256x256 / 256x192 8-wave counted-vmcnt pipeline (gemm_8ph.hip)
+  const bool big = cfg >= 6 && cfg <= 9;  // 8-wave counted-vmcnt pipeline (gemm_8ph.hip)
+  const int bn = (cfg == 7 || cfg == 9) ? 192 : 256;
+  if (big) {
     if (batch != 1 || a.causal != 0) return 1;
-    tiles = (long long)((a.M + 255) / 256) * ((a.N + (cfg == 7 ? 191 : 255)) / (cfg == 7 ? 192 : 256));
+    tiles = (long long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
   }
   // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
-  if (plain) a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : 1.8) : pick_splitk(a, tiles);
-  if (cfg == 6 || cfg == 7) {
-    const int rc = rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, cfg == 7 ? 192 : 256, stream);
+  if (plain && cfg <= 7) a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : 1.8) : pick_splitk(a, tiles);
+  if (big) {
+    // cfg 8 / 9 force the persistent form; 6 / 7 take it automatically where it applies
+    const bool persist = cfg >= 8 || (persist_enabled() && a.splitk == 1 && a_kmajor && b_kmajor &&
+                                      tiles > 256 && a.K >= 2 * gemm::BK);
+    const int rc = persist ? rtdc_gemm8p_launch(&a, a_kmajor, b_kmajor, out_fp32, bn, stream)
+                           : rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, bn, stream);
     if (rc) return rc;
   } else if (out_fp32) {
     if (a_kmajor && b_kmajor) launch_layout<true, true, float>(a, cfg, batch, stream);

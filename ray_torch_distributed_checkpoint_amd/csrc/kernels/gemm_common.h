@@ -211,6 +211,41 @@ __device__ __forceinline__ bf16x8 load_frag(const char* lds_tile, int R0, int ks
   }
 }
 
+// MN-major fragment through the asm transposing read (common.h ds_tr16 protocol): same lane
+// contract as load_frag<false, ROWS>, returned as the two unassembled halves.  The builtin
+// form costs an `s_waitcnt vmcnt(0)` (a drain of every staged tile in flight) in front of each
+// group of reads.
+template <int ROWS>
+__device__ __forceinline__ TrPair load_frag_tr(const char* lds_tile, int R0, int ks, int lane) {
+  const int idx = lane & 15, q = idx >> 2, p = idx & 3, g = lane >> 4;
+  const int c = (R0 >> 3) + (p >> 1);
+  const int kr0 = ks * 32 + 8 * g + q, kr1 = kr0 + 4;
+  TrPair f;
+  f.lo = ds_tr16(lds_tile + kr0 * (ROWS * 2) + ((c ^ mnmaj_swz<ROWS>(kr0)) << 4) + ((p & 1) << 3));
+  f.hi = ds_tr16(lds_tile + kr1 * (ROWS * 2) + ((c ^ mnmaj_swz<ROWS>(kr1)) << 4) + ((p & 1) << 3));
+  return f;
+}
+
+// fragment register type per operand layout: K-major = compiler-tracked ds_read_b128,
+// MN-major = asm TrPair (retire with lgkm_wait0(), read through fval())
+template <bool KMAJOR>
+struct Frag {
+  using T = bf16x8;
+};
+template <>
+struct Frag<false> {
+  using T = TrPair;
+};
+
+template <bool KMAJOR, int ROWS>
+__device__ __forceinline__ typename Frag<KMAJOR>::T load_fragx(const char* lds_tile, int R0, int ks, int lane) {
+  if constexpr (KMAJOR) return load_frag<true, ROWS>(lds_tile, R0, ks, lane);
+  else return load_frag_tr<ROWS>(lds_tile, R0, ks, lane);
+}
+
+__device__ __forceinline__ bf16x8 fval(bf16x8& f) { return f; }
+__device__ __forceinline__ bf16x8 fval(TrPair& f) { return tr_use(f); }
+
 template <typename OutT>
 __device__ __forceinline__ void load4(const OutT* p, float* v);
 template <>

@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from ._ext import gpu_ext
-from .gradbuf import grad_target
+from .gradbuf import claimed_target, grad_target
 from .shadow import shadow_of
 
 
@@ -34,14 +34,20 @@ class _Embedding(torch.autograd.Function):
         wte_shape, wpe_shape = ctx.shapes
         wte, wpe = ctx.params
         dwte = grad_target(wte)
-        dwte = torch.zeros(wte_shape, dtype=torch.float32, device=idx.device) if dwte is None else dwte.zero_()
+        accumulate = False
+        if dwte is None:
+            # tied table (GPT-2 LM head): add into the gradient the LM head already wrote
+            dwte = claimed_target(wte)
+            accumulate = dwte is not None
+        dwte = torch.zeros(wte_shape, dtype=torch.float32, device=idx.device) if dwte is None else \
+            (dwte if accumulate else dwte.zero_())
         dwpe = None
         if wpe_shape is not None:
             dwpe = grad_target(wpe)
             dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device) if dwpe is None else dwpe.zero_()
         sidx, perm = torch.sort(idx.reshape(-1), stable=True)
-        gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False)
-        return None, dwte, dwpe
+        gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)
+        return None, (None if accumulate else dwte), dwpe
 
 
 def embedding(idx: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor | None = None,

@@ -26,3 +26,19 @@ def grad_target(p: torch.Tensor | None) -> torch.Tensor | None:
         return None  # already handed out this step (second use of a tied weight)
     p._rtdc_claim = sp.step_id
     return sp.grad_view(p)
+
+
+def claimed_target(p: torch.Tensor | None) -> torch.Tensor | None:
+    """For the second use of a tied weight in one step: the flat-buffer view that the first
+    use's backward already wrote (handed out by grad_target, not yet adopted by AccumulateGrad),
+    so a native backward can ADD its contribution in place and return no gradient - instead
+    of a fresh zero-filled tensor that autograd adds out of place and the optimizer copies
+    back into the buffer (3 full passes over a 154 MB GPT-2 table)."""
+    if p is None:
+        return None
+    sp = getattr(p, "_rtdc_space", None)
+    if sp is None or sp.grad is None or not sp.fresh or p.grad is not None:
+        return None
+    if getattr(p, "_rtdc_claim", -1) != sp.step_id:
+        return None
+    return sp.grad_view(p)

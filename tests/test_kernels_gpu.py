@@ -381,6 +381,68 @@ def test_gemm_tile_configs(cfg, a_k, b_k):
     _close(C, Af @ Bf, 1e-5)
 
 
+@pytest.mark.parametrize("cfg", [8, 9])
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("K", [128, 320])
+def test_gemm_persistent_multi_tile(cfg, a_k, b_k, K):
+    """Persistent 8-wave kernel (cfg 8: 256x256, 9: 256x192): > 256 tiles so blocks walk
+    several tiles (cross-tile DMA stream, deferred epilogue), partial edge tiles, K = 2 and 5
+    K-tiles per tile."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(cfg * 100 + K + a_k * 2 + b_k)
+    M, N = 4352 + 40, 4160  # 18 x 17 (256) / 18 x 22 (192) tiles, last row/column partial
+    A = _bf(M, K) if a_k else _bf(K, M)
+    B = _bf(N, K) if b_k else _bf(K, N)
+    Af = A.float() if a_k else A.float().t()
+    Bf = B.float().t() if b_k else B.float()
+    ref = Af @ Bf
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k, tile_cfg=cfg)
+    _close(C, ref, 1e-5)
+    Cb = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, Cb, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k, tile_cfg=cfg)
+    _close(Cb, ref, 1e-2)
+
+
+def test_gemm_persistent_epilogues():
+    """bias + GELU (pre-activation side output) and residual epilogues through the persistent
+    kernel, against the 2-launch reference."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(77)
+    M, N, K = 4608, 3072, 768
+    x, w = _bf(M, K), _bf(N, K, scale=0.05)
+    bias = torch.randn(N, device=DEV)
+    res = _bf(M, N)
+    pre_ref = x.float() @ w.float().t() + bias
+    for cfg in (8, 9):
+        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        G.gemm_bf16(x, w, y, M, N, K, K, K, N, True, True, bias=bias, aux_out=pre, act=G.ACT_GELU, tile_cfg=cfg)
+        _close(pre, pre_ref, 1e-2)
+        _close(y, F.gelu(pre_ref, approximate="tanh"), 1e-2)
+        y2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        G.gemm_bf16(x, w, y2, M, N, K, K, K, N, True, True, Cin=res, beta=1.0, bias=bias, tile_cfg=cfg)
+        _close(y2, pre_ref + res.float(), 1e-2)
+
+
+def test_gemm_persistent_auto_matches_plain(monkeypatch):
+    """The automatic persistent dispatch (RTDC_GEMM_PERSIST, default on) is bitwise identical
+    to the per-tile launch: same tiles, same MFMA order, only the schedule differs."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(5)
+    x, w = _bf(16384, 768), _bf(3072, 768)
+    y_auto = G.linear_fwd(x, w)
+    y6 = torch.empty_like(y_auto)
+    G.gemm_bf16(x, w, y6, 16384, 3072, 768, 768, 768, 3072, True, True, tile_cfg=6)
+    y8 = torch.empty_like(y_auto)
+    G.gemm_bf16(x, w, y8, 16384, 3072, 768, 768, 768, 3072, True, True, tile_cfg=8)
+    assert torch.equal(y6, y8)
+    _close(y_auto, x.float() @ w.float().t(), 1e-2)
+
+
 def test_gemm_splitk_wgrad():
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
 
@@ -396,7 +458,8 @@ def test_gemm_splitk_wgrad():
 
 
 @pytest.mark.parametrize("impl", ["flash", "gemm"])
-@pytest.mark.parametrize("H,Hkv,Dh,T", [(4, 4, 64, 256), (4, 2, 64, 192), (2, 1, 128, 128), (3, 3, 128, 320)])
+@pytest.mark.parametrize("H,Hkv,Dh,T", [(4, 4, 64, 256), (4, 2, 64, 192), (2, 1, 128, 128), (3, 3, 128, 320),
+                                         (2, 2, 64, 1024), (2, 1, 128, 640)])
 def test_attention_impls(monkeypatch, impl, H, Hkv, Dh, T):
     from ray_torch_distributed_checkpoint_amd.ops import causal_attention
     from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref

@@ -37,6 +37,31 @@ def test_gpt2_tiny_matches_reference_and_trains():
     assert losses[-1] < losses[0] - 1.0, losses
 
 
+def test_gpt2_tied_embedding_grad_in_flat_space():
+    """With the fused optimizer's flat gradient buffer in fresh mode, the tied token table's
+    two contributions (LM head wgrad, then the embedding scatter-add accumulated in place)
+    must equal the reference gradient."""
+    from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW
+
+    torch.manual_seed(3)
+    cfg = GPT2Config.named("gpt2-tiny")
+    ref = GPT2(cfg)
+    gpu = copy.deepcopy(ref).cuda()
+    opt = FusedAdamW(gpu.parameters(), lr=1e-3)
+    opt.init_state()
+    for _ in range(2):  # the second step exercises a reused buffer
+        opt.zero_grad(set_to_none=True)
+        idx = torch.randint(0, cfg.vocab_size, (4, 128))
+        ref.zero_grad()
+        ref(idx, idx.roll(-1, 1)).backward()
+        gpu(idx.cuda(), idx.roll(-1, 1).cuda()).backward()
+        g, r = gpu.wte.grad.cpu(), ref.wte.grad
+        assert gpu.wte.grad.data_ptr() == opt.flat_space.grad_view(gpu.wte).data_ptr()
+        err = (g - r).abs().max().item()
+        assert err < 0.08 * r.abs().max().item(), err
+
+
 def test_toy_mlp_native_fp32():
     from ray_torch_distributed_checkpoint_amd.models import NeuralNetwork
     from ray_torch_distributed_checkpoint_amd.ops import cross_entropy
