@@ -100,18 +100,22 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return r;
 }
 
-// tanh-approximation GELU (GPT-2) and its derivative.
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+// tanh-approximation GELU (GPT-2) and its derivative, through the logistic form
+//   0.5 (1 + tanh(u)) = s = 1 / (1 + e^{-2u}),   1 - tanh(u)^2 = 4 s (1 - s)
+// so each costs one v_exp_f32 and one v_rcp_f32 instead of a libm tanhf (these run in the
+// GEMM epilogues of c_fc forward and c_proj dgrad, over 50M elements per GPT-2 layer).
+// |x| large: e -> inf gives s = 0 (x * 0 = -0 for x -> -inf, the exact limit) and e -> 0 gives
+// s = 1; no NaN for finite x.
+__device__ __forceinline__ float gelu_sigmoid_arg(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, m2log2e = -2.0f * 1.4426950408889634f;
+  const float u = k0 * fmaf(k1 * x, x * x, x);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(m2log2e * u));
 }
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_sigmoid_arg(x); }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float s = gelu_sigmoid_arg(x);
+  return fmaf(2.f * x * s * (1.f - s) * k0, fmaf(3.f * k1, x * x, 1.f), s);
 }
 
 // Philox4x32-10 counter-based RNG: deterministic function of (seed, counter), so dropout

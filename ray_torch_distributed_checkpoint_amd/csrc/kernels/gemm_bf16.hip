@@ -372,8 +372,10 @@ static int pick_cfg(const GemmArgs& a, int batch, bool a_kmajor, bool b_kmajor) 
       // and qkv forward (737 vs 778 for 128x128), where per-tile efficiency outweighs the
       // better wave quantisation
       const bool better7 = eff_of(t7) > eff_of(t6) + 0.05;
-      const bool use7 = better7 && ((a_kmajor && b_kmajor && (t7 <= 256 || a.K >= 2048)) ||
-                                    (a_kmajor && !b_kmajor && a.K <= 4096));
+      // (re-measured with the asm transposing reads and the persistent form,
+      // profiles/gemm_bench_v5_asm_tr_persist.jsonl: qkv forward 840 TF at 256x192 vs 728 at
+      // 128x128 - the better-quantised 192-wide tile now wins for every forward product)
+      const bool use7 = better7 && ((a_kmajor && b_kmajor) || (a_kmajor && !b_kmajor && a.K <= 4096));
       const long long t = use7 ? t7 : t6;
       const double eff = use7 ? eff_of(t7) : eff_of(t6);
       const int big = use7 ? 7 : 6;
