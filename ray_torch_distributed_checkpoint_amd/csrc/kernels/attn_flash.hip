@@ -49,7 +49,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 struct Args {
   const bf16_t* qkv;  // [B, T, W]
   bf16_t* out;        // [B, T, H*Dh]
-  float* lse;         // [B*H, T] natural-log LSE of the scaled scores
+  float* lse;         // [B*H, T] row log-sum-exp of the scaled scores, base 2 (log2 domain)
   const bf16_t* dout; // [B, T, H*Dh]
   const float* delta; // [B*H, T]
   bf16_t* dqkv;       // [B, T, W]
@@ -142,6 +142,11 @@ __device__ __forceinline__ bf16x8 pack_pair(const f32x4& a, const f32x4& b) {
   return r;
 }
 
+// 2^x as the bare v_exp_f32.  exp2f() adds a denormal-range fix-up around it (compare, select,
+// add, select, ldexp: 6 VALU instead of 1 - measured in the loop's .s), and the softmax
+// loops are VALU-issue bound; probabilities below 2^-126 only need to underflow to 0.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -202,14 +207,15 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) s[t] = mfma(frag_rows<DH>(kt, 16 * t, ks, lane), qf[ks], s[t]);
     }
-    // scale (log2 domain), causal mask on the diagonal block, running max
+    // causal mask on the diagonal block, running max of the raw scores (c > 0: scaling into the
+    // log2 domain commutes with max, so it folds into one FMA per probability)
     float mx = -INFINITY;
     const bool diag = (kb == qb);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = s[t][r] * c;
+        float v = s[t][r];
         if (diag) {
           const int key = kb * BKV + 16 * t + 4 * g + r;
           if (key > myq) v = -INFINITY;
@@ -219,15 +225,15 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
       }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float mn = fmaxf(m, mx * c);
+    const float alpha = fexp2(m - mn);
     m = mn;
     float ps = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[t][r] - mn);
+        const float p = fexp2(fmaf(s[t][r], c, -mn));
         s[t][r] = p;
         ps += p;
       }
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
     const uint2 v = make_uint2(pack_bf2(o[d][0] * inv, o[d][1] * inv), pack_bf2(o[d][2] * inv, o[d][3] * inv));
     *(uint2*)(orow + 16 * d + 4 * g) = v;
   }
-  if (g == 0) a.lse[(long long)bh * a.T + myq] = (m + log2f(l)) / LOG2E;
+  if (g == 0) a.lse[(long long)bh * a.T + myq] = m + log2f(l);
 }
 
 // Forward, 32 query rows per wave (block = 128 rows): every K fragment read from LDS feeds
@@ -354,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v = sc[qg][t][r] * c;
+            float v = sc[qg][t][r];
             if (diag) {
               const int key = kb * BKV + 16 * t + 4 * g + r;
               if (key > myq[qg]) v = -INFINITY;
@@ -364,15 +370,15 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
           }
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mn = fmaxf(m[qg], mx);
-        const float alpha = exp2f(m[qg] - mn);
+        const float mn = fmaxf(m[qg], mx * c);
+        const float alpha = fexp2(m[qg] - mn);
         m[qg] = mn;
         float ps = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float pv = exp2f(sc[qg][t][r] - mn);
+            const float pv = fexp2(fmaf(sc[qg][t][r], c, -mn));
             sc[qg][t][r] = pv;
             ps += pv;
           }
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
                                  pack_bf2(o[qg][d][2] * inv, o[qg][d][3] * inv));
       *(uint2*)(orow + 16 * d + 4 * g) = v;
     }
-    if (g == 0) a.lse[(long long)bh * a.T + myq[qg]] = (m[qg] + log2f(lt)) / LOG2E;
+    if (g == 0) a.lse[(long long)bh * a.T + myq[qg]] = m[qg] + log2f(lt);
   }
 }
 
@@ -538,7 +544,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * t + 4 * g + r;
-        float pv = exp2f(sacc[r] * c - lse_s[ql] * LOG2E);
+        float pv = fexp2(fmaf(sacc[r], c, -lse_s[ql]));
         if (diag && qb * BQ + ql < mykey) pv = 0.f;
         p[t][r] = pv;
         ds[t][r] = pv * (dpacc[r] - del_s[ql]);
@@ -611,7 +617,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
     of[ks] = gload8(a.dout + ((long long)b * a.T + myq) * C + h * DH + ks * 32 + g * 8);
   }
-  const float lse2 = a.lse[r] * LOG2E, del = a.delta[r];
+  const float lse2 = a.lse[r], del = a.delta[r];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     settle(qf[ks]);
@@ -647,7 +653,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int key = kb * BKV + 16 * t + 4 * g + rr;
-        float pv = exp2f(sacc[rr] * c - lse2);
+        float pv = fexp2(fmaf(sacc[rr], c, -lse2));
         if (diag && key > myq) pv = 0.f;
         ds[t][rr] = pv * (dpacc[rr] - del);
       }
