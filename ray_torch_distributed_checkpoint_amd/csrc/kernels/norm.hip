@@ -115,6 +115,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     const bf16_t* xr = x + (long long)row * D;
     const bf16_t* dyr = dy + (long long)row * D;
     float xh[CPL][8], dxh[CPL][8];
+    // the residual-gradient row is loaded with x and dy (one memory round trip per row, not two)
+    uint4 rraw[CPL];
+    if (dres) {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) rraw[i] = *(const uint4*)(dres + (long long)row * D + c * 8);
+      }
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
@@ -142,7 +151,14 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
       const int c = lane + 64 * i;
       if (c < nch) {
         float o[8], r[8];
-        if (dres) ld8(dres + (long long)row * D + c * 8, r);
+        if (dres) {
+          const uint32_t w[4] = {rraw[i].x, rraw[i].y, rraw[i].z, rraw[i].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            r[2 * k] = __uint_as_float(w[k] << 16);
+            r[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+          }
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           o[e] = rstd * (dxh[i][e] - m1 - xh[i][e] * m2);

@@ -93,15 +93,40 @@ __global__ __launch_bounds__(256) void xent_kernel(const T* logits, T* dlogits,
   const T* x = logits + (long long)row * ld;
   OnlineMax o{-INFINITY, 0.f, 0x7fffffff};
   if constexpr (VEC) {
-    // 8 elements per 16-B load (bf16) / 4 (fp32)
-    constexpr int E = 16 / sizeof(T);
-    for (int c = threadIdx.x * E; c < ld; c += 256 * E) {
-      float v[E];
-      ldvec<T>(x + c, v);
+    // 8 elements per 16-B load (bf16) / 4 (fp32); U loads in flight per thread, and the running
+    // max is rescaled once per 16-B chunk (chunk max first) instead of a data-dependent branch
+    // per element
+    constexpr int E = 16 / sizeof(T), U = 4;
+    for (int c0 = threadIdx.x * E; c0 < ld; c0 += 256 * E * U) {
+      float v[U][E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int j = c + e;
-        if (j < V) om_push(o, v[e], j);
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + u * 256 * E;
+        if (c < ld) ldvec<T>(x + c, v[u]);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (c >= ld || c + e >= V) v[u][e] = -INFINITY;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + u * 256 * E;
+        float cm = v[u][0];
+        int ca = c;
+#pragma unroll
+        for (int e = 1; e < E; ++e)
+          if (v[u][e] > cm) {
+            cm = v[u][e];
+            ca = c + e;
+          }
+        if (cm > o.m) {  // first occurrence wins ties: later chunks only replace on a strict max
+          o.s *= __expf(o.m - cm);
+          o.m = cm;
+          o.arg = ca;
+        }
+        if (o.m != -INFINITY) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) o.s += __expf(v[u][e] - o.m);
+        }
       }
     }
   } else {
