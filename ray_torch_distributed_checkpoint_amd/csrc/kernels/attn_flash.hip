@@ -92,15 +92,41 @@ __device__ __forceinline__ bf16x8 frag_rows(const char* tile, int R0, int ks, in
 }
 
 // MFMA operand with rows = tile columns [d0, d0+16), k = tile rows in the accumulator order
-// kbase + 16(j>>2) + 4g + (j&3): two transposing reads (ds_read_b64_tr_b16), issued as asm
-// (common.h ds_tr16 protocol: lgkm_wait0() then tr_use() before the MFMA reads them)
+// kbase + 16(j>>2) + 4g + (j&3): two transposing reads (ds_read_b64_tr_b16) issued as asm
+// (common.h ds_tr16 protocol: lgkm_wait0() then tr_use() before the MFMA reads them).
+// Addressing: with the tile-row base kbase + 16h a multiple of 16,
+// the swizzle term depends on the lane only, so each lane keeps one LDS offset per 16-column
+// group d (tr_lane_offsets, computed once per kernel) and every read is that offset + the slot
+// base (one add per d per step) + an immediate (kbase + 16h) * row bytes - instead of ~6 VALU of
+// address arithmetic per transposing read in the VALU-bound softmax loop.
 template <int DH>
-__device__ __forceinline__ TrPair frag_cols_tr(const char* tile, int kbase, int d0, int lane) {
+__device__ __forceinline__ void tr_lane_offsets(uint32_t (&off)[DH / 16], int lane) {
+  constexpr int RB = DH * 2;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int lr = 4 * g + q, pb = p >> 1;
+  const int f = DH == 64 ? ((lr >> 1) & 7) : (lr & 15);
+#pragma unroll
+  for (int d = 0; d < DH / 16; ++d) off[d] = lr * RB + ((((2 * d) + pb) ^ f) << 4) + ((p & 1) << 3);
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x4 ds_tr16_at(uint32_t addr) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+  return r;
+}
+
+// frag_cols_tr(tile, KB, 16 d, lane) given lane_addr = LDS address of the tile + off[d]
+template <int DH, int KB>
+__device__ __forceinline__ TrPair frag_cols_at(uint32_t lane_addr) {
   TrPair f;
-  f.lo = ds_tr16(tile + toff<DH>(kbase + 4 * g + q, (d0 >> 3) + (p >> 1)) + ((p & 1) << 3));
-  f.hi = ds_tr16(tile + toff<DH>(kbase + 16 + 4 * g + q, (d0 >> 3) + (p >> 1)) + ((p & 1) << 3));
+  f.lo = ds_tr16_at<KB * DH * 2>(lane_addr);
+  f.hi = ds_tr16_at<(KB + 16) * DH * 2>(lane_addr);
   return f;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
 
 // 16-B global load of row `row` columns [c, c+8) -> bf16x8
@@ -169,6 +195,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
   const int q0w = qb * BQ + wave * 16;
   const int myq = q0w + (lane & 15);
   const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
   const int nkb = qb + 1;
 
 #define KT(s) (smem + (s) * TILE)
@@ -199,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
       stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
     }
     const char* kt = KT(cur);
-    const char* vt = VT(cur);
+    const uint32_t vbase = lds_addr(VT(cur));
     f32x4 s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -248,8 +276,9 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
       TrPair vq[DB][2];
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        vq[d][0] = frag_cols_tr<DH>(vt, 0, 16 * (d0 + d), lane);
-        vq[d][1] = frag_cols_tr<DH>(vt, 32, 16 * (d0 + d), lane);
+        const uint32_t la = vbase + troff[d0 + d];
+        vq[d][0] = frag_cols_at<DH, 0>(la);
+        vq[d][1] = frag_cols_at<DH, 32>(la);
       }
       lgkm_wait0();
 #pragma unroll
@@ -297,6 +326,8 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) myq[qg] = q0w + 16 * qg + (lane & 15);
   const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
   const int nkb = (qb + 1) * (BQ2 / BKV);
 
 #define KT(s) (smem + (s) * TILE)
@@ -338,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
     // keys of this tile all after this wave's last row: nothing to add (barriers still run)
     if (kb * BKV <= q0w + 31) {
       const char* kt = KT(cur);
-      const char* vt = VT(cur);
+      const uint32_t vbase = lds_addr(VT(cur));
       f32x4 sc[QG][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -395,8 +426,9 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
         TrPair vq[DB][2];
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
-          vq[d][0] = frag_cols_tr<DH>(vt, 0, 16 * (d0 + d), lane);
-          vq[d][1] = frag_cols_tr<DH>(vt, 32, 16 * (d0 + d), lane);
+          const uint32_t la = vbase + troff[d0 + d];
+          vq[d][0] = frag_cols_at<DH, 0>(la);
+          vq[d][1] = frag_cols_at<DH, 32>(la);
         }
         lgkm_wait0();
 #pragma unroll
@@ -487,6 +519,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
   const int k0w = kb * BKV + wave * 16;
   const int mykey = k0w + (lane & 15);
   const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
 
   const int nq = nkb - kb;     // q blocks at/after the diagonal
   const int total = nq * grp;  // steps over (q-head in group, q block)
@@ -528,6 +562,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
     const char* st = smem + (it % NS) * STG;
     const char* qt = st;
     const char* ot = st + TILE;
+    const uint32_t qbase = lds_addr(qt), obase = lds_addr(ot);
     const float* lse_s = (const float*)(st + 2 * TILE);
     const float* del_s = lse_s + 64;
     const int qb = kb + it % nq;
@@ -557,10 +592,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
       TrPair fo[DB][2], fq[DB][2];
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        fo[d][0] = frag_cols_tr<DH>(ot, 0, 16 * (e0 + d), lane);
-        fo[d][1] = frag_cols_tr<DH>(ot, 32, 16 * (e0 + d), lane);
-        fq[d][0] = frag_cols_tr<DH>(qt, 0, 16 * (e0 + d), lane);
-        fq[d][1] = frag_cols_tr<DH>(qt, 32, 16 * (e0 + d), lane);
+        const uint32_t lo = obase + troff[e0 + d], lq = qbase + troff[e0 + d];
+        fo[d][0] = frag_cols_at<DH, 0>(lo);
+        fo[d][1] = frag_cols_at<DH, 32>(lo);
+        fq[d][0] = frag_cols_at<DH, 0>(lq);
+        fq[d][1] = frag_cols_at<DH, 32>(lq);
       }
       lgkm_wait0();
 #pragma unroll
@@ -600,6 +636,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
   const int qcol = h * DH, kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
   const int myq = qb * BQ + wave * 16 + (lane & 15);
   const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
   const long long r = (long long)bh * a.T + myq;
   const int nkb = qb + 1;
 
@@ -640,6 +678,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     }
     const char* kt = KT(cur);
     const char* vt = VT(cur);
+    const uint32_t kbase_lds = lds_addr(kt);
     const bool diag = (kb == qb);
     f32x4 ds[4];
 #pragma unroll
@@ -664,8 +703,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
       TrPair fk[DB][2];
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        fk[d][0] = frag_cols_tr<DH>(kt, 0, 16 * (e0 + d), lane);
-        fk[d][1] = frag_cols_tr<DH>(kt, 32, 16 * (e0 + d), lane);
+        const uint32_t lk = kbase_lds + troff[e0 + d];
+        fk[d][0] = frag_cols_at<DH, 0>(lk);
+        fk[d][1] = frag_cols_at<DH, 32>(lk);
       }
       lgkm_wait0();
 #pragma unroll
