@@ -96,7 +96,10 @@ def main():
     torch.manual_seed(1234)
     wl = build_workload(args, dev, rank)
     model, opt = wl["model"], wl["opt"]
-    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
+    # the last bucket's all-reduce (GPT-2: the tied token table, whose gradient completes at the
+    # end of backward) overlaps the fused optimizer's update of every other parameter
+    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, defer_tail_to_optimizer=True) \
+        if world > 1 else model
     B, T = wl["batch"], wl["seq_len"]
     fwd_loss = wl["loss"]
 

@@ -492,7 +492,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("flat_grad"), py::arg("bounds"), py::arg("param_bucket"), py::arg("segments"),
            py::arg("process_group"), py::arg("use_avg"), py::arg("post_scale"))
       .def("mark_ready", &rtdc_ddp::GradBucketEngine::mark_ready)
-      .def("finalize", &rtdc_ddp::GradBucketEngine::finalize)
+      .def("finalize", &rtdc_ddp::GradBucketEngine::finalize, py::arg("defer_last") = false)
+      .def("wait_tail", &rtdc_ddp::GradBucketEngine::wait_tail)
+      .def("tail_pending", &rtdc_ddp::GradBucketEngine::tail_pending)
+      .def("tail_start", &rtdc_ddp::GradBucketEngine::tail_start)
       .def("num_buckets", &rtdc_ddp::GradBucketEngine::num_buckets)
       .def("launched", &rtdc_ddp::GradBucketEngine::launched)
       .def("steps", &rtdc_ddp::GradBucketEngine::steps)

@@ -51,19 +51,31 @@ class GradBucketEngine {
     launch_ready();
   }
 
-  void finalize() {
+  // defer_last: make the current stream wait for every bucket but the last one; the last
+  // bucket's collective stays in flight until wait_tail() (the fused optimizer updates the
+  // other parameters meanwhile - the last bucket holds the parameters whose gradients finish
+  // last, e.g. GPT-2's tied 154 MB token table, so its all-reduce is the step's exposed tail).
+  // Backends without an averaging collective (gloo) get the 1/world scale per part: the
+  // final slices now, the deferred one in wait_tail().
+  void finalize(bool defer_last = false) {
+    wait_tail();
     // parameters that produced no gradient this step contribute zeros (their slots may hold
     // a previous step's values when gradients are written in place): only unlaunched
     // buckets can contain them
     for (size_t i = 0; i < marked_.size(); ++i)
       if (!marked_[i]) flat_.slice(0, seg_[i].first, seg_[i].first + seg_[i].second).zero_();
     while (next_ < works_.size()) launch(next_++);
+    const bool defer = defer_last && works_.size() > 1;
     {
       pybind11::gil_scoped_release nogil;
-      for (auto& w : works_)
-        if (w) w->wait();
+      for (size_t b = 0; b + (defer ? 1 : 0) < works_.size(); ++b)
+        if (works_[b]) works_[b]->wait();
     }
-    if (!use_avg_ && post_scale_ != 1.0) flat_.mul_(post_scale_);
+    if (defer) tail_ = works_.back();
+    if (!use_avg_ && post_scale_ != 1.0) {
+      if (defer) flat_.slice(0, 0, tail_start()).mul_(post_scale_);
+      else flat_.mul_(post_scale_);
+    }
     for (auto& w : works_) w.reset();
     pending_ = expected_;
     std::fill(launched_.begin(), launched_.end(), false);
@@ -71,6 +83,19 @@ class GradBucketEngine {
     next_ = 0;
     ++steps_;
   }
+
+  // stream-order the last bucket's all-reduce before later work (no-op when none is pending)
+  void wait_tail() {
+    if (!tail_) return;
+    {
+      pybind11::gil_scoped_release nogil;
+      tail_->wait();
+    }
+    tail_.reset();
+    if (!use_avg_ && post_scale_ != 1.0) flat_.slice(0, tail_start(), bounds_.back()).mul_(post_scale_);
+  }
+  bool tail_pending() const { return (bool)tail_; }
+  int64_t tail_start() const { return bounds_[bounds_.size() - 2]; }
 
   int64_t num_buckets() const { return (int64_t)works_.size(); }
   int64_t steps() const { return steps_; }
@@ -101,6 +126,7 @@ class GradBucketEngine {
   bool use_avg_;
   double post_scale_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  c10::intrusive_ptr<c10d::Work> tail_;
   std::vector<bool> launched_, marked_;
   size_t next_ = 0;
   int64_t steps_ = 0;

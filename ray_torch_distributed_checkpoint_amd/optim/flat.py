@@ -73,6 +73,16 @@ class FlatParamSpace:
             self.refresh_shadows()
         self.grad_scale = 1.0
         self._chunk_cache: dict = {}
+        # (flat offset, wait fn) of a gradient slice whose all-reduce is still in flight
+        # (DistributedDataParallel(defer_tail_to_optimizer=True)); everything below the offset
+        # is final
+        self.pending_tail = None
+
+    def wait_pending_tail(self) -> None:
+        t = self.pending_tail
+        if t is not None:
+            self.pending_tail = None
+            t[1]()
 
     @staticmethod
     def view(buf: torch.Tensor, s: Segment) -> torch.Tensor:
@@ -99,6 +109,7 @@ class FlatParamSpace:
     def zero_grad(self, set_to_none: bool = False):
         if self.grad is None:
             return
+        self.wait_pending_tail()
         if set_to_none:
             for p in self.params:
                 p.grad = None
@@ -121,12 +132,29 @@ class FlatParamSpace:
             g = p.grad
             if g is not None and g.data_ptr() == base + 4 * s.offset:
                 continue
+            self.wait_pending_tail()  # never write into a slice a collective still owns
             v = self.view(self.grad, s)
             if g is None:
                 v.zero_()
             else:
                 v.copy_(g)
             p.grad = v
+
+    def chunk_table_split(self, params_subset, decay_flags, split: int):
+        """Two chunk tables: segments below flat offset `split`, and the rest."""
+        key = ("split", tuple(id(p) for p in params_subset), tuple(decay_flags), split)
+        hit = self._chunk_cache.get(key)
+        if hit is not None:
+            return hit
+        lo, hi = [], []
+        for p, d in zip(params_subset, decay_flags):
+            s = self.segment_of(p)
+            for st in range(0, s.numel, CHUNK):
+                ln = min(CHUNK, s.numel - st)
+                (lo if s.offset < split else hi).append((s.offset + st, ln | (int(bool(d)) << 32)))
+        out = tuple((torch.tensor(r if r else [(0, 0)], dtype=torch.int64).to(self.device), len(r)) for r in (lo, hi))
+        self._chunk_cache[key] = out
+        return out
 
     def chunk_table(self, params_subset, decay_flags) -> tuple[torch.Tensor, int]:
         """int64 [nchunks, 2] rows of (start, len | decay<<32) for the native optimizer kernels."""

@@ -106,6 +106,25 @@ class _FlatOptimizer(torch.optim.Optimizer):
                             v.copy_(st[k].to(v.device, v.dtype))
                             st[k] = v
 
+    def _launch_split(self, sp, launches) -> None:
+        """launches: [(params, decay_flags, fn(chunks, n))] per group.  With a pending
+        last-bucket all-reduce (DDP defer_tail_to_optimizer), update everything below its
+        slice first, stream-wait for the collective, then the slice itself."""
+        tail = sp.pending_tail
+        if tail is None:
+            for ps, flags, fn in launches:
+                fn(*sp.chunk_table(ps, flags))
+            return
+        split = tail[0]
+        parts = [(sp.chunk_table_split(ps, flags, split), fn) for ps, flags, fn in launches]
+        for (lo, _hi), fn in parts:
+            if lo[1]:
+                fn(*lo)
+        sp.wait_pending_tail()
+        for (_lo, hi), fn in parts:
+            if hi[1]:
+                fn(*hi)
+
     def _use_native(self):
         ps = self._all_params()
         return bool(ps) and ps[0].is_cuda
@@ -143,6 +162,7 @@ class FusedAdamW(_FlatOptimizer):
             sp = self._ensure_space()
             sp.ensure_grad_views()
             ext = gpu_ext()
+            launches = []
             for group in self.param_groups:
                 ps = group["params"]
                 if not ps:
@@ -156,11 +176,18 @@ class FusedAdamW(_FlatOptimizer):
                     step = float(st["step"])
                 b1, b2 = group["betas"]
                 wd = group["weight_decay"]
-                chunks, n = sp.chunk_table(ps, [wd != 0.0] * len(ps))
-                ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"], sp.shadow,
-                          group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step, math.sqrt(1 - b2 ** step),
-                          sp.grad_scale)
+
+                def fn(chunks, n, group=group, b1=b1, b2=b2, wd=wd, step=step):
+                    ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"],
+                              sp.shadow, group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step,
+                              math.sqrt(1 - b2 ** step), sp.grad_scale)
+
+                launches.append((ps, [wd != 0.0] * len(ps), fn))
+            self._launch_split(sp, launches)
             return loss
+        sp = space_of(self._all_params())
+        if sp is not None:
+            sp.wait_pending_tail()
         for group in self.param_groups:
             b1, b2 = group["betas"]
             for p in group["params"]:
@@ -207,6 +234,7 @@ class FusedSGD(_FlatOptimizer):
             sp = self._ensure_space()
             sp.ensure_grad_views()
             ext = gpu_ext()
+            launches = []
             for group in self.param_groups:
                 ps = group["params"]
                 if not ps:
@@ -220,10 +248,18 @@ class FusedSGD(_FlatOptimizer):
                             first = True
                         self._bind_state(p)
                 wd = group["weight_decay"]
-                chunks, n = sp.chunk_table(ps, [wd != 0.0] * len(ps))
-                ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None, sp.shadow,
-                        group["lr"], mom, group["dampening"], wd, group["nesterov"], first, sp.grad_scale)
+
+                def fn(chunks, n, group=group, mom=mom, wd=wd, first=first):
+                    ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None,
+                            sp.shadow, group["lr"], mom, group["dampening"], wd, group["nesterov"], first,
+                            sp.grad_scale)
+
+                launches.append((ps, [wd != 0.0] * len(ps), fn))
+            self._launch_split(sp, launches)
             return loss
+        sp = space_of(self._all_params())
+        if sp is not None:
+            sp.wait_pending_tail()
         for group in self.param_groups:
             mom = group["momentum"]
             for p in group["params"]:

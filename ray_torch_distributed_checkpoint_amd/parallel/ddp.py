@@ -18,6 +18,10 @@ MI355X:
   of backward; the end-of-backward callback only makes the compute stream wait.
 * Averaging is folded into the collective (ReduceOp.AVG on RCCL - no divide kernel); gloo
   (CPU tests) uses SUM + one in-place scale of the flat buffer.
+* With `defer_tail_to_optimizer`, backward returns with the LAST bucket's all-reduce still in
+  flight (on RCCL): the fused optimizer steps every other parameter first and stream-waits for
+  it only before the last slice, hiding the step's exposed collective tail (GPT-2: the tied
+  154 MB token table, whose gradient completes at the very end of backward).
 * Parameters and buffers are broadcast from rank 0 once at construction as ONE flat tensor;
   module buffers (BatchNorm running stats) are broadcast before each forward when
   `broadcast_buffers` (distributed.py:1557-1558 semantics) as one coalesced flat tensor.
@@ -47,9 +51,14 @@ class _Bucket:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 2.0, broadcast_buffers: bool = True, device_ids=None,
-                 output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True):
+                 output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
+                 defer_tail_to_optimizer: bool = False):
         super().__init__()
         self.module = module
+        # the last bucket's all-reduce stays in flight after backward; the fused optimizer
+        # updates every other parameter first and waits for it only before the last bucket's
+        # slice (FlatParamSpace.pending_tail) - overlaps the step's exposed collective tail
+        self.defer_tail = defer_tail_to_optimizer
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.broadcast_buffers = broadcast_buffers
@@ -171,7 +180,12 @@ class DistributedDataParallel(nn.Module):
                     b.copy_(v.view(b.shape).to(b.dtype))
 
     # ------------------------------------------------------------------ forward
+    def wait_tail(self) -> None:
+        """Stream-order a deferred last-bucket all-reduce (no-op when none is pending)."""
+        self.space.wait_pending_tail()
+
     def forward(self, *args, **kwargs):
+        self.space.wait_pending_tail()
         if self.world_size > 1 and self.broadcast_buffers and self._bufspace is not None and self.training:
             self._sync_buffers()
         return self.module(*args, **kwargs)
@@ -227,7 +241,9 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._steps += 1
         if self._engine is not None:
-            self._engine.finalize()
+            self._engine.finalize(self.defer_tail)
+            if self._engine.tail_pending():
+                self.space.pending_tail = (self._engine.tail_start(), self._engine.wait_tail)
             if self._check:  # RTDC_COLLECTIVE_CHECK=1: desync detector (one tiny all-reduce per step)
                 self._agree(self._steps * 1000003 + self._engine.launched() + len(self.buckets), "step sequence")
             return

@@ -47,6 +47,50 @@ def test_ddp_python_engine_matches_torch_ddp():
     assert max(out) < 1e-5, out
 
 
+def _ddp_deferred_tail(rank, world, opt_kind):
+    """defer_tail_to_optimizer: backward returns with the last bucket's all-reduce pending; the
+    fused optimizer steps the rest first and waits for it before the last slice - the same
+    parameters as torch DDP + torch optimizer after several steps."""
+    import copy
+
+    from ray_torch_distributed_checkpoint_amd.optim import FusedAdamW, FusedSGD
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(7)
+    base = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64), torch.nn.ReLU(),
+                               torch.nn.Linear(64, 5))
+    ours_m, ref_m = copy.deepcopy(base), copy.deepcopy(base)
+    ours = DistributedDataParallel(ours_m, bucket_cap_mb=0.01, first_bucket_mb=0.005, defer_tail_to_optimizer=True)
+    ref = torch.nn.parallel.DistributedDataParallel(ref_m)
+    assert len(ours.buckets) > 1
+    if opt_kind == "adamw":
+        opt_o = FusedAdamW(ours.parameters(), lr=1e-2, weight_decay=0.1)
+        opt_r = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.1)
+    else:
+        opt_o = FusedSGD(ours.parameters(), lr=0.1, momentum=0.9)
+        opt_r = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(100 + rank)
+    pending = []
+    for _ in range(4):
+        x = torch.randn(8, 20, generator=g)
+        y = torch.randint(0, 5, (8,), generator=g)
+        for m, opt in ((ours, opt_o), (ref, opt_r)):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            if m is ours:
+                pending.append(ours.space.pending_tail is not None)
+            opt.step()
+        assert ours.space.pending_tail is None
+    assert all(pending), pending
+    return max(float((a - b).abs().max()) for a, b in zip(ours_m.parameters(), ref_m.parameters()))
+
+
+def test_ddp_deferred_tail_matches_torch():
+    for kind in ("sgd", "adamw"):
+        out = mp_util.run(_ddp_deferred_tail, 2, kind)
+        assert max(out) < 1e-5, (kind, out)
+
+
 def _ddp_unused(rank, world):
     """A parameter without a gradient in a step contributes zeros (in-place gradient mode)."""
     from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
