@@ -51,13 +51,26 @@ def main():
     for name, M, K, N in SHAPES:
         if args.only and args.only != name:
             continue
-        x = torch.randn(M, K, device="cuda").bfloat16()
-        w = torch.randn(N, K, device="cuda").bfloat16()
+        xs = float(os.environ.get("GEMM_BENCH_XSCALE", "1"))  # e.g. 0.05: model-like magnitudes
+        x = (torch.randn(M, K, device="cuda") * xs).bfloat16()
+        w = (torch.randn(N, K, device="cuda") * xs).bfloat16()
         dy = torch.randn(M, N, device="cuda").bfloat16()
         flops = 2.0 * M * N * K
         row = {"shape": name, "M": M, "K": K, "N": N}
+        bias = torch.randn(N, device="cuda").bfloat16()
+        bias32 = bias.float()  # the models pass their fp32 master bias
+        res_in = torch.randn(M, N, device="cuda").bfloat16()
+        pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         for lay, ours, ref in [
             ("fwd", lambda: G.linear_fwd(x, w), lambda: x @ w.t()),
+            # fused epilogues as the GPT-2 blocks use them (reference: unfused torch ops)
+            ("fwd_bias_gelu", lambda: G.linear_fwd(x, w, bias, act=G.ACT_GELU, aux_out=pre),
+             lambda: torch.nn.functional.gelu(torch.addmm(bias, x, w.t()), approximate="tanh")),
+            ("fwd_f32bias_gelu", lambda: G.linear_fwd(x, w, bias32, act=G.ACT_GELU, aux_out=pre),
+             lambda: torch.nn.functional.gelu(torch.addmm(bias32, x.float(), w.float().t()), approximate="tanh")),
+            ("fwd_bias_res", lambda: G.linear_fwd(x, w, bias, residual=res_in),
+             lambda: torch.addmm(bias, x, w.t()) + res_in),
+            ("dgrad_gelu", lambda: G.linear_dgrad(dy, w, G.ACT_GELU_BWD, aux_in=x), lambda: dy @ w),
             ("dgrad", lambda: G.linear_dgrad(dy, w), lambda: dy @ w),
             ("wgrad", lambda: G.linear_wgrad(dy, x), lambda: (dy.t() @ x)),
         ]:

@@ -96,6 +96,148 @@ __device__ __forceinline__ typename Frag<KMAJOR>::T load_frag96(const char* tile
   }
 }
 
+// ---- tile epilogue: lane holds C[m][n..n+3] of every (quadrant, i, j) fragment.
+// bf16 outputs (the launcher guarantees 16-B-aligned operands): the two column halves'
+// fragments (qb = 0, 1) are regrouped by pair_frags so that each lane owns 8 consecutive
+// columns and every global access is 16 B - half the memory instructions of the 4-wide form
+// (c_fc forward stores the GELU output AND the pre-activation).  All epilogue traffic goes
+// through buffer descriptors whose range check replaces the per-lane bounds branches (with
+// branches hipcc's wait insertion falls back to vmcnt(0) at every join).  The residual /
+// activation input of a fragment pair is loaded W pairs ahead of its use: a load issued right
+// behind stores waits for them too (vmcnt counts both), which would serialise the store
+// stream behind each load.  One specialisation per
+// activation keeps the per-element code branch-free.
+template <int ACT, int TMQ, int TNQ, int SA, int SB, int BH, bool ZERO>
+__device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
+                                                   int wa, int wb, int lane, float alpha) {
+  constexpr bool ACT_IN = ACT == 3 || ACT == 4;
+  // descriptors over this tile's rows m0.. (tile-relative 32-bit offsets: the launcher keeps
+  // 256 rows x ldc x 2 B under 2 GiB)
+  const long long tile_off = (long long)m0 * a.ldc * 2, rows_bytes = (long long)(a.M - m0) * a.ldc * 2;
+  const auto rC = make_rsrc(a.C, tile_off, rows_bytes);
+  const bool has_cin = a.Cin && a.beta != 0.f;
+  const auto rIn = make_rsrc(ACT_IN ? (const void*)a.aux_in : a.Cin, tile_off, (ACT_IN || has_cin) ? rows_bytes : 0);
+  const auto rCin = make_rsrc(a.Cin, tile_off, (ACT_IN && has_cin) ? rows_bytes : 0);
+  const auto rAux = make_rsrc(a.aux_out, tile_off, ACT == 2 ? rows_bytes : 0);
+  const int bias_elt = a.bias_type == 2 ? 4 : 2;
+  const auto rBias = make_rsrc(a.bias, 0, a.bias_type ? (long long)a.N * bias_elt : 0);
+
+  const int g = lane >> 4;
+  const int nrun = n0 + SB * wb + ((g & 1) ? BH : 0) + 8 * (g >> 1);  // + 16 j
+  const int rrow = SA * wa + (lane & 15);                               // + 128 qa + 16 i (tile-relative)
+  // fragment pairs in order P = (qa * TMQ + i) * TNQ + j: consecutive stores complete a row's
+  // run of SB columns (a column-run-outer order left each 128-B line half written for half
+  // the epilogue; with outputs that miss the caches, c_fc forward took 159 instead of 124 us)
+  constexpr int NP = 2 * TMQ * TNQ, W = 2;
+  // (the lane part of the offset is one register; the per-pair parts are wave-uniform, so
+  // nothing per pair is loop-invariant across the persistent kernel's tiles)
+  const int lbase = rrow * a.ldc + nrun, rows_left = a.M - m0;
+  auto poff = [&](int P) -> uint32_t {
+    const int ro = 128 * (P / (TMQ * TNQ)) + 16 * ((P / TNQ) % TMQ), no = 16 * (P % TNQ);
+    return (rrow + ro < rows_left && nrun + no < a.N) ? (uint32_t)(lbase + ro * a.ldc + no) * 2u : BUF_OOB;
+  };
+  float bb[TNQ][8];
+#pragma unroll
+  for (int j = 0; j < TNQ; ++j) {
+    const int n = nrun + 16 * j;
+    if (a.bias_type == 2) {
+      const uint32_t o = n < a.N ? (uint32_t)n * 4u : BUF_OOB;
+      const u32x4 x = buf_load16(rBias, o), y = buf_load16(rBias, o + 16u);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bb[j][r] = __uint_as_float(x[r]);
+        bb[j][4 + r] = __uint_as_float(y[r]);
+      }
+    } else {  // bf16 bias, or none (zero records: loads return 0)
+      unpack8bf(buf_load16(rBias, n < a.N ? (uint32_t)n * 2u : BUF_OOB), bb[j]);
+    }
+  }
+  u32x4 xin[NP];
+  const bool load_in = ACT_IN || has_cin;
+#pragma unroll
+  for (int P = 0; P < W; ++P)
+    if (load_in) xin[P] = buf_load16(rIn, poff(P));
+#pragma unroll
+  for (int P = 0; P < NP; ++P) {
+    const int qa = P / (TMQ * TNQ), i = (P / TNQ) % TMQ, j = P % TNQ;
+    if (load_in && P + W < NP) xin[P + W] = buf_load16(rIn, poff(P + W));
+    const uint32_t off = poff(P);
+    float v[8];
+    pair_frags(acc[qa][0][i][j], acc[qa][1][i][j], alpha, v);
+    if constexpr (ZERO) {
+      acc[qa][0][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[qa][1][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += bb[j][r];
+    float x[8];
+    if constexpr (ACT_IN) {
+      unpack8bf(xin[P], x);
+      if (has_cin) {  // (not produced by the models; kept for the GEMM contract)
+        float c[8];
+        unpack8bf(buf_load16(rCin, off), c);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] += a.beta * c[r];
+      }
+    } else if (has_cin) {
+      unpack8bf(xin[P], x);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] += a.beta * x[r];
+    }
+    if constexpr (ACT == 1) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+    } else if constexpr (ACT == 2) {
+      buf_store16(rAux, off, pack8bf(v));
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = gelu_tanh(v[r]);
+    } else if constexpr (ACT == 3) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] *= gelu_tanh_grad(x[r]);
+    } else if constexpr (ACT == 4) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = x[r] > 0.f ? v[r] : 0.f;
+    }
+    buf_store16(rC, off, pack8bf(v));
+  }
+}
+
+template <typename OutT, int TMQ, int TNQ, int SA, int SB, int BH, bool ZERO>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
+                                              int wa, int wb, int lane, float alpha) {
+  if constexpr (std::is_same_v<OutT, bf16_t>) {
+    switch (a.act) {
+      case 1: tile_epilogue_bf16<1, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+      case 2: tile_epilogue_bf16<2, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+      case 3: tile_epilogue_bf16<3, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+      case 4: tile_epilogue_bf16<4, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+      default: tile_epilogue_bf16<0, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+    }
+  } else {
+    OutT* C = (OutT*)a.C;
+    const OutT* Cin = (const OutT*)a.Cin;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i) {
+          const int m = m0 + 128 * qa + SA * wa + 16 * i + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            const int n = n0 + BH * qb + SB * wb + 16 * j + 4 * (lane >> 4);
+            if (m < a.M && n < a.N) {
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
+              epilogue4<OutT>(a, C, Cin, m, n, v);
+            }
+            if constexpr (ZERO) acc[qa][qb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+  }
+}
+
 // outstanding glds instructions allowed (wave-uniform): counted waits are immediates
 __device__ __forceinline__ void wait_vm(int allowed) {
   if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -271,26 +413,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
         }
     return;
   }
-  OutT* C = (OutT*)a.C;
-  const OutT* Cin = (const OutT*)a.Cin;
-#pragma unroll
-  for (int qa = 0; qa < 2; ++qa)
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-      for (int i = 0; i < TMQ; ++i) {
-        const int m = m0 + 128 * qa + SA * wa + 16 * i + (lane & 15);
-        if (m >= a.M) continue;
-#pragma unroll
-        for (int j = 0; j < TNQ; ++j) {
-          const int n = n0 + BH * qb + SB * wb + 16 * j + 4 * (lane >> 4);
-          if (n >= a.N) continue;
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
-          epilogue4<OutT>(a, C, Cin, m, n, v);
-        }
-      }
+  tile_epilogue<OutT, TMQ, TNQ, SA, SB, BH, false>(a, acc, m0, n0, wa, wb, lane, alpha);
 }
 
 // ---- persistent variant: one block per CU walks its tiles; the K-tile event stream runs on
@@ -382,8 +505,6 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
   __builtin_amdgcn_s_barrier();
 
   const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
-  OutT* C = (OutT*)a.C;
-  const OutT* Cin = (const OutT*)a.Cin;
 
   bf16x8 fa[TMQ][2], fbl[TNQ][2], fbh[TNQ][2];
   for (int s = 0; s < my_tiles; ++s) {
@@ -469,26 +590,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
         __builtin_amdgcn_s_setprio(0);
       }
     }
-    // ---- epilogue of tile s (its stores drain under tile s+1's first phases)
-#pragma unroll
-    for (int qa = 0; qa < 2; ++qa)
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-        for (int i = 0; i < TMQ; ++i) {
-          const int m = m0 + 128 * qa + SA * wa + 16 * i + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < TNQ; ++j) {
-            const int n = n0 + BH * qb + SB * wb + 16 * j + 4 * (lane >> 4);
-            if (m < a.M && n < a.N) {
-              float v[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
-              epilogue4<OutT>(a, C, Cin, m, n, v);
-            }
-            acc[qa][qb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
+    // ---- epilogue of tile s (its stores drain under tile s+1's first phases); re-zeroes acc
+    tile_epilogue<OutT, TMQ, TNQ, SA, SB, BH, true>(a, acc, m0, n0, wa, wb, lane, alpha);
   }
 }
 

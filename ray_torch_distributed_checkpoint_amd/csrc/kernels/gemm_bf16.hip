@@ -439,7 +439,12 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
                               hipStream_t stream) {
   GemmArgs a = *args;
   if (a.K % gemm::BK != 0 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
-  const int cfg = pick_cfg(a, batch, a_kmajor, b_kmajor);
+  int cfg = pick_cfg(a, batch, a_kmajor, b_kmajor);
+  // the 8-wave kernels write bf16 outputs 16 B at a time through tile-relative 32-bit buffer
+  // offsets (gemm_8ph.hip tile_epilogue)
+  const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
+                       (uintptr_t)a.bias;
+  if (cfg >= 6 && cfg <= 9 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;

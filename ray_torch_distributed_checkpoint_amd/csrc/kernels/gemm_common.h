@@ -311,6 +311,53 @@ __device__ __forceinline__ void epilogue4(const GemmArgs& a, OutT* C, const OutT
   store4<OutT>(C + off, v);
 }
 
+// 8-wide (16-B) form of epilogue4 for bf16 outputs: v = C[m][n..n+7], n % 8 == 0, every
+// operand 16-B aligned and ldc % 8 == 0 (checked by the launcher).  Half the global instructions of two epilogue4 calls.
+// Buffer descriptor over `bytes` bytes from base + byte_off (wave-uniform inputs; the
+// readfirstlanes make that provable to hipcc, else it wraps every buffer op in a waterfall
+// loop - cdna_hip_programming.md T20).  A voffset >= bytes (BUF_OOB) loads 0 / drops the store,
+// which replaces per-lane bounds branches: records are capped below BUF_OOB.
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+constexpr uint32_t BUF_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long byte_off, long long bytes) {
+  const uintptr_t u = (uintptr_t)base + byte_off;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  const long long cap = (long long)BUF_OOB - 16;
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0 ? 0 : (bytes > cap ? cap : bytes)));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void unpack8bf(const u32x4& x, float* v) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[2 * r] = __uint_as_float(x[r] << 16);
+    v[2 * r + 1] = __uint_as_float(x[r] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8bf(const float* v) {
+  return u32x4{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+}
+
+// Two MFMA 16x16 fragments x0 / x1 of the same rows (lane: row m, columns 4g..4g+3 of the
+// fragment, g = lane >> 4) -> one 8-column run per lane.  v_permlane16_swap exchanges the odd
+// 16-lane rows of its first operand with the even rows of its second, so after four swaps
+// lane rows g = 0, 1, 2, 3 hold columns 0-7 of x0, 0-7 of x1, 8-15 of x0, 8-15 of x1
+// (v = alpha-scaled).  All 64 lanes must execute it (no divergent branch around it).
+__device__ __forceinline__ void pair_frags(const f32x4& x0, const f32x4& x1, float alpha, float* v) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0[r]), __float_as_uint(x1[r]), false, false);
+    v[r] = __uint_as_float(s[0]) * alpha;
+    v[4 + r] = __uint_as_float(s[1]) * alpha;
+  }
+}
+
 // XCD-aware bijective remap of a flat tile id + GROUP_M super-rows (cdna_hip_programming.md
 // T1): consecutive tiles on one XCD share A row-panels in its L2.
 __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {

@@ -8,6 +8,7 @@ checkpoint runtime (which has no GPU dependency) is still used when the library 
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -26,7 +27,13 @@ def _import():
         if _mod is not None or _err is not None:
             return _mod
         try:
-            _mod = importlib.import_module("ray_torch_distributed_checkpoint_amd._C")
+            alt = os.environ.get("RTDC_EXT_SO")  # A/B runs: another build of the same module
+            if alt:
+                spec = importlib.util.spec_from_file_location("ray_torch_distributed_checkpoint_amd._C", alt)
+                _mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(_mod)
+            else:
+                _mod = importlib.import_module("ray_torch_distributed_checkpoint_amd._C")
         except Exception as e:  # pragma: no cover - exercised on unbuilt trees
             if os.environ.get("RTDC_AUTOBUILD", "0") == "1":
                 from .. import _build
