@@ -97,10 +97,12 @@ __device__ __forceinline__ typename Frag<KMAJOR>::T load_frag96(const char* tile
 }
 
 // ---- tile epilogue: lane holds C[m][n..n+3] of every (quadrant, i, j) fragment.
-// bf16 outputs (the launcher guarantees 16-B-aligned operands): the two column halves'
-// fragments (qb = 0, 1) are regrouped by pair_frags so that each lane owns 8 consecutive
-// columns and every global access is 16 B - half the memory instructions of the 4-wide form
-// (c_fc forward stores the GELU output AND the pre-activation).  All epilogue traffic goes
+// bf16 outputs (the launcher guarantees 16-B-aligned operands): two fragments of the same rows
+// are regrouped by pair_frags so that each lane owns 8 consecutive columns and every global
+// access is 16 B - half the memory instructions of the 4-wide form (c_fc forward stores the
+// GELU output AND the pre-activation).  With an even TNQ the pair is (j, j+1) of one column
+// half, so one store instruction writes 32 consecutive columns (64 B) of each of its 16 rows;
+// otherwise (256x192 tiles) it is the same j of the two halves.  All epilogue traffic goes
 // through buffer descriptors whose range check replaces the per-lane bounds branches (with
 // branches hipcc's wait insertion falls back to vmcnt(0) at every join).  The residual /
 // activation input of a fragment pair is loaded W pairs ahead of its use: a load issued right
@@ -122,10 +124,14 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
   const int bias_elt = a.bias_type == 2 ? 4 : 2;
   const auto rBias = make_rsrc(a.bias, 0, a.bias_type ? (long long)a.N * bias_elt : 0);
 
+  // column runs c < TNQ: pair (qb, 2jp), (qb, 2jp + 1) for c = qb * TNQ/2 + jp (PJ), or
+  // (0, c), (1, c) (PQ); the lane's 8 columns are nrun + cno(c)
+  constexpr bool PJ = TNQ % 2 == 0;
   const int g = lane >> 4;
-  const int nrun = n0 + SB * wb + ((g & 1) ? BH : 0) + 8 * (g >> 1);  // + 16 j
-  const int rrow = SA * wa + (lane & 15);                               // + 128 qa + 16 i (tile-relative)
-  // fragment pairs in order P = (qa * TMQ + i) * TNQ + j: consecutive stores complete a row's
+  const int nrun = n0 + SB * wb + (PJ ? 16 * (g & 1) : BH * (g & 1)) + 8 * (g >> 1);
+  auto cno = [&](int c) { return PJ ? BH * (c / (TNQ / 2)) + 32 * (c % (TNQ / 2)) : 16 * c; };
+  const int rrow = SA * wa + (lane & 15);  // + 128 qa + 16 i (tile-relative)
+  // fragment pairs in order P = (qa * TMQ + i) * TNQ + c: consecutive stores complete a row's
   // run of SB columns (a column-run-outer order left each 128-B line half written for half
   // the epilogue; with outputs that miss the caches, c_fc forward took 159 instead of 124 us)
   constexpr int NP = 2 * TMQ * TNQ, W = 2;
@@ -133,23 +139,23 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
   // nothing per pair is loop-invariant across the persistent kernel's tiles)
   const int lbase = rrow * a.ldc + nrun, rows_left = a.M - m0;
   auto poff = [&](int P) -> uint32_t {
-    const int ro = 128 * (P / (TMQ * TNQ)) + 16 * ((P / TNQ) % TMQ), no = 16 * (P % TNQ);
+    const int ro = 128 * (P / (TMQ * TNQ)) + 16 * ((P / TNQ) % TMQ), no = cno(P % TNQ);
     return (rrow + ro < rows_left && nrun + no < a.N) ? (uint32_t)(lbase + ro * a.ldc + no) * 2u : BUF_OOB;
   };
-  float bb[TNQ][8];
+  float bb[TNQ][8];  // bias of each column run
 #pragma unroll
-  for (int j = 0; j < TNQ; ++j) {
-    const int n = nrun + 16 * j;
+  for (int c = 0; c < TNQ; ++c) {
+    const int n = nrun + cno(c);
     if (a.bias_type == 2) {
       const uint32_t o = n < a.N ? (uint32_t)n * 4u : BUF_OOB;
       const u32x4 x = buf_load16(rBias, o), y = buf_load16(rBias, o + 16u);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        bb[j][r] = __uint_as_float(x[r]);
-        bb[j][4 + r] = __uint_as_float(y[r]);
+        bb[c][r] = __uint_as_float(x[r]);
+        bb[c][4 + r] = __uint_as_float(y[r]);
       }
     } else {  // bf16 bias, or none (zero records: loads return 0)
-      unpack8bf(buf_load16(rBias, n < a.N ? (uint32_t)n * 2u : BUF_OOB), bb[j]);
+      unpack8bf(buf_load16(rBias, n < a.N ? (uint32_t)n * 2u : BUF_OOB), bb[c]);
     }
   }
   u32x4 xin[NP];
@@ -159,17 +165,19 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
     if (load_in) xin[P] = buf_load16(rIn, poff(P));
 #pragma unroll
   for (int P = 0; P < NP; ++P) {
-    const int qa = P / (TMQ * TNQ), i = (P / TNQ) % TMQ, j = P % TNQ;
+    const int qa = P / (TMQ * TNQ), i = (P / TNQ) % TMQ, c = P % TNQ;
     if (load_in && P + W < NP) xin[P + W] = buf_load16(rIn, poff(P + W));
     const uint32_t off = poff(P);
     float v[8];
-    pair_frags(acc[qa][0][i][j], acc[qa][1][i][j], alpha, v);
+    f32x4& x0 = PJ ? acc[qa][c / (TNQ / 2)][i][2 * (c % (TNQ / 2))] : acc[qa][0][i][c];
+    f32x4& x1 = PJ ? acc[qa][c / (TNQ / 2)][i][2 * (c % (TNQ / 2)) + 1] : acc[qa][1][i][c];
+    pair_frags(x0, x1, alpha, v);
     if constexpr (ZERO) {
-      acc[qa][0][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[qa][1][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      x0 = f32x4{0.f, 0.f, 0.f, 0.f};
+      x1 = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] += bb[j][r];
+    for (int r = 0; r < 8; ++r) v[r] += bb[c][r];
     float x[8];
     if constexpr (ACT_IN) {
       unpack8bf(xin[P], x);
