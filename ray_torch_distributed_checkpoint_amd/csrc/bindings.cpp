@@ -25,10 +25,10 @@ int rtdc_layernorm_fwd(const void* x, const void* g, const void* b, void* y, flo
 int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rstd, int M, int D, float eps,
                      hipStream_t st);
 int rtdc_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean, const float* rstd,
-                       const void* dres, void* dx, float* ws, float* dg, float* db, int M, int D,
+                       const void* dres, void* dx, float* ws, float* dg, float* db, float* dxsum, int M, int D,
                        int nwaves, int accumulate, hipStream_t st);
 int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, const float* rstd, const void* dres,
-                     void* dx, float* ws, float* dg, int M, int D, int nwaves, int accumulate,
+                     void* dx, float* ws, float* dg, float* dxsum, int M, int D, int nwaves, int accumulate,
                      hipStream_t st);
 int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out, int accumulate,
                 int is_bf16, hipStream_t st);
@@ -98,7 +98,8 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
                       int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool a_kmajor, bool b_kmajor,
                       int64_t batch, int64_t batch_inner, int64_t sA0, int64_t sA1, int64_t sB0, int64_t sB1,
                       int64_t sC0, int64_t sC1, double alpha, double beta, int64_t act, int64_t causal,
-                      c10::optional<Tensor> ws, int64_t tile_cfg, c10::optional<Tensor> alpha_dev) {
+                      c10::optional<Tensor> ws, int64_t tile_cfg, c10::optional<Tensor> alpha_dev,
+                      c10::optional<Tensor> cs_out, c10::optional<Tensor> cs_ws) {
   check_dev(A, "A");
   check_dev(B, "B");
   check_dev(C, "C");
@@ -128,6 +129,14 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
     TORCH_CHECK(alpha_dev->scalar_type() == at::kFloat && alpha_dev->numel() == 1 && alpha_dev->is_cuda(),
                 "alpha_dev must be a 1-element fp32 GPU tensor");
     a.alpha_dev = alpha_dev->data_ptr<float>();
+  }
+  if (cs_out.has_value()) {  // column sums of C (fp32 [N]) with cs_ws scratch
+    TORCH_CHECK(cs_ws.has_value() && cs_out->scalar_type() == at::kFloat && cs_out->numel() >= N &&
+                    cs_ws->scalar_type() == at::kFloat && batch == 1,
+                "gemm_bf16: cs_out needs fp32 [N] + fp32 cs_ws scratch, batch 1");
+    a.cs_out = cs_out->data_ptr<float>();
+    a.cs_ws = cs_ws->data_ptr<float>();
+    a.cs_ws_elems = cs_ws->numel();
   }
   TORCH_CHECK(!(act == 2) || a.aux_out, "gelu forward needs aux_out");
   TORCH_CHECK(!(act == 3 || act == 4) || a.aux_in, "activation backward needs aux_in");
@@ -172,23 +181,29 @@ static void rmsnorm_fwd(Tensor x, Tensor g, Tensor y, Tensor rstd, double eps) {
                             cur_stream()),
            "rmsnorm_fwd");
 }
+// dxsum (optional, fp32 [D]): column sums of dx, produced by the same kernel
 static void layernorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
-                          Tensor dx, Tensor ws, Tensor dg, Tensor db, int64_t nwaves, bool accumulate) {
+                          Tensor dx, Tensor ws, Tensor dg, Tensor db, c10::optional<Tensor> dxsum, int64_t nwaves,
+                          bool accumulate) {
   const int D = (int)x.size(-1), M = (int)(x.numel() / D);
-  TORCH_CHECK(ws.numel() >= (2 * (nwaves / 4) + 128) * D, "layernorm_bwd workspace too small");
+  const int nz = 2 + (dxsum.has_value() ? 1 : 0);
+  TORCH_CHECK(ws.numel() >= nz * (nwaves / 4 + 64) * D, "layernorm_bwd workspace too small");
+  if (dxsum.has_value()) TORCH_CHECK(dxsum->numel() >= D && dxsum->scalar_type() == at::kFloat, "dxsum: fp32 [D]");
   check_rc(rtdc_layernorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr<float>(),
                               rstd.data_ptr<float>(), ptr_or_null(dres), dx.data_ptr(), ws.data_ptr<float>(),
-                              dg.data_ptr<float>(), db.data_ptr<float>(), M, D, (int)nwaves, accumulate,
-                              cur_stream()),
+                              dg.data_ptr<float>(), db.data_ptr<float>(), (float*)ptr_or_null(dxsum), M, D,
+                              (int)nwaves, accumulate, cur_stream()),
            "layernorm_bwd");
 }
 static void rmsnorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor rstd, c10::optional<Tensor> dres, Tensor dx,
-                        Tensor ws, Tensor dg, int64_t nwaves, bool accumulate) {
+                        Tensor ws, Tensor dg, c10::optional<Tensor> dxsum, int64_t nwaves, bool accumulate) {
   const int D = (int)x.size(-1), M = (int)(x.numel() / D);
-  TORCH_CHECK(ws.numel() >= (2 * (nwaves / 4) + 128) * D, "rmsnorm_bwd workspace too small");
+  const int nz = 1 + (dxsum.has_value() ? 1 : 0);
+  TORCH_CHECK(ws.numel() >= nz * (nwaves / 4 + 64) * D, "rmsnorm_bwd workspace too small");
+  if (dxsum.has_value()) TORCH_CHECK(dxsum->numel() >= D && dxsum->scalar_type() == at::kFloat, "dxsum: fp32 [D]");
   check_rc(rtdc_rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), rstd.data_ptr<float>(), ptr_or_null(dres),
-                            dx.data_ptr(), ws.data_ptr<float>(), dg.data_ptr<float>(), M, D, (int)nwaves,
-                            accumulate, cur_stream()),
+                            dx.data_ptr(), ws.data_ptr<float>(), dg.data_ptr<float>(), (float*)ptr_or_null(dxsum), M,
+                            D, (int)nwaves, accumulate, cur_stream()),
            "rmsnorm_bwd");
 }
 static void colsum(Tensor X, int64_t M, int64_t N, int64_t ld, Tensor ws, int64_t nblk, Tensor out,

@@ -35,6 +35,12 @@ struct GemmArgs {
   // per row-tile t and column n: mean and M2 over the tile's rows -> [tiles_m][N] each
   float* stats_mean;
   float* stats_m2;
+  // optional column sums of the bf16 output C (bias gradient of the next layer down):
+  // cs_out [N] (overwritten), cs_ws >= (tiles_m * 4 + 64) * N floats of scratch.  Fused into
+  // the 8-wave kernels' gelu-backward epilogue, a separate reduction otherwise.
+  float* cs_out;
+  float* cs_ws;
+  long long cs_ws_elems;
 };
 
 // fp32 MFMA GEMM (gemm_f32.hip)

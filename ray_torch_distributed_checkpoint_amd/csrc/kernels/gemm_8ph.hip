@@ -158,6 +158,17 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
       unpack8bf(buf_load16(rBias, n < a.N ? (uint32_t)n * 2u : BUF_OOB), bb[c]);
     }
   }
+  // column sums of the gelu-backward output (the c_fc bias gradient): per lane over its pairs,
+  // then over the 16 lanes of a row group, one partial row per (row tile, wave row) in cs_ws
+  constexpr bool CSUM = ACT == 3;
+  const bool do_cs = CSUM && a.cs_ws != nullptr;
+  float cs[CSUM ? TNQ : 1][8];
+  if constexpr (CSUM) {
+#pragma unroll
+    for (int c = 0; c < TNQ; ++c)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) cs[c][r] = 0.f;
+  }
   u32x4 xin[NP];
   const bool load_in = ACT_IN || has_cin;
 #pragma unroll
@@ -202,11 +213,38 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
     } else if constexpr (ACT == 3) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] *= gelu_tanh_grad(x[r]);
+      if (do_cs && off != BUF_OOB) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cs[c][r] += v[r];
+      }
     } else if constexpr (ACT == 4) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = x[r] > 0.f ? v[r] : 0.f;
     }
     buf_store16(rC, off, pack8bf(v));
+  }
+  if constexpr (CSUM) {
+    if (do_cs) {
+      constexpr int WA = 128 / SA;
+      float* dst = a.cs_ws + (long long)((m0 / 256) * WA + wa) * a.N;
+#pragma unroll
+      for (int c = 0; c < TNQ; ++c) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          float t = cs[c][r];
+          t += __shfl_xor(t, 1);
+          t += __shfl_xor(t, 2);
+          t += __shfl_xor(t, 4);
+          t += __shfl_xor(t, 8);
+          cs[c][r] = t;
+        }
+        const int n = nrun + cno(c);
+        if ((lane & 15) == 0 && n < a.N) {
+          *(f32x4*)(dst + n) = f32x4{cs[c][0], cs[c][1], cs[c][2], cs[c][3]};
+          *(f32x4*)(dst + n + 4) = f32x4{cs[c][4], cs[c][5], cs[c][6], cs[c][7]};
+        }
+      }
+    }
   }
 }
 

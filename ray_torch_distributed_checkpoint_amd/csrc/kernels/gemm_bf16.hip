@@ -391,6 +391,10 @@ static int pick_cfg(const GemmArgs& a, int batch, bool a_kmajor, bool b_kmajor) 
   return 0;
 }
 
+extern "C" int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out, int accumulate,
+                           int is_bf16, hipStream_t st);
+extern "C" int rtdc_colsum_rows(const float* ws, int W, int D, float* tmp, float* out, int accumulate,
+                                hipStream_t st);
 extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
                                  hipStream_t st);
 extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
@@ -487,6 +491,22 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws,
                          a.splitk, a.M, a.N, (bf16_t*)a.C, (const bf16_t*)a.Cin, a.ldc, a.beta);
+  }
+  if (a.cs_out) {
+    // column sums of C: the 8-wave gelu-backward epilogue left one partial row per (row tile,
+    // wave row) in cs_ws; anything else reduces C itself
+    const int tiles_m = (a.M + 255) / 256;
+    if (big && a.act == 3 && !out_fp32) {
+      const int W = tiles_m * (bn == 256 ? 2 : 4);
+      if ((long long)(W + 64) * a.N > a.cs_ws_elems) return 1;
+      const int rc = rtdc_colsum_rows(a.cs_ws, W, a.N, a.cs_ws + (long long)W * a.N, a.cs_out, 0, stream);
+      if (rc) return rc;
+    } else {
+      const int nblk = a.M / 64 < 1 ? 1 : (a.M / 64 > 256 ? 256 : a.M / 64);
+      if ((long long)(nblk + 64) * a.N > a.cs_ws_elems) return 1;
+      const int rc = rtdc_colsum(a.C, a.M, a.N, a.ldc, a.cs_ws, nblk, a.cs_out, 0, out_fp32 ? 0 : 1, stream);
+      if (rc) return rc;
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -86,21 +86,29 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
 
 // dxhat = dy*g ; dx = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat*xhat))   (LayerNorm)
 // dx = rstd * (dxhat - xhat * mean(dxhat*xhat))                                  (RMSNorm)
-template <int CPL, bool RMS>
+// CS: also the column sums of dx itself (the residual-stream gradient this kernel produces is
+// the output gradient of the block's residual projection, whose bias gradient is exactly that
+// colsum - computed here on the way out instead of re-reading dx in a separate reduction).
+// Partial rows per block: ws_dg [nblk][D], ws_db = ws_dg + nblk*D, ws_cs = ws_db + nblk*D.
+template <int CPL, bool RMS, bool CS>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ ws_dg,
-    float* __restrict__ ws_db, int M, int D) {
+    float* __restrict__ ws_db, float* __restrict__ ws_cs, int M, int D) {
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nw = gridDim.x * 4;
   const int nch = D >> 3;
-  float adg[CPL][8], adb[CPL][8];
+  float adg[CPL][8], adb[CPL][8], acs[CS ? CPL : 1][8];
 #pragma unroll
   for (int i = 0; i < CPL; ++i)
 #pragma unroll
     for (int e = 0; e < 8; ++e) adg[i][e] = adb[i][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < (CS ? CPL : 1); ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acs[i][e] = 0.f;
 
   float gg[CPL][8];
 #pragma unroll
@@ -163,13 +171,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
         for (int e = 0; e < 8; ++e) {
           o[e] = rstd * (dxh[i][e] - m1 - xh[i][e] * m2);
           if (dres) o[e] += r[e];
+          if constexpr (CS) acs[i][e] += o[e];
         }
         st8(dxr + c * 8, o);
       }
     }
   }
   // combine the block's 4 waves in LDS (fixed wave order), one partial row per block
-  extern __shared__ float red[];  // [D] dgamma (+ [D] dbeta)
+  extern __shared__ float red[];  // [D] dgamma (+ [D] dbeta) (+ [D] colsum(dx))
+  constexpr int KCS = RMS ? 1 : 2;
   const int wv = threadIdx.x >> 6;
   for (int w = 0; w < 4; ++w) {
     if (wv == w) {
@@ -181,6 +191,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
           for (int e = 0; e < 8; ++e) {
             red[c * 8 + e] = w ? red[c * 8 + e] + adg[i][e] : adg[i][e];
             if (!RMS) red[D + c * 8 + e] = w ? red[D + c * 8 + e] + adb[i][e] : adb[i][e];
+            if constexpr (CS) red[KCS * D + c * 8 + e] = w ? red[KCS * D + c * 8 + e] + acs[i][e] : acs[i][e];
           }
         }
       }
@@ -190,6 +201,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   for (int d = threadIdx.x; d < D; d += 256) {
     ws_dg[(long long)blockIdx.x * D + d] = red[d];
     if (!RMS) ws_db[(long long)blockIdx.x * D + d] = red[D + d];
+    if constexpr (CS) ws_cs[(long long)blockIdx.x * D + d] = red[KCS * D + d];
   }
 }
 
@@ -200,13 +212,17 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
 // [y*R, (y+1)*R) of 64 columns; 4 waves stride the rows, combined in LDS in fixed order.
 // Run twice (W -> S -> 1) so every thread keeps only a few independent loads in flight and
 // the reduction order is fixed (deterministic).
-__global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict__ ws, float* __restrict__ out,
-                                                       int W, int D, int R, int accumulate, long long ws_z,
-                                                       long long out_z) {
+struct OutPtrs {
+  float* p[4];
+};
+// out: tmp + z * out_z when tmp is set (first of two stages), else outs.p[z]
+__global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict__ ws, float* __restrict__ tmp,
+                                                       OutPtrs outs, int W, int D, int R, int accumulate,
+                                                       long long ws_z, long long out_z) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   ws += blockIdx.z * ws_z;  // z = independent reductions batched into one launch
-  out += blockIdx.z * out_z;
+  float* out = tmp ? tmp + blockIdx.z * out_z : outs.p[blockIdx.z];
   const int d = blockIdx.x * 64 + lane;
   const int r0 = blockIdx.y * R, r1 = min(W, r0 + R);
   float s0 = 0.f, s1 = 0.f;
@@ -227,23 +243,24 @@ __global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict_
   }
 }
 
-// nz independent reductions ws + z*ws_z [W][D] (W partial rows) -> out + z*out_z [D];
+// nz <= 4 independent reductions ws + z*ws_z [W][D] (W partial rows) -> outs.p[z] [D];
 // tmp holds nz x S intermediate rows (nz * 64 * D floats).
-static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, float* out, int accumulate, hipStream_t st,
-                             int nz = 1, long long ws_z = 0, long long out_z = 0) {
+static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, OutPtrs outs, int accumulate,
+                             hipStream_t st, int nz = 1, long long ws_z = 0) {
   int S = W / 32;
   S = S < 1 ? 1 : (S > 64 ? 64 : S);
   if (S > 1 && tmp) {
     const int R = (W + S - 1) / S;
-    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, S, nz), dim3(256), 0, st, ws, tmp, W, D, R, 0, ws_z,
-                       64LL * D);
-    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1, nz), dim3(256), 0, st, (const float*)tmp, out, S, D, S,
-                       accumulate, 64LL * D, out_z);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, S, nz), dim3(256), 0, st, ws, tmp, outs, W, D, R, 0,
+                       ws_z, 64LL * D);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1, nz), dim3(256), 0, st, (const float*)tmp,
+                       (float*)nullptr, outs, S, D, S, accumulate, 64LL * D, 0LL);
   } else {
-    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1, nz), dim3(256), 0, st, ws, out, W, D, W, accumulate,
-                       ws_z, out_z);
+    hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, 1, nz), dim3(256), 0, st, ws, (float*)nullptr, outs, W,
+                       D, W, accumulate, ws_z, 0LL);
   }
 }
+static OutPtrs outs1(float* a, float* b = nullptr, float* c = nullptr) { return OutPtrs{{a, b, c, nullptr}}; }
 
 // Column sums of a [M][N] matrix (bias gradient), stage 1: block (x, y) reduces rows
 // [x*R, (x+1)*R) of columns [y*512, y*512+512): lane = 8 columns (16-B loads for bf16), the 4
@@ -313,32 +330,47 @@ static int launch_norm_fwd(const void* x, const void* g, const void* b, void* y,
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// ws layout: [nz][nblk][D] partials (dgamma | dbeta | colsum(dx)) | nz x [64][D] level-2 rows,
+// nz = (RMS ? 1 : 2) + (dxsum != nullptr).  dxsum is always written (never accumulated).
 template <bool RMS>
 static int launch_norm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                            const float* rstd, const void* dres, void* dx, float* ws, float* dg,
-                           float* db, int M, int D, int nwaves, int accumulate, hipStream_t st) {
+                           float* db, float* dxsum, int M, int D, int nwaves, int accumulate, hipStream_t st) {
   if (D % 8 != 0 || nwaves % 4 != 0) return 1;
   const int cpl = (D / 8 + 63) / 64;
   const int nblk = nwaves / 4;
+  const bool cs = dxsum != nullptr;
+  const int nz = (RMS ? 1 : 2) + (cs ? 1 : 0);
   dim3 grid(nblk), block(256);
-  // ws layout: [nblk][D] dgamma partials | [nblk][D] dbeta partials | 2 x [64][D] level-2 rows
+  const long long part = (long long)nblk * D;
   float* ws_dg = ws;
-  float* ws_db = ws + (long long)nblk * D;
-  float* tmp = ws + 2LL * nblk * D;
-  const size_t lds = (RMS ? 1 : 2) * (size_t)D * sizeof(float);
+  float* ws_db = ws + part;
+  float* ws_cs = ws + (RMS ? 1 : 2) * part;
+  float* tmp = ws + nz * part;
+  const size_t lds = (size_t)nz * D * sizeof(float);
   if (lds > 160 * 1024) return 1;
-#define L(C)                                                                                  \
-  hipLaunchKernelGGL((norm_bwd_kernel<C, RMS>), grid, block, lds, st, (const bf16_t*)dy,       \
+#define L(C, CS)                                                                              \
+  hipLaunchKernelGGL((norm_bwd_kernel<C, RMS, CS>), grid, block, lds, st, (const bf16_t*)dy,   \
                      (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \
-                     (bf16_t*)dx, ws_dg, ws_db, M, D)
-  if (cpl <= 1) L(1);
-  else if (cpl <= 2) L(2);
-  else if (cpl <= 4) L(4);
-  else if (cpl <= 8) L(8);
+                     (bf16_t*)dx, ws_dg, ws_db, ws_cs, M, D)
+#define LC(C) \
+  if (cs) L(C, true); else L(C, false)
+  if (cpl <= 1) { LC(1); }
+  else if (cpl <= 2) { LC(2); }
+  else if (cpl <= 4) { LC(4); }
+  else if (cpl <= 8) { LC(8); }
   else return 1;
+#undef LC
 #undef L
-  if (RMS) colsum_ws_reduce(ws_dg, nblk, D, tmp, dg, accumulate, st);
-  else colsum_ws_reduce(ws_dg, nblk, D, tmp, dg, accumulate, st, 2, (long long)nblk * D, ((long long)(uintptr_t)db - (long long)(uintptr_t)dg) / (long long)sizeof(float));
+  // one reduction launch pair for all of them; the colsum of dx is never accumulated, so it
+  // gets its own pair when dgamma/dbeta accumulate
+  if (!cs || !accumulate) {
+    OutPtrs o = RMS ? outs1(dg, cs ? dxsum : nullptr) : outs1(dg, db, cs ? dxsum : nullptr);
+    colsum_ws_reduce(ws, nblk, D, tmp, o, accumulate, st, nz, part);
+  } else {
+    colsum_ws_reduce(ws, nblk, D, tmp, RMS ? outs1(dg) : outs1(dg, db), accumulate, st, nz - 1, part);
+    colsum_ws_reduce(ws_cs, nblk, D, tmp, outs1(dxsum), 0, st, 1, part);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -352,16 +384,22 @@ extern "C" int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rs
 }
 extern "C" int rtdc_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                                   const float* rstd, const void* dres, void* dx, float* ws,
-                                  float* dg, float* db, int M, int D, int nwaves, int accumulate,
-                                  hipStream_t st) {
-  return launch_norm_bwd<false>(dy, x, g, mean, rstd, dres, dx, ws, dg, db, M, D, nwaves,
+                                  float* dg, float* db, float* dxsum, int M, int D, int nwaves,
+                                  int accumulate, hipStream_t st) {
+  return launch_norm_bwd<false>(dy, x, g, mean, rstd, dres, dx, ws, dg, db, dxsum, M, D, nwaves,
                                 accumulate, st);
 }
 extern "C" int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, const float* rstd,
-                                const void* dres, void* dx, float* ws, float* dg, int M, int D,
-                                int nwaves, int accumulate, hipStream_t st) {
-  return launch_norm_bwd<true>(dy, x, g, nullptr, rstd, dres, dx, ws, dg, nullptr, M, D, nwaves,
+                                const void* dres, void* dx, float* ws, float* dg, float* dxsum, int M,
+                                int D, int nwaves, int accumulate, hipStream_t st) {
+  return launch_norm_bwd<true>(dy, x, g, nullptr, rstd, dres, dx, ws, dg, nullptr, dxsum, M, D, nwaves,
                                accumulate, st);
+}
+// out[D] (+)= sum of W partial rows ws[W][D] (tmp: 64 * D floats of scratch)
+extern "C" int rtdc_colsum_rows(const float* ws, int W, int D, float* tmp, float* out, int accumulate,
+                                hipStream_t st) {
+  colsum_ws_reduce(ws, W, D, tmp, outs1(out), accumulate, st);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 extern "C" int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out,
                            int accumulate, int is_bf16, hipStream_t st) {
@@ -376,6 +414,6 @@ extern "C" int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int n
     if (vec) CS(float, true); else CS(float, false);
   }
 #undef CS
-  colsum_ws_reduce(ws, nblk, N, ws + (long long)nblk * N, out, accumulate, st);
+  colsum_ws_reduce(ws, nblk, N, ws + (long long)nblk * N, outs1(out), accumulate, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -83,12 +83,14 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd, cfg.layer_norm_eps)
         self.mlp = MLP(cfg)
 
-    def forward(self, x):
+    def forward(self, x, prev_bias=None):
         # the residual stream passes through each LayerNorm so its gradient is summed inside
-        # the norm's backward kernel (no separate add of the two branches' gradients)
-        h, x = self.ln_1(x, passthrough=True)
+        # the norm's backward kernel (no separate add of the two branches' gradients); that
+        # kernel also reduces the bias gradient of the projection that wrote the stream
+        # (prev_bias: the previous block's MLP c_proj, then this block's attention c_proj)
+        h, x = self.ln_1(x, passthrough=True, grad_sum_into=prev_bias)
         x = self.attn(h, residual=x)
-        h, x = self.ln_2(x, passthrough=True)
+        h, x = self.ln_2(x, passthrough=True, grad_sum_into=self.attn.c_proj.bias)
         return self.mlp(h, residual=x)
 
 
@@ -123,9 +125,11 @@ class GPT2(nn.Module):
 
     def forward(self, idx: torch.Tensor, targets: torch.Tensor | None = None):
         x = ops.embedding(idx, self.wte, self.wpe)
+        prev_bias = None
         for blk in self.h:
-            x = blk(x)
-        x = self.ln_f(x)
+            x = blk(x, prev_bias)
+            prev_bias = blk.mlp.c_proj.bias
+        x = self.ln_f(x, grad_sum_into=prev_bias)
         if targets is not None:
             return ops.lm_head_cross_entropy(x, self.wte, targets, self.cfg.vocab_size)
         logits = ops.linear(x, self.wte)

@@ -64,10 +64,12 @@ class LayerNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(dim))
         self.bias = nn.Parameter(torch.zeros(dim))
 
-    def forward(self, x, passthrough: bool = False):
+    def forward(self, x, passthrough: bool = False, grad_sum_into=None):
         """passthrough=True -> (LN(x), x): use the second output as the residual so its
-        gradient is folded into the norm's backward kernel."""
-        return ops.layer_norm(x, self.weight, self.bias, self.eps, passthrough=passthrough)
+        gradient is folded into the norm's backward kernel.  grad_sum_into: bias of the
+        projection that produced x, whose gradient the backward kernel then reduces."""
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, passthrough=passthrough,
+                              grad_sum_into=grad_sum_into)
 
 
 class RMSNorm(nn.Module):

@@ -7,6 +7,8 @@ MFMA path used by fp32 models (the reference toy MLP, R/my_ray_module.py:94-112)
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from ._ext import gpu_ext
@@ -32,15 +34,20 @@ def workspace(device, numel: int, tag: str = "ws") -> torch.Tensor:
 
 def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, Cin=None, bias=None,
               aux_in=None, aux_out=None, alpha=1.0, beta=0.0, act=ACT_NONE, causal=CAUSAL_NONE,
-              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0), tile_cfg=-1, alpha_dev=None):
+              batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0), tile_cfg=-1, alpha_dev=None, colsum_out=None):
+    """colsum_out (fp32 [N]): also the column sums of C (fused into the gelu-backward epilogue
+    of the 8-wave kernels, a separate reduction otherwise)."""
     sA0, sA1, sB0, sB1, sC0, sC1 = strides
     ws = None
     if act == ACT_NONE and bias is None and causal == CAUSAL_NONE and batch == 1 and M * N <= SPLITK_MAX_OUT:
         # split-K slabs for long-K / small-output GEMMs (weight gradients); the launcher decides
         ws = workspace(C.device, min(16 * M * N, SPLITK_WS_ELEMS), "splitk")
+    cs_ws = None
+    if colsum_out is not None:
+        cs_ws = workspace(C.device, (max(4 * ((M + 255) // 256), _COLSUM_BLOCKS) + 64) * N, "colsum_gemm")
     gpu_ext().gemm_bf16(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
                         batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act, causal,
-                        ws, tile_cfg, alpha_dev)
+                        ws, tile_cfg, alpha_dev, colsum_out, cs_ws)
     return C
 
 
@@ -55,12 +62,16 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     return y
 
 
-def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None):
-    """dx[M,K] = alpha (* alpha_dev[0]) * dy[M,N] @ w[N,K]  (optionally * act'(aux_in))."""
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None,
+                 colsum_out=None):
+    """dx[M,K] = alpha (* alpha_dev[0]) * dy[M,N] @ w[N,K]  (optionally * act'(aux_in)).
+    colsum_out (fp32 [K]): also sum_m dx[m, :] (the bias gradient of the layer that produced
+    the activation), reduced by the GEMM epilogue instead of a second pass over dx."""
     M, N = dy.shape
     K = w.shape[1]
     dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
-    gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev)
+    gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev,
+              colsum_out=colsum_out)
     return dx
 
 
@@ -75,9 +86,41 @@ def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False
     return out
 
 
+# Column sums that a gradient's producer computed on the way out (LayerNorm backward: the
+# residual-stream gradient), keyed by the gradient tensor itself: (weakref, data_ptr, numel,
+# last dim, version counter, sums).  colsum() of the same tensor takes them instead of
+# re-reading it.  Entries whose tensor is gone are dropped on every offer.
+_offered: list = []
+
+
+def offer_colsum(t: torch.Tensor, sums: torch.Tensor) -> None:
+    _offered[:] = [e for e in _offered if e[0]() is not None][-7:]
+    _offered.append((weakref.ref(t), t.data_ptr(), t.numel(), t.shape[-1], t._version, sums))
+
+
+def _take_colsum(x2d: torch.Tensor):
+    for k, (ref, ptr, numel, last, ver, sums) in enumerate(_offered):
+        t = ref()
+        if (t is not None and ptr == x2d.data_ptr() and numel == x2d.numel() and last == x2d.shape[-1]
+                and x2d.is_contiguous() and t._version == ver):
+            del _offered[k]
+            return sums
+    return None
+
+
 def colsum(x2d: torch.Tensor, out=None, accumulate=False):
-    """fp32 column sums of a [M,N] matrix (bias gradient), deterministic two-stage reduce."""
+    """fp32 column sums of a [M,N] matrix (bias gradient), deterministic two-stage reduce (or
+    the sums the matrix's producer already offered, see offer_colsum)."""
     M, N = x2d.shape
+    sums = _take_colsum(x2d)
+    if sums is not None:
+        if out is None:
+            return sums
+        if accumulate:
+            out.add_(sums)
+        elif out.data_ptr() != sums.data_ptr():
+            out.copy_(sums)
+        return out
     if out is None:
         out = torch.empty((N,), dtype=torch.float32, device=x2d.device)
     nblk = min(_COLSUM_BLOCKS, max(1, M // 64))

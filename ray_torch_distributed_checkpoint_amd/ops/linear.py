@@ -145,9 +145,12 @@ class _FusedMLP(torch.autograd.Function):
         w_fc, b_fc, w_proj, b_proj = ctx.params
         dw_proj = G.linear_wgrad(dy2, g, out=grad_target(w_proj))
         db_proj = G.colsum(dy2, out=grad_target(b_proj))
-        dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_GELU_BWD, aux_in=pre)
+        # c_fc's bias gradient = column sums of dpre, reduced in the dgrad GEMM's epilogue
+        db_fc = grad_target(b_fc)
+        if db_fc is None and b_fc is not None:
+            db_fc = torch.empty(b_fc.shape, dtype=torch.float32, device=dy2.device)
+        dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_GELU_BWD, aux_in=pre, colsum_out=db_fc)
         dw_fc = G.linear_wgrad(dpre, x2, out=grad_target(w_fc))
-        db_fc = G.colsum(dpre, out=grad_target(b_fc))
         dx = G.linear_dgrad(dpre, wfs).view(ctx.in_shape)
         return dx, dw_fc, db_fc, dw_proj, db_proj, (dy if ctx.has_res else None)
 

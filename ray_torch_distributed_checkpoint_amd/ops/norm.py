@@ -16,8 +16,9 @@ def _bwd_waves(M: int) -> int:
     return max(4, min(4096, (M + 3) // 4 * 4))
 
 
-def _bwd_ws_elems(nw: int, D: int) -> int:
-    return (2 * (nw // 4) + 2 * 64) * D
+def _bwd_ws_elems(nw: int, D: int, nz: int = 3) -> int:
+    # nz reductions (dgamma, dbeta, colsum(dx)): [nz][nw/4][D] partials + nz x [64][D] rows
+    return nz * (nw // 4 + 64) * D
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -26,7 +27,7 @@ class _LayerNorm(torch.autograd.Function):
     (dres) instead of by a separate autograd add."""
 
     @staticmethod
-    def forward(ctx, x, w, b, eps, passthrough=False):
+    def forward(ctx, x, w, b, eps, passthrough=False, sum_param=None):
         ctx.set_materialize_grads(False)
         D = x.shape[-1]
         xc = x.contiguous()
@@ -38,6 +39,7 @@ class _LayerNorm(torch.autograd.Function):
         gpu_ext().layernorm_fwd(xc, ws, bs, y, mean, rstd, eps)
         ctx.save_for_backward(xc, ws, mean, rstd)
         ctx.params = (w, b)
+        ctx.sum_param = sum_param
         return (y, xc) if passthrough else y
 
     @staticmethod
@@ -57,8 +59,20 @@ class _LayerNorm(torch.autograd.Function):
             dg = dgb[0] if dg is None else dg
             db = dgb[1] if db is None else db
         dres = dpass.contiguous() if dpass is not None else None
-        gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, dres, dx, wsp, dg, db, nw, False)
-        return dx, dg, db, None, None
+        # dx is the residual-stream gradient: its column sums are the bias gradient of the
+        # residual projection that produced x (sum_param: attention / MLP c_proj bias).  They
+        # are reduced by this kernel on the way out - straight into that bias's slot of the
+        # flat gradient buffer when it has one - and offered to the projection's colsum(),
+        # which then returns them as the bias gradient without touching dx again.
+        dxsum = None
+        if ctx.sum_param is not None:
+            dxsum = grad_target(ctx.sum_param)
+            if dxsum is None:
+                dxsum = torch.empty(D, dtype=torch.float32, device=xc.device)
+        gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, dres, dx, wsp, dg, db, dxsum, nw, False)
+        if dxsum is not None:
+            G.offer_colsum(dx, dxsum)
+        return dx, dg, db, None, None, None
 
 
 class _RMSNorm(torch.autograd.Function):
@@ -90,17 +104,18 @@ class _RMSNorm(torch.autograd.Function):
         if dg is None:
             dg = torch.empty(D, dtype=torch.float32, device=xc.device)
         dres = dpass.contiguous() if dpass is not None else None
-        gpu_ext().rmsnorm_bwd(dy.contiguous(), xc, ws, rstd, dres, dx, wsp, dg, nw, False)
+        gpu_ext().rmsnorm_bwd(dy.contiguous(), xc, ws, rstd, dres, dx, wsp, dg, None, nw, False)
         return dx, dg, None, None
 
 
-def layer_norm(x, w, b, eps=1e-5, passthrough=False):
+def layer_norm(x, w, b, eps=1e-5, passthrough=False, grad_sum_into=None):
     """LayerNorm over the last axis; passthrough=True returns (y, x) with the residual-stream
-    gradient fused into the backward kernel."""
+    gradient fused into the backward kernel.  grad_sum_into: the bias of the projection that
+    produced x; its gradient (= column sums of dx) is then reduced by the backward kernel."""
     if not x.is_cuda or x.dtype != torch.bfloat16:
         y = F.layer_norm(x, (x.shape[-1],), w.to(x.dtype), b.to(x.dtype), eps)
         return (y, x) if passthrough else y
-    return _LayerNorm.apply(x, w, b, eps, passthrough)
+    return _LayerNorm.apply(x, w, b, eps, passthrough, grad_sum_into)
 
 
 def rms_norm(x, w, eps=1e-5, passthrough=False):

@@ -87,6 +87,28 @@ def test_gemm_bf16_epilogues():
     _close(Cb, base * gd, 1e-4)
 
 
+@pytest.mark.parametrize("cfg", [-1, 6, 7])
+def test_gemm_gelu_bwd_colsum(cfg):
+    """dpre = (dy @ W) * gelu'(pre) with the column sums of dpre (the c_fc bias gradient)
+    reduced by the 8-wave epilogue (cfg 6 / 7: 256x256 / 256x192 tiles; rows past M and a
+    partial last row tile excluded) or by the fallback reduction (cfg -1 picks the 4-wave
+    kernel at this size)."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(11)
+    M, N, K = 1000, 256, 768  # dx[M, K] = dy[M, N] @ w[N, K]
+    dy, w, pre = _bf(M, N), _bf(N, K, scale=0.1), _bf(M, K)
+    out = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    cs = torch.full((K,), float("nan"), device=DEV)
+    G.gemm_bf16(dy, w, out, M, K, N, N, K, K, True, False, aux_in=pre, act=G.ACT_GELU_BWD, tile_cfg=cfg,
+                colsum_out=cs)
+    hf = pre.float().requires_grad_(True)
+    (gd,) = torch.autograd.grad(F.gelu(hf, approximate="tanh").sum(), hf)
+    ref = (dy.float() @ w.float()) * gd
+    _close(out, ref, 1e-2)
+    _close(cs, ref.sum(0), 5e-3)
+
+
 def test_gemm_bf16_batched_strided():
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
 
@@ -218,7 +240,39 @@ def test_layernorm_rmsnorm():
         _close(w.grad, wr2.grad, 1e-3)
 
 
-@pytest.mark.parametrize("dtype,V,ld", [(torch.float32, 10, 10), (torch.bfloat16, 1000, 1024), (torch.float32, 333, 333)])
+def test_layernorm_bwd_offers_dx_colsum():
+    """LayerNorm backward also reduces the column sums of the residual-stream gradient it
+    writes (passthrough form, dres added); colsum() of that gradient takes them (no second
+    reduction) and they match a plain fp32 sum, also when accumulating into a bias grad."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+    from ray_torch_distributed_checkpoint_amd.ops import layer_norm
+
+    torch.manual_seed(8)
+    M, D = 4096, 768
+    x = _bf(M, D, scale=2.0).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    producer_bias = torch.zeros(D, device=DEV, requires_grad=True)  # the projection that wrote x
+    y, xp = layer_norm(x, w, b, passthrough=True, grad_sum_into=producer_bias)
+    dres = _bf(M, D)
+    torch.autograd.backward([y, xp], [_bf(M, D), dres])
+    dx = x.grad
+    assert len(G._offered) > 0
+    ref = dx.float().sum(0)
+    got = G.colsum(dx.view(M, D))
+    _close(got, ref, 5e-3)  # fp32 sums of the unrounded dx vs the bf16 dx
+    assert G._take_colsum(dx.view(M, D)) is None  # taken once
+    acc = torch.ones(D, device=DEV)
+    G.offer_colsum(dx, got.clone())
+    G.colsum(dx.view(M, D), out=acc, accumulate=True)
+    _close(acc, ref + 1, 5e-3)
+    # a tensor modified in place after the offer is reduced again, not served stale sums
+    G.offer_colsum(dx, got.clone())
+    dx.mul_(2)
+    _close(G.colsum(dx.view(M, D)), 2 * ref, 1e-3)
+
+
+@pytest.mark.parametrize("dtype,V,ld",[(torch.float32, 10, 10), (torch.bfloat16, 1000, 1024), (torch.float32, 333, 333)])
 def test_cross_entropy(dtype, V, ld):
     from ray_torch_distributed_checkpoint_amd.ops import cross_entropy, xent_metrics
 
