@@ -217,7 +217,14 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
   f32x4 o[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  // row sums of P on the matrix core: an all-ones A operand makes every row of the P.V-shaped
+  // product the sum over the keys, so lacc[*] = l for the lane's query row (no VALU adds, no
+  // cross-lane reduction at the end; the sum is over the same bf16 P the numerator uses)
+  f32x4 lacc = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
+  float m = -INFINITY;
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int cur = kb % NS;
@@ -253,24 +260,27 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
       }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx * c);
-    const float alpha = fexp2(m - mn);
-    m = mn;
-    float ps = 0.f;
+    // lazy rescale: the running max moves (and O, l are rescaled) only when some row of the
+    // wave would otherwise see probabilities above 2^8 - after the first key blocks the max
+    // rarely grows that much, so the 4*DT+4 multiplies and the exp are skipped (wave-uniform)
+    if (__any(mx * c > m + 8.f)) {
+      const float mn = fmaxf(m, mx * c);
+      const float alpha = fexp2(m - mn);
+      m = mn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lacc[r] *= alpha;
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[d][r] *= alpha;
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = fexp2(fmaf(s[t][r], c, -mn));
-        s[t][r] = p;
-        ps += p;
-      }
-    l = l * alpha + ps;
-#pragma unroll
-    for (int d = 0; d < DT; ++d)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[d][r] *= alpha;
+      for (int r = 0; r < 4; ++r) s[t][r] = fexp2(fmaf(s[t][r], c, -m));
     const bf16x8 p0 = pack_pair(s[0], s[1]), p1 = pack_pair(s[2], s[3]);
+    lacc = mfma(ones, p0, lacc);
+    lacc = mfma(ones, p1, lacc);
 #pragma unroll
     for (int d0 = 0; d0 < DT; d0 += DB) {
       TrPair vq[DB][2];
@@ -292,8 +302,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
   }
 #undef KT
 #undef VT
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  const float l = lacc[0];
   const float inv = 1.f / l;
   bf16_t* orow = a.out + ((long long)b * a.T + myq) * C + h * DH;
 #pragma unroll

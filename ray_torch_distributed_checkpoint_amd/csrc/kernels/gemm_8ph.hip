@@ -284,6 +284,12 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& a, f32x4 (&acc)[2]
   }
 }
 
+// Timing-only builds (results are wrong; never shipped): bit 1 drops the main loop's vmcnt
+// waits, bit 2 reads LDS fragments in the first K-tile only, bit 4 drops the loop barriers.
+#ifndef RTDC_G8_DIAG
+#define RTDC_G8_DIAG 0
+#endif
+
 // outstanding glds instructions allowed (wave-uniform): counted waits are immediates
 __device__ __forceinline__ void wait_vm(int allowed) {
   if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -374,14 +380,15 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
       // after the lgkmcnt wait below)
       typename Frag<AK>::T ra[TMQ][2];
       typename Frag<BKM>::T rb[TNQ][2];
-      if (p == 1 || p == 3) {
+      const bool rd = !(RTDC_G8_DIAG & 2) || t == 0;
+      if ((p == 1 || p == 3) && rd) {
         const char* ah = buf + (p == 1 ? 0 : HALF);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(ah, SA * wa + 16 * i, ks, lane);
       }
-      if (p == 1 || p == 2) {
+      if ((p == 1 || p == 2) && rd) {
         const char* bh = buf + 2 * HALF + (p == 1 ? 0 : BHALF);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
@@ -395,20 +402,20 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
       const int e = p < 4 ? 4 * t + 4 + p : 4 * t + 8;
       issue(e);
       // 3. retire what the next phase reads (p3 -> p4 reads nothing new)
-      if (p != 3 && (p != 4 || t + 1 < nt)) {
+      if (p != 3 && (p != 4 || t + 1 < nt) && !(RTDC_G8_DIAG & 1)) {
         const int need = p == 1 ? 4 * t + 2 : (p == 2 ? 4 * t + 3 : 4 * t + 5);
         wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
       }
       asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if (!(RTDC_G8_DIAG & 4)) __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (p == 1 || p == 3) {
+      if ((p == 1 || p == 3) && rd) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int i = 0; i < TMQ; ++i) fa[i][ks] = fval(ra[i][ks]);
       }
-      if (p == 1 || p == 2) {
+      if ((p == 1 || p == 2) && rd) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -435,6 +442,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
     }
   }
 
+  if (RTDC_G8_DIAG) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   // ---- epilogue: lane holds C[m][n..n+3] of every (quadrant, i, j) fragment ----
   const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
   if (a.splitk > 1) {
