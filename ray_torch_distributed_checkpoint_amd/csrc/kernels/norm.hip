@@ -332,23 +332,48 @@ static int launch_norm_fwd(const void* x, const void* g, const void* b, void* y,
 
 // ws layout: [nz][nblk][D] partials (dgamma | dbeta | colsum(dx)) | nz x [64][D] level-2 rows,
 // nz = (RMS ? 1 : 2) + (dxsum != nullptr).  dxsum is always written (never accumulated).
+// resident 256-thread blocks of a norm_bwd_kernel variant on this device (cached per variant)
+template <int C, bool RMS, bool CS>
+static int resident_blocks(size_t lds) {
+  static int cus = 0, occ = 0;
+  static size_t occ_lds = ~(size_t)0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  if (lds != occ_lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, norm_bwd_kernel<C, RMS, CS>, 256, lds) != hipSuccess ||
+        occ <= 0)
+      occ = 1;
+    occ_lds = lds;
+  }
+  return cus * occ;
+}
+
 template <bool RMS>
 static int launch_norm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                            const float* rstd, const void* dres, void* dx, float* ws, float* dg,
                            float* db, float* dxsum, int M, int D, int nwaves, int accumulate, hipStream_t st) {
   if (D % 8 != 0 || nwaves % 4 != 0) return 1;
   const int cpl = (D / 8 + 63) / 64;
-  const int nblk = nwaves / 4;
   const bool cs = dxsum != nullptr;
   const int nz = (RMS ? 1 : 2) + (cs ? 1 : 0);
+  const size_t lds = (size_t)nz * D * sizeof(float);
+  if (lds > 160 * 1024) return 1;
+  // one wave of blocks: a grid past the resident block slots leaves a partial second wave
+  // (GPT-2: 1024 blocks on 768 slots ran 0.94 ms/step of LayerNorm backward, 768 blocks 0.67)
+#define RB(C) (cs ? resident_blocks<C, RMS, true>(lds) : resident_blocks<C, RMS, false>(lds))
+  const int slots = cpl <= 1 ? RB(1) : cpl <= 2 ? RB(2) : cpl <= 4 ? RB(4) : RB(8);
+#undef RB
+  const int nblk = nwaves / 4 < slots ? nwaves / 4 : slots;
   dim3 grid(nblk), block(256);
   const long long part = (long long)nblk * D;
   float* ws_dg = ws;
   float* ws_db = ws + part;
   float* ws_cs = ws + (RMS ? 1 : 2) * part;
   float* tmp = ws + nz * part;
-  const size_t lds = (size_t)nz * D * sizeof(float);
-  if (lds > 160 * 1024) return 1;
 #define L(C, CS)                                                                              \
   hipLaunchKernelGGL((norm_bwd_kernel<C, RMS, CS>), grid, block, lds, st, (const bf16_t*)dy,   \
                      (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \

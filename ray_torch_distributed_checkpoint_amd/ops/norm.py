@@ -1,6 +1,8 @@
 """LayerNorm / RMSNorm on the native wave64 row kernels (bf16 activations, fp32 master params)."""
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -10,10 +12,13 @@ from .gradbuf import grad_target
 from .shadow import shadow_of
 
 
+_BWD_WAVES = int(os.environ.get("RTDC_NORM_BWD_WAVES", "4096"))
+
+
 def _bwd_waves(M: int) -> int:
     # up to 4096 waves (4 blocks of 4 waves per CU) for latency hiding; the kernel combines
     # each block's 4 waves, so the partial workspace is (waves / 4) rows
-    return max(4, min(4096, (M + 3) // 4 * 4))
+    return max(4, min(_BWD_WAVES, (M + 3) // 4 * 4))
 
 
 def _bwd_ws_elems(nw: int, D: int, nz: int = 3) -> int:
