@@ -57,6 +57,11 @@ class GpuProfiler:
                 rec["power_w"] = pw.get("current_socket_power") or pw.get("average_socket_power")
             except Exception:
                 pass
+            try:
+                clk = smi.amdsmi_get_clock_info(h, smi.AmdSmiClkType.GFX)
+                rec["gfx_clock_mhz"] = clk.get("clk")
+            except Exception:
+                pass
             self.samples.append(rec)
 
     def _loop(self):
@@ -101,8 +106,10 @@ class GpuProfiler:
         for g, ss in by.items():
             busy = [x.get("gfx_busy_pct") for x in ss if isinstance(x.get("gfx_busy_pct"), (int, float))]
             vram = [x.get("vram_used_mb") for x in ss if isinstance(x.get("vram_used_mb"), (int, float))]
+            power = [x.get("power_w") for x in ss if isinstance(x.get("power_w"), (int, float))]
             out[f"gpu{g}"] = {"mean_busy_pct": sum(busy) / len(busy) if busy else None,
-                              "max_vram_used_mb": max(vram) if vram else None}
+                              "max_vram_used_mb": max(vram) if vram else None,
+                              "mean_power_w": sum(power) / len(power) if power else None}
         return out
 
     def card_components(self):
