@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-scope", default="full", choices=["full", "model"],
                     help="full = model + optimizer train state (default); model = weights only")
+    ap.add_argument("--ckpt-scope-fallback", action="store_true",
+                    help="if the full train state does not fit on disk, measure model scope (flagged)")
     ap.add_argument("--overlap-steps", type=int, default=5)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (multi-rank rehearsal on 1 GPU)")
     args = ap.parse_args()
@@ -248,12 +250,19 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
         return 0
 
     # the box's scratch disk bounds what one rank can write (Llama-3-8B full train state is
-    # 96 GB on one GPU, 12 GB per rank at 8): fall back to the model shard if it does not fit
+    # 96 GB on one GPU, 12 GB per rank at 8).  The scope is never reduced silently: a state
+    # that does not fit is reported as unmeasured (or, with --ckpt-scope-fallback, measured at
+    # model scope and flagged as downgraded).
     free = shutil.disk_usage(base).free
+    downgraded = False
     if scope == "full" and nbytes_of(state()) / max(world, 1) * 1.15 > free:
-        scope = "model"
+        if not args.ckpt_scope_fallback:
+            return {"ckpt_unmeasured": f"full train state ({nbytes_of(state()) / 1e9:.1f} GB) larger than free "
+                                       f"disk ({free / 1e9:.0f} GB) at {base}; pass --ckpt-scope-fallback for a "
+                                       f"model-only measurement"}
+        scope, downgraded = "model", True
     if nbytes_of(state()) / max(world, 1) * 1.15 > free:
-        return {"ckpt_skipped": f"state larger than free disk ({free / 1e9:.0f} GB)"}
+        return {"ckpt_unmeasured": f"state larger than free disk ({free / 1e9:.0f} GB)"}
 
     # ---- async save overlapped with training steps
     torch.cuda.synchronize()
@@ -287,38 +296,87 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     t2 = time.perf_counter()
     dcp.save(state(), path2)
     t_sync = time.perf_counter() - t2
-    # ---- restore into the live model + optimizer
-    torch.cuda.synchronize()
+    # ---- restore into the live model + optimizer: first warm (shards still in the page cache
+    # right after the write), then cold (every shard dropped from the page cache with
+    # posix_fadvise(DONTNEED) after its fsync, so the bytes come from the device)
+    def restore():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t3 = time.perf_counter()
+        sd = state()
+        dcp.load(sd, path2)
+        set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t3
+
+    t_restore_warm = restore()
+    dropped = drop_page_cache(path2)
     if world > 1:
         dist.barrier()
-    t3 = time.perf_counter()
-    sd = state()
-    dcp.load(sd, path2)
-    set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t_restore = time.perf_counter() - t3
-    vals = torch.tensor([t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write], device=dev)
+    t_restore = restore()
+    vals = torch.tensor([t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm], device=dev)
     if world > 1:
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-    t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write = vals.tolist()
+    t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm = vals.tolist()
     if rank == 0:
         shutil.rmtree(path, ignore_errors=True)
         shutil.rmtree(path2, ignore_errors=True)
     total = nbytes.item()
-    return {
+    out = {
         "ckpt_bytes_total": int(total),
         "ckpt_save_blocking_s": round(t_resume, 4),
         "ckpt_save_durable_s": round(t_durable, 4),
         "ckpt_save_sync_s": round(t_sync, 4),
         "ckpt_restore_s": round(t_restore, 4),
+        "ckpt_restore_cold": dropped,
+        "ckpt_restore_warm_s": round(t_restore_warm, 4),
         "ckpt_save_plus_restore_s": round(t_sync + t_restore, 4),
         "ckpt_write_GBps": round(total / max(t_sync, 1e-9) / 1e9, 3),
+        "ckpt_restore_GBps": round(total / max(t_restore, 1e-9) / 1e9, 3),
         "ms_per_step_during_async_save": round(overlap_ms, 3),
-        "ckpt_format": "torch.distributed.checkpoint (.metadata + __r_0.distcp), native engine",
+        "ckpt_format": f"torch.distributed.checkpoint (.metadata + __<rank>_0.distcp x {world}), native engine",
         "ckpt_scope": "model + optimizer + step" if scope == "full" else "model + step",
+        "ckpt_fs": _fs_of(base),
     }
+    if downgraded:
+        out["ckpt_scope_downgraded"] = True
+    return out
+
+
+def drop_page_cache(path: str) -> bool:
+    """posix_fadvise(DONTNEED) every (fsynced, hence clean) shard so the next read is cold.
+    False when the files live on a RAM-backed filesystem, where there is no cold read."""
+    ok = True
+    for root, _dirs, files in os.walk(path):
+        for name in files:
+            fd = os.open(os.path.join(root, name), os.O_RDONLY)
+            try:
+                os.fsync(fd)
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            finally:
+                os.close(fd)
+    if _fs_of(path) in ("tmpfs", "ramfs"):
+        ok = False
+    return ok
+
+
+def _fs_of(path: str) -> str:
+    """Filesystem type of the mount holding `path` (from /proc/mounts)."""
+    try:
+        best, fs = "", "?"
+        p = os.path.realpath(path)
+        with open("/proc/mounts") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 3 and (p == parts[1] or p.startswith(parts[1].rstrip("/") + "/")):
+                    if len(parts[1]) > len(best):
+                        best, fs = parts[1], parts[2]
+        return fs
+    except OSError:
+        return "?"
 
 
 if __name__ == "__main__":

@@ -311,7 +311,8 @@ def read_metadata(checkpoint_id: str) -> Metadata:
 
 
 def _zip_data_record(path: str, base: int, length: int) -> tuple[int, int]:
-    """(absolute data offset, size) of the tensor record '<prefix>/data/0' in a zip slice."""
+    """(absolute data offset, size) of the tensor record '<prefix>/data/0' in a zip slice.
+    Handles ZIP64 (records >= 4 GiB, offsets past 4 GiB, zip64 end-of-central-directory)."""
     with open(path, "rb") as f:
         tail_len = min(length, 1 << 16)
         f.seek(base + length - tail_len)
@@ -320,17 +321,43 @@ def _zip_data_record(path: str, base: int, length: int) -> tuple[int, int]:
         if eocd < 0:
             raise IOError(f"{path}@{base}: no zip end record")
         n, cd_size, cd_off = struct.unpack("<HII", tail[eocd + 10:eocd + 20])
+        if n == 0xFFFF or cd_size == 0xFFFFFFFF or cd_off == 0xFFFFFFFF:
+            loc = eocd - 20
+            if loc < 0 or tail[loc:loc + 4] != b"PK\x06\x07":
+                raise IOError(f"{path}@{base}: zip64 locator missing")
+            (z64_off,) = struct.unpack("<Q", tail[loc + 8:loc + 16])
+            f.seek(base + z64_off)
+            rec = f.read(56)
+            if rec[:4] != b"PK\x06\x06":
+                raise IOError(f"{path}@{base}: bad zip64 end record")
+            n, _n2, cd_size, cd_off = struct.unpack("<QQQQ", rec[24:56])
         f.seek(base + cd_off)
         cd = f.read(cd_size)
         pos = 0
         for _ in range(n):
             (sig,) = struct.unpack("<I", cd[pos:pos + 4])
-            assert sig == 0x02014B50
-            csize, = struct.unpack("<I", cd[pos + 20:pos + 24])
+            if sig != 0x02014B50:
+                raise IOError(f"{path}@{base}: corrupt central directory")
+            csize, usize = struct.unpack("<II", cd[pos + 20:pos + 28])
             nlen, elen, clen = struct.unpack("<HHH", cd[pos + 28:pos + 34])
             lho, = struct.unpack("<I", cd[pos + 42:pos + 46])
             name = cd[pos + 46:pos + 46 + nlen].decode()
             if name.endswith("/data/0"):
+                if 0xFFFFFFFF in (csize, usize, lho):
+                    extra = cd[pos + 46 + nlen:pos + 46 + nlen + elen]
+                    e = 0
+                    while e + 4 <= len(extra):
+                        tag, sz = struct.unpack("<HH", extra[e:e + 4])
+                        if tag == 1:
+                            vals = list(struct.unpack("<" + "Q" * (sz // 8), extra[e + 4:e + 4 + sz]))
+                            if usize == 0xFFFFFFFF:
+                                usize = vals.pop(0)
+                            if csize == 0xFFFFFFFF:
+                                csize = vals.pop(0)
+                            if lho == 0xFFFFFFFF:
+                                lho = vals.pop(0)
+                            break
+                        e += 4 + sz
                 f.seek(base + lho)
                 lh = f.read(30)
                 lnlen, lelen = struct.unpack("<HH", lh[26:30])
@@ -387,7 +414,34 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
                 if tuple(c.offsets) == tuple(idx.offset):
                     csizes = tuple(c.sizes)
             reqs.append((dest, tuple(idx.offset), csizes or tuple(dest.shape), path, off, n, mdt.properties.dtype))
-    # batched: parallel pread into a pinned buffer, then H2D into the destination
+    # device destinations whose region is one contiguous run of the same dtype stream straight
+    # from the file: native pread -> pinned ring -> H2D on the engine's copy stream, pipelined
+    # (torchsave.get_engine().read_to_device); anything else (host destinations, resharded
+    # chunks, dtype casts) goes through a pinned staging buffer + copy_
+    direct: dict[str, tuple[list, list, list]] = {}
+    staged = []
+    for r in reqs:
+        dest, offs, csz, path, off, n, dt = r
+        region = dest
+        for dim, (o, sz) in enumerate(zip(offs, csz)):
+            region = region.narrow(dim, o, sz)
+        if (dest.is_cuda and region.is_contiguous() and region.dtype == dt
+                and region.numel() * region.element_size() == n and torch.cuda.is_available()):
+            o_, l_, d_ = direct.setdefault(path, ([], [], []))
+            o_.append(off)
+            l_.append(n)
+            d_.append(region.data_ptr())
+        else:
+            staged.append(r)
+    if direct:
+        from . import torchsave
+
+        eng = torchsave.get_engine()
+        torch.cuda.current_stream().synchronize()  # destinations may still be read by queued kernels
+        for path, (o, l, d) in direct.items():
+            eng.read_to_device(path, o, l, d, threads)
+    reqs = staged
+    # batched: parallel pread into a pinned buffer, then copy into the destination
     cap = max(pinned_mb << 20, max([r[5] for r in reqs], default=0))
     staging = _pinned(min(cap, sum(r[5] for r in reqs))) if reqs else None
     i = 0
@@ -409,8 +463,8 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
         for (dest, offs, csz, path, off, n, dt), at in batch:
             src = staging[at:at + n].view(dt).view(csz)
             region = dest
-            for dim, (o, s) in enumerate(zip(offs, csz)):
-                region = region.narrow(dim, o, s)
+            for dim, (o, s_) in enumerate(zip(offs, csz)):
+                region = region.narrow(dim, o, s_)
             with torch.no_grad():
                 region.copy_(src, non_blocking=dest.is_cuda)
         if dest_is_cuda(batch):

@@ -90,6 +90,8 @@ def get_optimizer_state_dict(model: nn.Module, optimizers, *, options: StateDict
     for opt in _optims(optimizers):
         if any(p not in opt.state for g in opt.param_groups for p in g["params"]):
             _init_optim_state(opt)
+        if hasattr(opt, "_materialize_steps"):
+            opt._materialize_steps()  # fused optimizers keep step counts as host ints
         for g in opt.param_groups:
             pg = {k: v for k, v in g.items() if k != "params"}
             pg["params"] = [names[p] for p in g["params"]]

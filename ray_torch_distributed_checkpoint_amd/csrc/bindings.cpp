@@ -219,6 +219,22 @@ static void xent(Tensor logits, c10::optional<Tensor> dlogits, c10::optional<Ten
                  c10::optional<Tensor> loss, c10::optional<Tensor> lse, c10::optional<Tensor> argmax, int64_t M,
                  int64_t V, int64_t ld, double grad_scale, int64_t ignore_index) {
   TORCH_CHECK(logits.is_cuda(), "xent: GPU tensor expected");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
+              "xent: logits must be fp32 or bf16");
+  TORCH_CHECK(logits.is_contiguous() && ld >= V && logits.numel() >= M * ld, "xent: logits [M, ld] contiguous");
+  if (dlogits.has_value())
+    TORCH_CHECK(dlogits->scalar_type() == logits.scalar_type() && dlogits->is_contiguous() &&
+                    dlogits->numel() >= M * ld,
+                "xent: dlogits must match logits");
+  if (target.has_value())
+    TORCH_CHECK(target->scalar_type() == at::kLong && target->is_contiguous() && target->numel() >= M,
+                "xent: target must be a contiguous int64 [M] tensor");
+  if (loss.has_value())
+    TORCH_CHECK(loss->scalar_type() == at::kFloat && loss->is_contiguous() && loss->numel() >= M,
+                "xent: loss must be a contiguous fp32 [M] tensor");
+  if (lse.has_value()) TORCH_CHECK(lse->scalar_type() == at::kFloat && lse->numel() >= M, "xent: lse fp32 [M]");
+  if (argmax.has_value())
+    TORCH_CHECK(argmax->scalar_type() == at::kLong && argmax->numel() >= M, "xent: argmax int64 [M]");
   check_rc(rtdc_xent(logits.data_ptr(), ptr_or_null(dlogits), (const int64_t*)ptr_or_null(target),
                      (float*)ptr_or_null(loss), (float*)ptr_or_null(lse), (int64_t*)ptr_or_null(argmax), (int)M,
                      (int)V, (int)ld, (float)grad_scale, (int)ignore_index,
@@ -591,6 +607,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             py::gil_scoped_release nogil;
             return e.wait(id);
           })
+      .def(
+          "read_to_device",
+          [](Engine& e, const std::string& path, std::vector<uint64_t> offs, std::vector<uint64_t> lens,
+             std::vector<uintptr_t> dsts, int nthreads) {
+            py::gil_scoped_release nogil;
+            e.read_to_device(path, offs, lens, dsts, nthreads);
+          },
+          py::arg("path"), py::arg("offs"), py::arg("lens"), py::arg("dsts"), py::arg("nthreads") = 8)
       .def_property_readonly("slot_bytes", &Engine::slot_bytes)
       .def_property_readonly("pinned", &Engine::pinned);
 }

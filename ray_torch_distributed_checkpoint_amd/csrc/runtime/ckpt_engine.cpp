@@ -51,8 +51,15 @@ static bool g_have_gpu() {
 }
 
 // ------------------------------------------------------------------------------------------
-// zip layout (no zip64: every record and archive < 4 GiB; asserted)
+// zip layout.  ZIP64 is used exactly where the 32-bit fields overflow (the scheme
+// PyTorchStreamWriter/miniz writes and torch.load reads): a record >= 4 GiB carries a zip64
+// extra field (0x0001) with its 64-bit sizes in the local header and the central directory;
+// a local header past 4 GiB carries its 64-bit offset in the central-directory extra; an
+// archive whose central directory lies past 4 GiB or holds >= 65535 entries gets a zip64
+// end-of-central-directory record + locator in front of the classic EOCD.
 // ------------------------------------------------------------------------------------------
+static constexpr uint64_t kZ32 = 0xFFFFFFFFull;
+
 struct Record {
   std::string name;
   std::string inline_data;    // small records (pickle, version files)
@@ -61,7 +68,8 @@ struct Record {
   bool on_device = false;
   // layout
   uint64_t header_off = 0, data_off = 0;
-  uint16_t extra_len = 0;
+  uint16_t extra_len = 0;     // local-header extra: zip64 sizes (if z64_size) + 'FB' padding
+  bool z64_size = false;
   uint32_t crc = 0;
 };
 
@@ -69,77 +77,143 @@ static void put16(std::string& s, uint16_t v) { s.push_back(v & 0xff); s.push_ba
 static void put32(std::string& s, uint32_t v) {
   for (int i = 0; i < 4; ++i) s.push_back((v >> (8 * i)) & 0xff);
 }
+static void put64(std::string& s, uint64_t v) {
+  for (int i = 0; i < 8; ++i) s.push_back((char)((v >> (8 * i)) & 0xff));
+}
+
+static uint64_t rec_size(const Record& r) { return r.src ? r.nbytes : r.inline_data.size(); }
 
 static std::string local_header(const Record& r, uint64_t size) {
   std::string h;
   put32(h, 0x04034b50);
-  put16(h, 20);  // version needed
+  put16(h, r.z64_size ? 45 : 20);  // version needed (4.5 = zip64)
   put16(h, 0);   // flags
   put16(h, 0);   // STORED
   put16(h, 0);   // mod time
   put16(h, 0x21);  // mod date (1980-01-01)
   put32(h, r.crc);
-  put32(h, (uint32_t)size);
-  put32(h, (uint32_t)size);
+  put32(h, r.z64_size ? (uint32_t)kZ32 : (uint32_t)size);
+  put32(h, r.z64_size ? (uint32_t)kZ32 : (uint32_t)size);
   put16(h, (uint16_t)r.name.size());
   put16(h, r.extra_len);
   h += r.name;
-  if (r.extra_len) {
+  uint16_t pad = r.extra_len;
+  if (r.z64_size) {
+    put16(h, 0x0001);
+    put16(h, 16);
+    put64(h, size);
+    put64(h, size);
+    pad -= 20;
+  }
+  if (pad) {
     put16(h, 0x4246);  // 'FB' padding field (PyTorchStreamWriter uses the same tag)
-    put16(h, (uint16_t)(r.extra_len - 4));
-    h.append(r.extra_len - 4, 'Z');
+    put16(h, (uint16_t)(pad - 4));
+    h.append(pad - 4, 'Z');
   }
   return h;
 }
-
-static uint64_t rec_size(const Record& r) { return r.src ? r.nbytes : r.inline_data.size(); }
 
 // Assign offsets; data of every record starts 64-B aligned.
 static uint64_t layout_records(std::vector<Record>& recs, uint64_t base) {
   uint64_t off = base;
   for (auto& r : recs) {
     r.header_off = off;
-    uint64_t hdr = 30 + r.name.size();
+    r.z64_size = rec_size(r) >= kZ32;
+    const uint64_t z = r.z64_size ? 20 : 0;
+    uint64_t hdr = 30 + r.name.size() + z;
     uint64_t data = off + hdr;
     uint64_t pad = (64 - (data % 64)) % 64;
     if (pad > 0 && pad < 4) pad += 64;  // extra field needs >= 4 bytes
-    r.extra_len = (uint16_t)pad;
+    r.extra_len = (uint16_t)(z + pad);
     r.data_off = data + pad;
     off = r.data_off + rec_size(r);
   }
   return off;
 }
 
+static uint64_t cd_entry_extra(const Record& r) {
+  return (r.z64_size ? 16 : 0) + (r.header_off >= kZ32 ? 8 : 0);
+}
+
+static bool eocd64_needed(const std::vector<Record>& recs, uint64_t cd_off, uint64_t cd_bytes) {
+  return recs.size() >= 0xFFFF || cd_off >= kZ32 || cd_bytes >= kZ32;
+}
+
+// central-directory bytes (entries only) of an archive whose data ends at cd_off
+static uint64_t cd_entries_size(const std::vector<Record>& recs) {
+  uint64_t n = 0;
+  for (auto& r : recs) {
+    const uint64_t e = cd_entry_extra(r);
+    n += 46 + r.name.size() + (e ? 4 + e : 0);
+  }
+  return n;
+}
+
+static uint64_t cd_size(const std::vector<Record>& recs, uint64_t cd_off) {
+  const uint64_t entries = cd_entries_size(recs);
+  return entries + 22 + (eocd64_needed(recs, cd_off, entries) ? 56 + 20 : 0);
+}
+
 static std::string central_dir(const std::vector<Record>& recs, uint64_t cd_off) {
   std::string cd;
   for (auto& r : recs) {
+    const uint64_t size = rec_size(r);
+    const bool z64_off = r.header_off >= kZ32;
+    const uint64_t extra = cd_entry_extra(r);
     put32(cd, 0x02014b50);
     put16(cd, 0x031e);  // made by: unix, 3.0
-    put16(cd, 20);
+    put16(cd, extra ? 45 : 20);
     put16(cd, 0);
     put16(cd, 0);
     put16(cd, 0);
     put16(cd, 0x21);
     put32(cd, r.crc);
-    put32(cd, (uint32_t)rec_size(r));
-    put32(cd, (uint32_t)rec_size(r));
+    put32(cd, r.z64_size ? (uint32_t)kZ32 : (uint32_t)size);
+    put32(cd, r.z64_size ? (uint32_t)kZ32 : (uint32_t)size);
     put16(cd, (uint16_t)r.name.size());
-    put16(cd, 0);  // extra
+    put16(cd, (uint16_t)(extra ? 4 + extra : 0));  // extra
     put16(cd, 0);  // comment
     put16(cd, 0);  // disk
     put16(cd, 0);  // internal attr
     put32(cd, 0);  // external attr
-    put32(cd, (uint32_t)r.header_off);
+    put32(cd, z64_off ? (uint32_t)kZ32 : (uint32_t)r.header_off);
     cd += r.name;
+    if (extra) {
+      put16(cd, 0x0001);
+      put16(cd, (uint16_t)extra);
+      if (r.z64_size) {
+        put64(cd, size);
+        put64(cd, size);
+      }
+      if (z64_off) put64(cd, r.header_off);
+    }
   }
-  const uint64_t cd_size = cd.size();
+  const uint64_t entries = cd.size();
+  const bool z64 = eocd64_needed(recs, cd_off, entries);
+  if (z64) {
+    const uint64_t eocd64_off = cd_off + entries;
+    put32(cd, 0x06064b50);
+    put64(cd, 44);
+    put16(cd, 45);
+    put16(cd, 45);
+    put32(cd, 0);
+    put32(cd, 0);
+    put64(cd, recs.size());
+    put64(cd, recs.size());
+    put64(cd, entries);
+    put64(cd, cd_off);
+    put32(cd, 0x07064b50);  // locator
+    put32(cd, 0);
+    put64(cd, eocd64_off);
+    put32(cd, 1);
+  }
   put32(cd, 0x06054b50);
   put16(cd, 0);
   put16(cd, 0);
-  put16(cd, (uint16_t)recs.size());
-  put16(cd, (uint16_t)recs.size());
-  put32(cd, (uint32_t)cd_size);
-  put32(cd, (uint32_t)cd_off);
+  put16(cd, z64 ? 0xFFFF : (uint16_t)recs.size());
+  put16(cd, z64 ? 0xFFFF : (uint16_t)recs.size());
+  put32(cd, z64 ? (uint32_t)kZ32 : (uint32_t)entries);
+  put32(cd, z64 ? (uint32_t)kZ32 : (uint32_t)cd_off);
   put16(cd, 0);
   return cd;
 }
@@ -245,12 +319,6 @@ struct Archive {
   uint64_t size = 0;      // full archive size (incl. central directory)
 };
 
-static uint64_t cd_size(const std::vector<Record>& recs) {
-  uint64_t n = 22;
-  for (auto& r : recs) n += 46 + r.name.size();
-  return n;
-}
-
 // Assign archive bases and record offsets; returns the file size.
 static uint64_t layout_archives(std::vector<Archive>& arcs) {
   uint64_t off = 0;
@@ -268,7 +336,7 @@ static uint64_t layout_archives(std::vector<Archive>& arcs) {
       a.size = n;
     } else {
       a.data_end = layout_records(a.recs, 0);
-      a.size = a.data_end + cd_size(a.recs);
+      a.size = a.data_end + cd_size(a.recs, a.data_end);
     }
     off += a.size;
   }
@@ -385,6 +453,64 @@ class Engine {
 
   size_t slot_bytes() const { return ring_.slot_bytes(); }
   bool pinned() const { return ring_.pinned(); }
+
+  // Restore path: stream file ranges to device memory through the same pinned ring.
+  // Ranges are split into slot-sized pieces; `nthreads` readers each take a piece, pread it
+  // into a free pinned slot, enqueue the H2D copy on the engine's copy stream and release
+  // the slot once that copy has landed - so the pread of one piece overlaps the DMA of the
+  // others and host memory stays bounded by the ring.  Blocks until every byte is on the
+  // device (the caller must not be using the destinations on another stream).
+  void read_to_device(const std::string& path, const std::vector<uint64_t>& offs,
+                      const std::vector<uint64_t>& lens, const std::vector<uintptr_t>& dsts, int nthreads) {
+    if (!stream_) throw std::runtime_error("read_to_device: no GPU");
+    if (offs.size() != lens.size() || offs.size() != dsts.size())
+      throw std::runtime_error("read_to_device: offs/lens/dsts length mismatch");
+    int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("open failed: " + path + ": " + strerror(errno));
+    struct P { uint64_t off, len; char* dst; };
+    std::vector<P> pieces;
+    const uint64_t S = ring_.slot_bytes();
+    for (size_t i = 0; i < offs.size(); ++i)
+      for (uint64_t o = 0; o < lens[i]; o += S)
+        pieces.push_back({offs[i] + o, std::min(S, lens[i] - o), (char*)dsts[i] + o});
+    std::atomic<size_t> next{0};
+    std::string err;
+    std::mutex emu, cmu;
+    auto work = [&] {
+      hipSetDevice(device_);
+      while (true) {
+        const size_t k = next++;
+        if (k >= pieces.size()) return;
+        {
+          std::lock_guard<std::mutex> lk(emu);
+          if (!err.empty()) return;
+        }
+        const int s = ring_.acquire();
+        try {
+          pread_all(fd, ring_.ptr(s), pieces[k].len, pieces[k].off);
+          hipError_t e;
+          {
+            std::lock_guard<std::mutex> lk(cmu);
+            e = hipMemcpyAsync(pieces[k].dst, ring_.ptr(s), pieces[k].len, hipMemcpyHostToDevice, stream_);
+            if (e == hipSuccess) e = hipEventRecord(ring_.event(s), stream_);
+          }
+          if (e == hipSuccess) e = hipEventSynchronize(ring_.event(s));
+          if (e != hipSuccess) throw std::runtime_error(std::string("restore H2D: ") + hipGetErrorString(e));
+        } catch (std::exception& ex) {
+          std::lock_guard<std::mutex> lk(emu);
+          err = ex.what();
+        }
+        ring_.release(s);
+      }
+    };
+    std::vector<std::thread> ts;
+    const int nt = std::max(1, std::min<int>(std::min<int>(nthreads, (int)ring_.nslots()), (int)pieces.size()));
+    for (int i = 0; i < nt; ++i) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+    ::close(fd);
+    if (err.empty() && hipStreamSynchronize(stream_) != hipSuccess) err = "restore: copy stream failed";
+    if (!err.empty()) throw std::runtime_error(err);
+  }
 
  private:
   struct WJob {

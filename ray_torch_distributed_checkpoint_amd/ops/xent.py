@@ -21,28 +21,48 @@ from .shadow import shadow_of
 IGNORE_INDEX = -100
 
 
+def _valid_count(target: torch.Tensor) -> torch.Tensor:
+    """Number of non-ignored rows as a 1-element fp32 device tensor (no host sync)."""
+    return (target.reshape(-1) != IGNORE_INDEX).sum(dtype=torch.float32).clamp_min(1.0).reshape(1)
+
+
+def _check_target(target: torch.Tensor) -> None:
+    if target.dtype != torch.int64:
+        raise TypeError(f"cross_entropy: int64 class targets expected, got {target.dtype}")
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, n_valid):
+        """n_valid: host int (fixed divisor) or None (count of non-ignored rows, on device)."""
         M, V = logits.shape
         lg = logits.contiguous()
         loss = torch.empty(M, dtype=torch.float32, device=lg.device)
         grad = torch.empty_like(lg)
-        gpu_ext().xent(lg, grad, target.contiguous(), loss, None, None, M, V, V, 1.0 / n_valid, IGNORE_INDEX)
-        ctx.save_for_backward(grad)
+        scale = 1.0 / n_valid if n_valid is not None else 1.0
+        gpu_ext().xent(lg, grad, target.contiguous(), loss, None, None, M, V, V, scale, IGNORE_INDEX)
+        if n_valid is None:
+            cnt = _valid_count(target)
+            ctx.save_for_backward(grad, cnt)
+            return (loss.sum() / cnt).reshape(())
+        ctx.save_for_backward(grad, None)
         return loss.sum() / n_valid
 
     @staticmethod
     def backward(ctx, g):
-        (grad,) = ctx.saved_tensors
-        return grad * g.to(grad.dtype), None, None
+        grad, cnt = ctx.saved_tensors
+        a = g.to(torch.float32) if cnt is None else (g.to(torch.float32) / cnt).reshape(())
+        return grad * a.to(grad.dtype), None, None
 
 
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor, n_valid: int | None = None) -> torch.Tensor:
+    """nn.CrossEntropyLoss() (mean over rows whose target != -100).  On the GPU the divisor is
+    counted on the device unless the caller passes `n_valid`."""
     if not logits.is_cuda:
         return F.cross_entropy(logits.float(), target, ignore_index=IGNORE_INDEX)
-    if n_valid is None:
-        n_valid = target.numel()
+    _check_target(target)
+    if logits.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(f"cross_entropy: fp32 or bf16 logits expected on the GPU, got {logits.dtype}")
     return _CrossEntropy.apply(logits, target, n_valid)
 
 
@@ -58,29 +78,38 @@ class _LMHeadXent(torch.autograd.Function):
         M = x2.shape[0]
         logits = G.linear_fwd(x2, ws)  # [M, Vp] bf16
         loss = torch.empty(M, dtype=torch.float32, device=x.device)
+        scale = 1.0 / n_valid if n_valid is not None else 1.0
         gpu_ext().xent(logits, logits, target.reshape(-1).contiguous(), loss, None, None, M, vocab, Vp,
-                       1.0 / n_valid, IGNORE_INDEX)
-        ctx.save_for_backward(x2, ws, logits)
+                       scale, IGNORE_INDEX)
+        cnt = _valid_count(target) if n_valid is None else None
+        ctx.save_for_backward(x2, ws, logits, cnt)
         ctx.in_shape = x.shape
         ctx.w = w
+        if cnt is not None:
+            return (loss.sum() / cnt).reshape(())
         return loss.sum() / n_valid
 
     @staticmethod
     def backward(ctx, g):
-        x2, ws, dlogits = ctx.saved_tensors
-        # the upstream loss gradient is applied as a device-side alpha inside both GEMMs
-        gs = g.detach().to(torch.float32).reshape(1).contiguous()
+        x2, ws, dlogits, cnt = ctx.saved_tensors
+        # the upstream loss gradient (and the 1/#valid divisor) is a device-side alpha inside both GEMMs
+        gs = g.detach().to(torch.float32).reshape(1)
+        if cnt is not None:
+            gs = gs / cnt
+        gs = gs.contiguous()
         dx = G.linear_dgrad(dlogits, ws, alpha_dev=gs)
         dw = G.linear_wgrad(dlogits, x2, out=grad_target(ctx.w), alpha_dev=gs)
         return dx.view(ctx.in_shape), dw, None, None, None
 
 
 def lm_head_cross_entropy(x, w, target, vocab: int, n_valid: int | None = None):
-    if n_valid is None:
-        n_valid = target.numel()
+    """Tied/untied LM head + mean cross-entropy over non-ignored targets (see cross_entropy)."""
     if not x.is_cuda:
         logits = F.linear(x, w.to(x.dtype))[..., :vocab]
         return F.cross_entropy(logits.reshape(-1, vocab).float(), target.reshape(-1), ignore_index=IGNORE_INDEX)
+    _check_target(target)
+    if x.dtype != torch.bfloat16:
+        raise TypeError(f"lm_head_cross_entropy: bf16 activations expected on the GPU, got {x.dtype}")
     return _LMHeadXent.apply(x, w, target, vocab, n_valid)
 
 

@@ -124,21 +124,28 @@ class FlatParamSpace:
                 p.grad = v
 
     def ensure_grad_views(self):
-        """Re-attach grads that were replaced (e.g. zero_grad(set_to_none=True))."""
+        """Fold gradients that autograd allocated outside the flat buffer back into it.
+        Parameters without a gradient stay `None` (the optimizers skip them, like torch)."""
         if self.grad is None:
             return
         base = self.grad.data_ptr()
         for p, s in zip(self.params, self.segments):
             g = p.grad
-            if g is not None and g.data_ptr() == base + 4 * s.offset:
+            if g is None or g.data_ptr() == base + 4 * s.offset:
                 continue
             self.wait_pending_tail()  # never write into a slice a collective still owns
             v = self.view(self.grad, s)
-            if g is None:
-                v.zero_()
-            else:
-                v.copy_(g)
+            v.copy_(g)
             p.grad = v
+
+    def attach_grad_views(self):
+        """Point every parameter's `.grad` at its flat slice (after a data-parallel reduce
+        every slice holds the averaged gradient, whether or not this rank produced one)."""
+        if self.grad is None:
+            return
+        for p, s in zip(self.params, self.segments):
+            if p.grad is None:
+                p.grad = self.view(self.grad, s)
 
     def chunk_table_split(self, params_subset, decay_flags, split: int):
         """Two chunk tables: segments below flat offset `split`, and the rest."""

@@ -5,6 +5,14 @@ API and `state_dict()` format match `torch.optim.AdamW` / `torch.optim.SGD` (sta
 torch.  On the GPU the state tensors are views into flat fp32 buffers and the step is the
 chunk-table kernel in csrc/kernels/optim.hip, which also refreshes the bf16 compute shadows.
 On the CPU the same math runs per tensor with torch ops (reference path).
+
+Host cost per step is O(#params) Python dict work and nothing else: AdamW step counts are
+plain host integers (torch keeps one CPU tensor per parameter and does `step += 1` plus a
+`float()` on each - ~150 tensor ops per GPT-2 step that left the GPU idle before the
+optimizer launch); the per-parameter `step` tensors are materialised only by
+`state_dict()` and parsed back by `load_state_dict()`, so checkpoints stay torch-compatible.
+Like torch.optim, parameters without a gradient this step are skipped entirely (no weight
+decay, no momentum), and the chunk table is built only from parameters that have one.
 """
 from __future__ import annotations
 
@@ -23,6 +31,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self._space: FlatParamSpace | None = None
         self._bufs: dict[str, torch.Tensor] = {}
+        self._steps: dict = {}  # param -> number of optimizer steps taken (host int)
+        self._bound: set = set()
 
     # -- flat setup ------------------------------------------------------------------------
     def _all_params(self):
@@ -39,6 +49,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
             for p, g in zip(params, saved):
                 if g is not None:
                     p.grad.copy_(g)
+                else:
+                    p.grad = None
         self._space = sp
         for k in self._state_keys:
             self._bufs[k] = torch.zeros(sp.numel, dtype=torch.float32, device=sp.device)
@@ -56,11 +68,14 @@ class _FlatOptimizer(torch.optim.Optimizer):
         return sp
 
     def _bind_state(self, p):
+        if p in self._bound:
+            return self.state[p]
         st = self.state[p]
         seg = self._space.segment_of(p)
         for k in self._state_keys:
             if k not in st:
                 st[k] = FlatParamSpace.view(self._bufs[k], seg)
+        self._bound.add(p)
         return st
 
     @torch.no_grad()
@@ -80,10 +95,23 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 for k in self._state_keys:
                     if k not in st:
                         st[k] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            self._init_extra(st)
+            self._init_extra(p, st)
+        self._materialize_steps()
 
-    def _init_extra(self, st) -> None:
+    def _init_extra(self, p, st) -> None:
         pass
+
+    # -- torch-compatible state dict -------------------------------------------------------
+    def _materialize_steps(self) -> None:
+        """Write the host step counters into the per-parameter `step` tensors torch keeps."""
+        for p, n in self._steps.items():
+            st = self.state.get(p)
+            if st is not None:
+                st["step"] = torch.tensor(float(n))
+
+    def state_dict(self):
+        self._materialize_steps()
+        return super().state_dict()
 
     def zero_grad(self, set_to_none: bool = True):
         if self._space is not None and self._space.grad is not None:
@@ -93,6 +121,12 @@ class _FlatOptimizer(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
+        self._steps = {}
+        self._bound = set()
+        for p in self._all_params():
+            st = self.state.get(p)
+            if st and "step" in st:
+                self._steps[p] = int(float(st["step"]))
         if self._space is not None:
             for p in self._all_params():
                 st = self.state.get(p)
@@ -107,9 +141,9 @@ class _FlatOptimizer(torch.optim.Optimizer):
                             st[k] = v
 
     def _launch_split(self, sp, launches) -> None:
-        """launches: [(params, decay_flags, fn(chunks, n))] per group.  With a pending
-        last-bucket all-reduce (DDP defer_tail_to_optimizer), update everything below its
-        slice first, stream-wait for the collective, then the slice itself."""
+        """launches: [(params, decay_flags, fn(chunks, n))].  With a pending last-bucket
+        all-reduce (DDP defer_tail_to_optimizer), update everything below its slice first,
+        stream-wait for the collective, then the slice itself."""
         tail = sp.pending_tail
         if tail is None:
             for ps, flags, fn in launches:
@@ -129,6 +163,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
         ps = self._all_params()
         return bool(ps) and ps[0].is_cuda
 
+    @staticmethod
+    def _with_grad(group) -> list:
+        return [p for p in group["params"] if p.grad is not None]
+
     @property
     def flat_space(self):
         return self._space
@@ -137,9 +175,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
 class FusedAdamW(_FlatOptimizer):
     _state_keys = ("exp_avg", "exp_avg_sq")
 
-    def _init_extra(self, st) -> None:
-        if "step" not in st:
-            st["step"] = torch.tensor(0.0)
+    def _init_extra(self, p, st) -> None:
+        self._steps.setdefault(p, 0)
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
                  maximize=False):
@@ -148,6 +185,16 @@ class FusedAdamW(_FlatOptimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
                                       maximize=False, foreach=None, capturable=False, differentiable=False,
                                       fused=None))
+
+    def _count(self, ps) -> dict:
+        """Advance the step counter of every parameter in `ps`; {step: [params]}."""
+        steps = self._steps
+        by = {}
+        for p in ps:
+            n = steps.get(p, 0) + 1
+            steps[p] = n
+            by.setdefault(n, []).append(p)
+        return by
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -164,25 +211,20 @@ class FusedAdamW(_FlatOptimizer):
             ext = gpu_ext()
             launches = []
             for group in self.param_groups:
-                ps = group["params"]
+                ps = self._with_grad(group)
                 if not ps:
                     continue
-                step = None
                 for p in ps:
-                    st = self._bind_state(p)
-                    if "step" not in st:
-                        st["step"] = torch.tensor(0.0)
-                    st["step"] += 1
-                    step = float(st["step"])
+                    self._bind_state(p)
                 b1, b2 = group["betas"]
                 wd = group["weight_decay"]
+                for step, sub in self._count(ps).items():
+                    def fn(chunks, n, group=group, b1=b1, b2=b2, wd=wd, step=step):
+                        ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"],
+                                  sp.shadow, group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step,
+                                  math.sqrt(1 - b2 ** step), sp.grad_scale)
 
-                def fn(chunks, n, group=group, b1=b1, b2=b2, wd=wd, step=step):
-                    ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"],
-                              sp.shadow, group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step,
-                              math.sqrt(1 - b2 ** step), sp.grad_scale)
-
-                launches.append((ps, [wd != 0.0] * len(ps), fn))
+                    launches.append((sub, [wd != 0.0] * len(sub), fn))
             self._launch_split(sp, launches)
             return loss
         sp = space_of(self._all_params())
@@ -190,22 +232,19 @@ class FusedAdamW(_FlatOptimizer):
             sp.wait_pending_tail()
         for group in self.param_groups:
             b1, b2 = group["betas"]
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
-                st = self.state[p]
-                if "step" not in st:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p)
-                    st["exp_avg_sq"] = torch.zeros_like(p)
-                st["step"] += 1
-                t = float(st["step"])
-                g = p.grad
-                p.mul_(1 - group["lr"] * group["weight_decay"])
-                st["exp_avg"].lerp_(g, 1 - b1)
-                st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
-                denom = (st["exp_avg_sq"].sqrt() / math.sqrt(1 - b2 ** t)).add_(group["eps"])
-                p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / (1 - b1 ** t))
+            ps = self._with_grad(group)
+            for step, sub in self._count(ps).items():
+                for p in sub:
+                    st = self.state[p]
+                    if "exp_avg" not in st:
+                        st["exp_avg"] = torch.zeros_like(p)
+                        st["exp_avg_sq"] = torch.zeros_like(p)
+                    g = p.grad
+                    p.mul_(1 - group["lr"] * group["weight_decay"])
+                    st["exp_avg"].lerp_(g, 1 - b1)
+                    st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+                    denom = (st["exp_avg_sq"].sqrt() / math.sqrt(1 - b2 ** step)).add_(group["eps"])
+                    p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / (1 - b1 ** step))
         return loss
 
 
@@ -236,25 +275,28 @@ class FusedSGD(_FlatOptimizer):
             ext = gpu_ext()
             launches = []
             for group in self.param_groups:
-                ps = group["params"]
+                ps = self._with_grad(group)
                 if not ps:
                     continue
                 mom = group["momentum"]
-                first = False
-                if mom != 0.0:
-                    for p in ps:
-                        st = self.state[p]
-                        if "momentum_buffer" not in st:
-                            first = True
-                        self._bind_state(p)
                 wd = group["weight_decay"]
+                # torch's first momentum step is `buf = d` (a clone): parameters without a
+                # buffer yet form their own launch with first=True
+                parts = [(ps, False)]
+                if mom != 0.0:
+                    fresh = [p for p in ps if "momentum_buffer" not in self.state[p]]
+                    if fresh:
+                        old = [p for p in ps if "momentum_buffer" in self.state[p]]
+                        parts = [(fresh, True)] + ([(old, False)] if old else [])
+                    for p in fresh:
+                        self._bind_state(p)
+                for sub, first in parts:
+                    def fn(chunks, n, group=group, mom=mom, wd=wd, first=first):
+                        ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None,
+                                sp.shadow, group["lr"], mom, group["dampening"], wd, group["nesterov"], first,
+                                sp.grad_scale)
 
-                def fn(chunks, n, group=group, mom=mom, wd=wd, first=first):
-                    ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None,
-                            sp.shadow, group["lr"], mom, group["dampening"], wd, group["nesterov"], first,
-                            sp.grad_scale)
-
-                launches.append((ps, [wd != 0.0] * len(ps), fn))
+                    launches.append((sub, [wd != 0.0] * len(sub), fn))
             self._launch_split(sp, launches)
             return loss
         sp = space_of(self._all_params())
@@ -262,9 +304,7 @@ class FusedSGD(_FlatOptimizer):
             sp.wait_pending_tail()
         for group in self.param_groups:
             mom = group["momentum"]
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
+            for p in self._with_grad(group):
                 d = p.grad
                 if group["weight_decay"] != 0:
                     d = d.add(p, alpha=group["weight_decay"])

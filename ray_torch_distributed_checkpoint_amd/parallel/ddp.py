@@ -246,6 +246,7 @@ class DistributedDataParallel(nn.Module):
                 self.space.pending_tail = (self._engine.tail_start(), self._engine.wait_tail)
             if self._check:  # RTDC_COLLECTIVE_CHECK=1: desync detector (one tiny all-reduce per step)
                 self._agree(self._steps * 1000003 + self._engine.launched() + len(self.buckets), "step sequence")
+            self.space.attach_grad_views()
             return
         # params that produced no gradient this step: zero-filled grads, still reduced
         while self._next < len(self.buckets):
@@ -261,6 +262,7 @@ class DistributedDataParallel(nn.Module):
         if not self._use_avg:
             with torch.no_grad():
                 self.space.grad.mul_(1.0 / self.world_size)
+        self.space.attach_grad_views()
         self._next = 0
         self._callback_queued = False
 

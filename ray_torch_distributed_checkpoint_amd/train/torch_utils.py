@@ -82,6 +82,18 @@ class _Len:
         return self.n
 
 
+def _record_stream(b, stream) -> None:
+    if torch.is_tensor(b):
+        if b.is_cuda:
+            b.record_stream(stream)
+    elif isinstance(b, (list, tuple)):
+        for x in b:
+            _record_stream(x, stream)
+    elif isinstance(b, dict):
+        for x in b.values():
+            _record_stream(x, stream)
+
+
 class DeviceLoader:
     """Wraps a DataLoader: pinned batches copied H2D on a side stream one batch ahead."""
 
@@ -117,8 +129,13 @@ class DeviceLoader:
 
         nxt = stage()
         while nxt is not None:
-            torch.cuda.current_stream().wait_stream(stream)
+            consumer = torch.cuda.current_stream()
+            consumer.wait_stream(stream)
             cur = nxt
+            # the batch was allocated on the side stream but is read on the consumer stream:
+            # without this the caching allocator could hand its block to a later H2D copy while
+            # this step's kernels still read it
+            _record_stream(cur, consumer)
             nxt = stage()
             yield cur
 

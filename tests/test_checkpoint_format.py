@@ -151,3 +151,30 @@ def test_dcp_verify_mode_reads_back_and_detects_corruption(tmp_path, monkeypatch
         f.write(bytes([b[0] ^ 0xFF]))
     with pytest.raises(IOError):
         h2.wait()
+
+
+def test_zip64_record_over_4gib_is_torch_loadable(tmp_path):
+    """A record >= 4 GiB (e.g. a Llama-3-8B embedding's AdamW state in one .pt) must be written as
+    ZIP64, not silently truncated to 32-bit sizes: stock torch.load reads it back, and so does
+    the DCP reader when the same archive is a .distcp item."""
+    n = (1 << 32) + 4096 + 77  # bytes
+    big = torch.empty(n, dtype=torch.uint8)
+    big[:4096] = torch.arange(4096, dtype=torch.int64).to(torch.uint8)
+    big[-77:] = 201
+    small = torch.arange(5, dtype=torch.float32)
+    path = str(tmp_path / "big.pt")
+    torchsave.save({"big": big, "small": small}, path, crc=False)
+    with zipfile.ZipFile(path) as z:  # zip64 central directory parses
+        infos = {i.filename.split("/", 1)[1]: i for i in z.infolist()}
+        assert infos["data/0"].file_size == n
+    del big
+    out = torch.load(path, weights_only=True, mmap=True)
+    assert out["big"].numel() == n and int(out["big"][4095]) == 4095 % 256 and int(out["big"][-1]) == 201
+    assert torch.equal(out["small"], small)
+    del out
+    # the DCP record locator (used by dcp.load) on the same archive
+    off, size = dcp._zip_data_record(path, 0, os.path.getsize(path))
+    assert size == n
+    with open(path, "rb") as f:
+        f.seek(off + n - 77)
+        assert f.read(77) == bytes([201]) * 77
