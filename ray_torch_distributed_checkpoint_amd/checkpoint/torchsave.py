@@ -103,7 +103,22 @@ _engine = None
 _engine_lock = threading.Lock()
 
 
+_engine_cfg: tuple | None = None
+
+
+def configure_engine(nslots: int, slot_mb: int, writers: int = 0) -> None:
+    """Size the process-wide engine (CheckpointConfig.pinned_ring_mb / ring_slot_mb /
+    writer_threads); must run before the first checkpoint I/O of the process."""
+    global _engine_cfg
+    if _engine is not None:
+        return
+    w = writers or min(8, max(2, (os.cpu_count() or 4) // 2))
+    _engine_cfg = (int(nslots), int(slot_mb) << 20, int(w))
+
+
 def engine_config():
+    if _engine_cfg is not None and "RTDC_CKPT_SLOTS" not in os.environ:
+        return _engine_cfg
     slot_mb = int(os.environ.get("RTDC_CKPT_SLOT_MB", "64"))
     nslots = int(os.environ.get("RTDC_CKPT_SLOTS", "8"))
     writers = int(os.environ.get("RTDC_CKPT_WRITERS", str(min(8, max(2, (os.cpu_count() or 4) // 2)))))

@@ -105,6 +105,23 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restric
   }
 }
 
+__global__ __launch_bounds__(256) void bf16_to_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
+                                                         long long n, float scale) {
+  for (long long i = (blockIdx.x * 256LL + threadIdx.x) * 4; i < n; i += gridDim.x * 256LL * 4) {
+    if (i + 4 <= n) {
+      const uint2 u = *(const uint2*)(x + i);
+      f32x4 v;
+      v[0] = __uint_as_float(u.x << 16) * scale;
+      v[1] = __uint_as_float(u.x & 0xffff0000u) * scale;
+      v[2] = __uint_as_float(u.y << 16) * scale;
+      v[3] = __uint_as_float(u.y & 0xffff0000u) * scale;
+      *(f32x4*)(y + i) = v;
+    } else {
+      for (long long e = i; e < n; ++e) y[e] = bf2f(x[e]) * scale;
+    }
+  }
+}
+
 // sum of squares per chunk -> partial[ci] (for grad-norm clipping); deterministic
 __global__ __launch_bounds__(256) void sumsq_kernel(const Chunk* __restrict__ chunks, int nchunks,
                                                    const float* __restrict__ g, float* __restrict__ partial) {
@@ -158,5 +175,13 @@ extern "C" int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float
   if (nchunks <= 0) return 0;
   hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
                      nchunks, g, partial);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_bf16_to_f32(const void* x, float* y, long long n, float scale, hipStream_t st) {
+  long long blocks = (n / 4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)x, y, n, scale);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

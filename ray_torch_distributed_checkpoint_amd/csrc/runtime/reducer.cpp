@@ -14,10 +14,23 @@
 //   * finalize() (queued at the end of backward) launches what is left (parameters that got
 //     no gradient), waits for every Work - which on RCCL makes the current stream wait, not
 //     the host - applies the 1/world post-scale for backends without AVG (gloo), and resets.
+// Reduced-precision communication (grad_comm_dtype="bf16"): when a bucket is ready its fp32
+// slice is rounded into a parallel bf16 buffer on the compute stream (one streaming kernel),
+// the bf16 slice is all-reduced (half the xGMI bytes of fp32), and as soon as that collective
+// completes a side stream widens it back into the fp32 master-gradient slice - so `p.grad`
+// still holds the averaged gradient and the optimizer is unchanged; the compute stream only
+// waits for the side stream's event at the end of backward.
 // Bucket bookkeeping is lock-free single-threaded state: autograd invokes the hooks from
 // one engine thread per device.
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
+
+extern "C" {
+int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st);
+int rtdc_bf16_to_f32(const void* x, float* y, long long n, float scale, hipStream_t st);
+}
 
 namespace rtdc_ddp {
 
@@ -26,12 +39,25 @@ class GradBucketEngine {
   // seg: per parameter (offset, numel) inside flat_grad, same order as param_bucket
   GradBucketEngine(at::Tensor flat_grad, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
                    std::vector<std::pair<int64_t, int64_t>> seg, c10::intrusive_ptr<c10d::ProcessGroup> pg,
-                   bool use_avg, double post_scale)
+                   bool use_avg, double post_scale, c10::optional<at::Tensor> comm_buf)
       : flat_(std::move(flat_grad)), bounds_(std::move(bounds)), param_bucket_(std::move(param_bucket)),
         seg_(std::move(seg)), pg_(std::move(pg)), use_avg_(use_avg), post_scale_(post_scale) {
     TORCH_CHECK(seg_.size() == param_bucket_.size(), "one segment per parameter");
     TORCH_CHECK(bounds_.size() >= 2, "need at least one bucket");
     const size_t nb = bounds_.size() - 1;
+    if (comm_buf.has_value()) {
+      lp_ = *comm_buf;
+      TORCH_CHECK(lp_.scalar_type() == at::kBFloat16 && lp_.numel() == flat_.numel() &&
+                      lp_.device() == flat_.device() && lp_.is_contiguous(),
+                  "comm buffer: contiguous bf16 twin of the flat gradient buffer");
+      if (flat_.is_cuda()) {
+        side_.emplace(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true,
+                                                                      flat_.device().index()));
+        events_.resize(nb, nullptr);
+        for (auto& e : events_) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
+                                            "hipEventCreate");
+      }
+    }
     expected_.assign(nb, 0);
     for (int64_t b : param_bucket_) {
       TORCH_CHECK(b >= 0 && (size_t)b < nb, "bad bucket index");
@@ -57,6 +83,11 @@ class GradBucketEngine {
   // last, e.g. GPT-2's tied 154 MB token table, so its all-reduce is the step's exposed tail).
   // Backends without an averaging collective (gloo) get the 1/world scale per part: the
   // final slices now, the deferred one in wait_tail().
+  ~GradBucketEngine() {
+    for (auto e : events_)
+      if (e) hipEventDestroy(e);
+  }
+
   void finalize(bool defer_last = false) {
     wait_tail();
     // parameters that produced no gradient this step contribute zeros (their slots may hold
@@ -66,17 +97,24 @@ class GradBucketEngine {
       if (!marked_[i]) flat_.slice(0, seg_[i].first, seg_[i].first + seg_[i].second).zero_();
     while (next_ < works_.size()) launch(next_++);
     const bool defer = defer_last && works_.size() > 1;
-    {
-      pybind11::gil_scoped_release nogil;
-      for (size_t b = 0; b + (defer ? 1 : 0) < works_.size(); ++b)
-        if (works_[b]) works_[b]->wait();
+    const size_t nwait = works_.size() - (defer ? 1 : 0);
+    if (side_) {
+      // the widened fp32 slices are final once the side stream passed each bucket's event
+      hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+      if (nwait > 0) TORCH_CHECK(hipStreamWaitEvent(cur, events_[nwait - 1], 0) == hipSuccess, "hipStreamWaitEvent");
+    } else {
+      {
+        pybind11::gil_scoped_release nogil;
+        for (size_t b = 0; b < nwait; ++b)
+          if (works_[b]) works_[b]->wait();
+      }
+      if (lp_.defined())  // CPU (gloo): widen in place after the blocking wait
+        for (size_t b = 0; b < nwait; ++b) widen(b);
+      else if (!use_avg_ && post_scale_ != 1.0)
+        flat_.slice(0, 0, bounds_[nwait]).mul_(post_scale_);
     }
     if (defer) tail_ = works_.back();
-    if (!use_avg_ && post_scale_ != 1.0) {
-      if (defer) flat_.slice(0, 0, tail_start()).mul_(post_scale_);
-      else flat_.mul_(post_scale_);
-    }
-    for (auto& w : works_) w.reset();
+    for (size_t b = 0; b < nwait; ++b) works_[b].reset();
     pending_ = expected_;
     std::fill(launched_.begin(), launched_.end(), false);
     std::fill(marked_.begin(), marked_.end(), false);
@@ -87,12 +125,23 @@ class GradBucketEngine {
   // stream-order the last bucket's all-reduce before later work (no-op when none is pending)
   void wait_tail() {
     if (!tail_) return;
-    {
-      pybind11::gil_scoped_release nogil;
-      tail_->wait();
+    const size_t last = works_.size() - 1;
+    if (side_) {
+      hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+      TORCH_CHECK(hipStreamWaitEvent(cur, events_[last], 0) == hipSuccess, "hipStreamWaitEvent");
+    } else {
+      {
+        pybind11::gil_scoped_release nogil;
+        tail_->wait();
+      }
+      if (lp_.defined()) widen(last);
+      else if (!use_avg_ && post_scale_ != 1.0) flat_.slice(0, tail_start(), bounds_.back()).mul_(post_scale_);
     }
     tail_.reset();
-    if (!use_avg_ && post_scale_ != 1.0) flat_.slice(0, tail_start(), bounds_.back()).mul_(post_scale_);
+    works_[last].reset();
+  }
+  int64_t comm_bytes_per_step() const {
+    return (bounds_.back() - bounds_.front()) * (lp_.defined() ? 2 : 4);
   }
   bool tail_pending() const { return (bool)tail_; }
   int64_t tail_start() const { return bounds_[bounds_.size() - 2]; }
@@ -102,7 +151,8 @@ class GradBucketEngine {
   int64_t launched() const { return (int64_t)next_; }
   std::vector<int64_t> bucket_bytes() const {
     std::vector<int64_t> out;
-    for (size_t b = 0; b + 1 < bounds_.size(); ++b) out.push_back((bounds_[b + 1] - bounds_[b]) * 4);
+    for (size_t b = 0; b + 1 < bounds_.size(); ++b)
+      out.push_back((bounds_[b + 1] - bounds_[b]) * (lp_.defined() ? 2 : 4));
     return out;
   }
 
@@ -112,14 +162,52 @@ class GradBucketEngine {
   }
 
   void launch(size_t b) {
-    std::vector<at::Tensor> t{flat_.slice(0, bounds_[b], bounds_[b + 1])};
+    const int64_t lo = bounds_[b], hi = bounds_[b + 1];
+    at::Tensor src = flat_.slice(0, lo, hi);
+    std::vector<at::Tensor> t{src};
+    if (lp_.defined()) {
+      at::Tensor dst = lp_.slice(0, lo, hi);
+      if (flat_.is_cuda()) {
+        hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+        TORCH_CHECK(rtdc_f32_to_bf16(src.data_ptr<float>(), dst.data_ptr(), hi - lo, cur) == 0, "f32->bf16");
+      } else {
+        dst.copy_(src);
+      }
+      t[0] = dst;
+    }
     c10d::AllreduceOptions opts;
     opts.reduceOp = use_avg_ ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
     works_[b] = pg_->allreduce(t, opts);
     launched_[b] = true;
+    if (side_) {
+      // widen back on the side stream right after the collective (Work::wait on a CUDA-like
+      // backend only makes the current stream wait for the communication stream)
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*side_);
+      works_[b]->wait();
+      widen(b);
+      TORCH_CHECK(hipEventRecord(events_[b], side_->stream()) == hipSuccess, "hipEventRecord");
+    }
   }
 
-  at::Tensor flat_;
+  // bf16 reduced slice -> fp32 master gradient slice (x post-scale for SUM backends)
+  void widen(size_t b) {
+    const int64_t lo = bounds_[b], hi = bounds_[b + 1];
+    const float scale = use_avg_ ? 1.f : (float)post_scale_;
+    if (flat_.is_cuda()) {
+      hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+      TORCH_CHECK(rtdc_bf16_to_f32(lp_.slice(0, lo, hi).data_ptr(), flat_.slice(0, lo, hi).data_ptr<float>(),
+                                   hi - lo, scale, st) == 0,
+                  "bf16->f32");
+    } else {
+      at::Tensor f = flat_.slice(0, lo, hi);
+      f.copy_(lp_.slice(0, lo, hi));
+      if (scale != 1.f) f.mul_(scale);
+    }
+  }
+
+  at::Tensor flat_, lp_;
+  c10::optional<c10::hip::HIPStreamMasqueradingAsCUDA> side_;
+  std::vector<hipEvent_t> events_;
   std::vector<int64_t> bounds_, param_bucket_, expected_, pending_;
   std::vector<std::pair<int64_t, int64_t>> seg_;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;

@@ -18,6 +18,11 @@ MI355X:
   of backward; the end-of-backward callback only makes the compute stream wait.
 * Averaging is folded into the collective (ReduceOp.AVG on RCCL - no divide kernel); gloo
   (CPU tests) uses SUM + one in-place scale of the flat buffer.
+* `grad_comm_dtype="bf16"` halves the bytes on xGMI: each ready bucket is rounded into a bf16
+  twin of the flat gradient buffer on the compute stream, all-reduced in bf16, and widened back
+  into the fp32 master gradients on a side stream as soon as its collective lands (the
+  compute stream waits for that stream once, at the end of backward).  `bucket_cap_mb` counts
+  communicated bytes, like torch DDP's bucket_cap_mb counts bytes of the gradient dtype.
 * With `defer_tail_to_optimizer`, backward returns with the LAST bucket's all-reduce still in
   flight (on RCCL): the fused optimizer steps every other parameter first and stream-waits for
   it only before the last slice, hiding the step's exposed collective tail (GPT-2: the tied
@@ -52,8 +57,12 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 2.0, broadcast_buffers: bool = True, device_ids=None,
                  output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 defer_tail_to_optimizer: bool = False):
+                 defer_tail_to_optimizer: bool = False, grad_comm_dtype: str = "fp32"):
         super().__init__()
+        if grad_comm_dtype not in ("fp32", "bf16"):
+            raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
+        self.grad_comm_dtype = grad_comm_dtype
+        self.bucket_cap_mb = bucket_cap_mb
         self.module = module
         # the last bucket's all-reduce stays in flight after backward; the fused optimizer
         # updates every other parameter first and waits for it only before the last bucket's
@@ -96,10 +105,11 @@ class DistributedDataParallel(nn.Module):
                 self._bufspace = (flat, list(zip(bufs, views)))
             if self.world_size > 1:
                 self._sync_buffers()
-        # static bucket plan over the flat gradient buffer
+        # static bucket plan over the flat gradient buffer (caps in communicated bytes)
         self.buckets: list[_Bucket] = []
-        cap = int(bucket_cap_mb * (1 << 20) / 4)
-        first_cap = int(first_bucket_mb * (1 << 20) / 4)
+        esz = 2 if grad_comm_dtype == "bf16" else 4
+        cap = int(bucket_cap_mb * (1 << 20) / esz)
+        first_cap = int(first_bucket_mb * (1 << 20) / esz)
         cur, cur_start, cur_end = [], None, 0
         for p, s in zip(self.space.params, self.space.segments):
             limit = first_cap if not self.buckets else cap
@@ -124,6 +134,9 @@ class DistributedDataParallel(nn.Module):
         self._engine = None
         self._check = os.environ.get("RTDC_COLLECTIVE_CHECK", "0") == "1"
         self._steps = 0
+        self._comm = None
+        if self.world_size > 1 and grad_comm_dtype == "bf16":
+            self._comm = torch.empty(self.space.numel, dtype=torch.bfloat16, device=dev)
         if self.world_size > 1:
             self._verify_plan_across_ranks()
             self._engine = self._native_engine(process_group)
@@ -164,7 +177,17 @@ class DistributedDataParallel(nn.Module):
         segs = [(s.offset, s.numel) for s in self.space.segments]
         pg = process_group if process_group is not None else dist.distributed_c10d._get_default_group()
         return mod.GradBucketEngine(self.space.grad, bounds, param_bucket, segs, pg, self._use_avg,
-                                    1.0 / self.world_size)
+                                    1.0 / self.world_size, self._comm)
+
+    def comm_plan(self) -> dict:
+        """Self-description of the gradient all-reduce (what a multi-GPU bench reports)."""
+        sizes = self.bucket_sizes_bytes()
+        return {"world_size": self.world_size, "grad_comm_dtype": self.grad_comm_dtype,
+                "bucket_cap_mb": self.bucket_cap_mb, "buckets": len(sizes),
+                "bucket_mb": [round(b / (1 << 20), 2) for b in sizes],
+                "allreduce_bytes_per_step": int(sum(sizes)),
+                "engine": "native" if self._engine is not None else "python",
+                "defer_tail_to_optimizer": self.defer_tail}
 
     # ------------------------------------------------------------------ buffers
     def _sync_buffers(self):
@@ -228,6 +251,10 @@ class DistributedDataParallel(nn.Module):
 
     def _launch(self, b: _Bucket):
         view = self.space.grad[b.start:b.end]
+        if self._comm is not None:
+            lp = self._comm[b.start:b.end]
+            lp.copy_(view)
+            view = lp
         op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
         b.work = dist.all_reduce(view, op=op, group=self.process_group, async_op=True)
         b.launched = True
@@ -256,6 +283,9 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
+                if self._comm is not None:
+                    with torch.no_grad():
+                        self.space.grad[b.start:b.end].copy_(self._comm[b.start:b.end])
             b.work = None
             b.launched = False
             b.pending = len(b.params)
@@ -271,4 +301,5 @@ class DistributedDataParallel(nn.Module):
         return super().state_dict(*args, **kwargs)
 
     def bucket_sizes_bytes(self):
-        return [(b.end - b.start) * 4 for b in self.buckets]
+        esz = 2 if self._comm is not None else 4
+        return [(b.end - b.start) * esz for b in self.buckets]

@@ -59,7 +59,14 @@ def main():
         dist.init_process_group(backend, store=pg_store, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=payload["timeout_s"]), **kw)
         ctx = S.TrainContext(world, rank, local, world, 0, payload["experiment_name"], payload["trial_dir"],
-                             payload["storage_path"], os.path.basename(payload["trial_dir"]), attempt)
+                             payload["storage_path"], os.path.basename(payload["trial_dir"]), attempt,
+                             torch_config=payload.get("torch_config"),
+                             checkpoint_config=payload["checkpoint_config"])
+        from ..checkpoint import torchsave
+
+        cc = payload["checkpoint_config"]
+        if hasattr(cc, "ring_slots"):  # size the native engine's pinned ring from the typed config
+            torchsave.configure_engine(cc.ring_slots, cc.ring_slot_mb, cc.writer_threads)
         resume = payload.get("resume_checkpoint")
         sess = S._Session(ctx, store, payload["checkpoint_config"], Checkpoint(resume) if resume else None)
         fail_at = os.environ.get("RTDC_FAIL_AT_REPORT")

@@ -34,12 +34,26 @@ class CheckpointConfig:
     checkpoint_score_order: str = "max"
     checkpoint_frequency: int = 0
     checkpoint_at_end: Optional[bool] = None
+    # MI355X-native knobs of the sharded checkpoint engine
+    ckpt_every_n_steps: Optional[int] = None  # step-granular sharded saves (workload loops)
+    async_checkpoint: bool = True             # HBM snapshot + background write + background commit
+    pinned_ring_mb: int = 512                 # bounded pinned-host ring per rank (D2H staging)
+    ring_slot_mb: int = 64                    # ring slot = unit of one D2H copy / pwrite
+    writer_threads: int = 0                   # 0 = min(8, max(2, ncpu // 2))
 
     def __post_init__(self):
         if self.num_to_keep is not None and self.num_to_keep <= 0:
             raise ValueError("num_to_keep must be a positive integer or None")
         if self.checkpoint_score_order not in ("max", "min"):
             raise ValueError("checkpoint_score_order must be 'max' or 'min'")
+        if self.ckpt_every_n_steps is not None and self.ckpt_every_n_steps <= 0:
+            raise ValueError("ckpt_every_n_steps must be a positive integer or None")
+        if self.pinned_ring_mb < self.ring_slot_mb or self.ring_slot_mb <= 0:
+            raise ValueError("pinned_ring_mb must hold at least one ring slot (ring_slot_mb > 0)")
+
+    @property
+    def ring_slots(self) -> int:
+        return max(1, self.pinned_ring_mb // self.ring_slot_mb)
 
 
 @dataclass
@@ -61,9 +75,12 @@ class RunConfig:
     stop: Any = None
     callbacks: Any = None
     log_to_file: bool = False
-    # MI355X-native knobs
-    worker_timeout_s: float = 1800.0  # process-group timeout (Ray TorchConfig default)
-    heartbeat_timeout_s: float = 600.0
+    # MI355X-native knobs (failure detection)
+    heartbeat_timeout_s: float = 600.0       # a worker process stopped heart-beating (host hang)
+    # a worker that published a step counter (train.report_progress / report) and then did not
+    # advance it for this long is stalled - e.g. stuck in a collective whose peer died or hung,
+    # which the heartbeat thread cannot see.  None disables the check.
+    progress_timeout_s: Optional[float] = 300.0
 
     def resolved_storage_path(self) -> str:
         p = self.storage_path or os.environ.get("RTDC_STORAGE_PATH") or os.path.join("~", "rtdc_results")
@@ -72,6 +89,27 @@ class RunConfig:
 
 @dataclass
 class TorchConfig:
+    """Process-group backend + data-parallel engine knobs (Ray's TorchConfig, extended).
+
+    bucket_cap_mb / first_bucket_mb: gradient bucket plan (parallel/ddp.py has the xGMI sizing
+    rationale and profiles/ the sweep); grad_comm_dtype: "fp32" (torch DDP semantics) or "bf16"
+    (gradients rounded to bf16 for the all-reduce - half the xGMI bytes - and widened back into
+    the fp32 master gradients on a side stream); timeout_s: process-group collective timeout."""
     backend: Optional[str] = None  # None -> "nccl" (RCCL) with GPUs, "gloo" on CPU
     init_method: str = "env"
     timeout_s: int = 1800
+    bucket_cap_mb: float = 32.0
+    first_bucket_mb: float = 2.0
+    grad_comm_dtype: str = "fp32"
+    # leave the last bucket's all-reduce in flight after backward; only valid with this
+    # framework's fused optimizers (they wait for it before its slice) - stock torch optimizers
+    # would read that slice un-reduced, so it is off unless the training loop opts in
+    defer_tail_to_optimizer: bool = False
+
+    def __post_init__(self):
+        if self.grad_comm_dtype not in ("fp32", "bf16"):
+            raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
+
+    def ddp_kwargs(self) -> dict:
+        return dict(bucket_cap_mb=self.bucket_cap_mb, first_bucket_mb=self.first_bucket_mb,
+                    grad_comm_dtype=self.grad_comm_dtype, defer_tail_to_optimizer=self.defer_tail_to_optimizer)

@@ -8,6 +8,10 @@ torch.distributed rendezvous (RCCL unique-id exchange / gloo) and the control pl
 * a worker exiting non-zero, publishing an error, or missing heartbeats for
   `heartbeat_timeout_s` fails the attempt; every surviving worker of the gang is killed
   (SIGKILL to its process group - a partially failed RCCL communicator cannot recover);
+* a worker whose training-thread step counter (`train.report_progress`, `report`) stops
+  advancing for `progress_timeout_s` fails the attempt the same way: this catches a rank
+  stuck inside a collective (a dead or hung peer), which the heartbeat thread keeps hiding
+  until the 30-minute process-group timeout;
 * up to `FailureConfig.max_failures` restarts, each resuming from the latest committed
   checkpoint of the same trial (Ray FailureConfig semantics; SURVEY §5.3);
 * fault injection for tests: env `RTDC_FAIL_AT_REPORT=K[:rank]` makes a worker SIGKILL itself
@@ -68,6 +72,9 @@ class WorkerGroup:
                 "RTDC_STORE_PORT": str(self.port), "RTDC_ATTEMPT": str(attempt), "RTDC_PAYLOAD": payload_path,
             })
             env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            # one intra-op thread pool per worker must not oversubscribe the host (gloo ranks
+            # busy-poll): split the CPUs between the ranks unless the user chose
+            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // self.n)))
             # workers import the user's modules (cloudpickle pickles module functions by
             # reference) and this package exactly as the driver does
             pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -93,10 +100,13 @@ class WorkerGroup:
             except subprocess.TimeoutExpired:
                 pass
 
-    def supervise(self, attempt: int, heartbeat_timeout_s: float, on_report=None) -> AttemptOutcome:
+    def supervise(self, attempt: int, heartbeat_timeout_s: float, on_report=None,
+                  progress_timeout_s: float | None = None) -> AttemptOutcome:
         out = AttemptOutcome(ok=False)
         seen = 0
         t_start = time.time()
+        t_prog_check = 0.0
+        self._progress = {}  # rank -> (step, host time the step last changed)
         try:
             while True:
                 n = self.store.add(f"a{attempt}/nreports", 0)
@@ -123,6 +133,17 @@ class WorkerGroup:
                             on_report(msg)
                     out.ok = True
                     return out
+                now = time.time()
+                if progress_timeout_s and now - t_prog_check >= min(1.0, progress_timeout_s / 4):
+                    t_prog_check = now
+                    stalled = self._stalled_rank(attempt, progress_timeout_s, now)
+                    if stalled is not None:
+                        r, step = stalled
+                        out.error = (f"worker rank {r} made no training progress for {progress_timeout_s}s "
+                                     f"(stuck at step {step}: hung collective or kernel?)")
+                        out.failed_rank = r
+                        self.kill_all()
+                        return out
                 if heartbeat_timeout_s and time.time() - t_start > heartbeat_timeout_s:
                     stale = self._stale_rank(attempt, heartbeat_timeout_s)
                     if stale is not None:
@@ -134,6 +155,28 @@ class WorkerGroup:
         except BaseException:
             self.kill_all()
             raise
+
+    def _stalled_rank(self, attempt, timeout, now):
+        """First rank whose published step counter has not changed for `timeout` seconds
+        (ranks that never published, or finished, are not watched)."""
+        for r in range(self.n):
+            key = f"a{attempt}/prog/{r}"
+            try:
+                if not self.store.check([key]):
+                    continue
+                v = self.store.get(key).decode()
+            except Exception:
+                continue
+            if v == "done":
+                self._progress.pop(r, None)
+                continue
+            step = int(v.split()[0])
+            prev = self._progress.get(r)
+            if prev is None or prev[0] != step:
+                self._progress[r] = (step, now)
+            elif now - prev[1] > timeout:
+                return r, step
+        return None
 
     def _stale_rank(self, attempt, timeout):
         now = time.time()

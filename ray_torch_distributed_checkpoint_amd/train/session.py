@@ -13,17 +13,30 @@ Reference call sites: `ray.train.get_context().get_world_size()/get_world_rank()
      enforces `num_to_keep`, publishes the metrics to the driver;
   4. barrier - the report call synchronises workers like Ray's.
 Asynchronous (sharded DCP) checkpoints skip step 1: shards are written by the native
-engine straight into the staging dir and a background committer runs steps 2-3 once every
-rank's write is durable, so `report` returns immediately.
+engine straight into the staging dir (`get_context().next_checkpoint_dir()`) and a background
+committer runs steps 2-3 once every rank's write is durable, so `report` returns immediately;
+the driver learns the checkpoint path only after that commit.  The stage / write / commit
+seconds of each async checkpoint are attached to the next reported metrics row
+(`ckpt_stage_s`, `ckpt_write_s`, `ckpt_commit_s`, `ckpt_index`).
+
+Progress and fault injection: `report_progress(step)` publishes a monotone step
+counter from the TRAINING thread (rate-limited TCPStore writes), which the supervisor watches
+for stalls - unlike the heartbeat thread, it stops when the training thread is stuck in a
+collective.  It is also the step-granular fault-injection point (first attempt only):
+  RTDC_FAIL_AT_STEP=K[:rank]  SIGKILL at the start of step K,
+  RTDC_HANG_AT_STEP=K[:rank]  block forever at the start of step K (peers then hang in their
+                              next collective: a real collective stall).
 """
 from __future__ import annotations
 
 import json
 import os
 import queue
+import signal
 import threading
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
+from typing import Any
 
 from . import storage
 from .checkpoint import Checkpoint
@@ -61,6 +74,19 @@ class TrainContext:
     storage_path: str
     trial_name: str
     attempt: int = 0
+    torch_config: Any = None
+    checkpoint_config: Any = None
+    run_config: Any = field(default=None, repr=False)
+
+    def get_torch_config(self):
+        from .config import TorchConfig
+
+        return self.torch_config or TorchConfig()
+
+    def get_checkpoint_config(self):
+        from .config import CheckpointConfig
+
+        return self.checkpoint_config or CheckpointConfig()
 
     def get_world_size(self):
         return self.world_size
@@ -115,6 +141,43 @@ class _Session:
         self._committer = None
         self._commit_err = None
         self.last_metrics = None
+        self._ckpt_timing: dict = {}  # timings of the last completed async checkpoint
+        self._timing_lock = threading.Lock()
+        # progress publishing + fault injection
+        self._prog_key = f"a{ctx.attempt}/prog/{ctx.world_rank}"
+        self._prog_last = 0.0
+        self._prog_step = -1
+        self._fail_at = self._parse_injector("RTDC_FAIL_AT_STEP")
+        self._hang_at = self._parse_injector("RTDC_HANG_AT_STEP")
+
+    def _parse_injector(self, var):
+        v = os.environ.get(var)
+        if not v or self.ctx.attempt != 0:
+            return None
+        k, _, r = v.partition(":")
+        if r and int(r) != self.ctx.world_rank:
+            return None
+        return int(k)
+
+    # ------------------------------------------------------------------ progress
+    def report_progress(self, step: int, force: bool = False):
+        if self._fail_at is not None and step >= self._fail_at:
+            os.kill(os.getpid(), signal.SIGKILL)
+        if self._hang_at is not None and step >= self._hang_at:
+            self._publish_progress(step)
+            threading.Event().wait()  # never returns: the gang is killed by the supervisor
+        self._prog_step = max(self._prog_step, int(step))
+        now = time.time()
+        if force or now - self._prog_last >= 1.0:
+            self._publish_progress(self._prog_step, now)
+
+    def _publish_progress(self, step, now=None):
+        now = now or time.time()
+        self._prog_last = now
+        try:
+            self.store.set(self._prog_key, f"{step} {now}")
+        except Exception:
+            pass
 
     # ------------------------------------------------------------------ report
     def report(self, metrics: dict, checkpoint: Checkpoint | None = None):
@@ -126,6 +189,16 @@ class _Session:
         stage = storage.staging_dir(self.ctx.trial_dir, self.next_index)
         is_async = checkpoint is not None and (
             checkpoint._pending is not None or os.path.abspath(checkpoint.path) == os.path.abspath(stage))
+        if is_async and os.path.abspath(checkpoint.path) != os.path.abspath(stage):
+            # an in-place (async) checkpoint must have been written into the directory this
+            # report commits; anything else would commit an empty staging dir
+            raise ValueError(f"async checkpoint written to {checkpoint.path}, but this report commits {stage}: "
+                             f"save into train.get_context().next_checkpoint_dir()")
+        self._publish_progress(self._prog_step)
+        with self._timing_lock:
+            if self._ckpt_timing:
+                metrics = dict(metrics, **self._ckpt_timing)
+                self._ckpt_timing = {}
         if checkpoint is not None:
             self.store.add(key + "/ck", 1)
         if is_async:
@@ -155,14 +228,16 @@ class _Session:
         if rank == 0:
             row = self.logger.log(metrics, idx)
             self.last_metrics = row
-            self._publish(row, None if idx is None else storage.final_dir(self.ctx.trial_dir, idx))
+            # an async checkpoint is announced by the committer once it is committed
+            done = idx is not None and not any_async
+            self._publish({"type": "report", "metrics": row,
+                           "checkpoint": storage.final_dir(self.ctx.trial_dir, idx) if done else None})
         self.barrier.wait(f"r{n}d")
         self.n_reports += 1
 
-    def _publish(self, row, ckpt_path):
-        msg = json.dumps({"metrics": row, "checkpoint": ckpt_path}, default=str)
+    def _publish(self, msg: dict):
         k = self.store.add(f"a{self.ctx.attempt}/nreports", 1)
-        self.store.set(f"a{self.ctx.attempt}/report/{k}", msg)
+        self.store.set(f"a{self.ctx.attempt}/report/{k}", json.dumps(msg, default=str))
 
     # ------------------------------------------------------------------ async commits
     def _enqueue_commit(self, idx, checkpoint, metrics):
@@ -178,8 +253,14 @@ class _Session:
                 return
             idx, ck, metrics = item
             try:
+                t_q = time.perf_counter()
+                h = getattr(ck, "_handle", None) if ck is not None else None
                 if ck is not None:
                     ck.wait()  # this rank's shard files durable
+                timing = {"ckpt_index": idx}
+                if h is not None and getattr(h, "t_return", None) is not None:
+                    timing["ckpt_stage_s"] = round(h.t_return, 6)
+                    timing["ckpt_write_s"] = round(h.write_s if h.write_s is not None else 0.0, 6)
                 key = f"s{self.ctx.attempt}/commit/{idx}"
                 self.store.add(key, 1)
                 if self.ctx.world_rank == 0:
@@ -188,12 +269,20 @@ class _Session:
                         if time.time() - t0 > 3600:
                             raise TimeoutError("async checkpoint commit barrier timed out")
                         time.sleep(0.002)
+                    t_c = time.perf_counter()
                     if ck is not None and hasattr(ck, "_finish"):
                         ck._finish()  # rank-0 metadata write (DCP .metadata)
-                    os.makedirs(storage.staging_dir(self.ctx.trial_dir, idx), exist_ok=True)
+                    stage = storage.staging_dir(self.ctx.trial_dir, idx)
+                    if not os.path.isdir(stage):
+                        raise FileNotFoundError(f"async checkpoint staging dir {stage} missing at commit")
                     path = storage.commit(self.ctx.trial_dir, idx)
                     self.logger.register(idx, path, metrics)
+                    timing["ckpt_commit_s"] = round(time.perf_counter() - t_c, 6)
+                    timing["ckpt_durable_s"] = round(time.perf_counter() - t_q + timing.get("ckpt_stage_s", 0.0), 6)
                     self.store.set(f"s{self.ctx.attempt}/committed/{idx}", path)
+                    self._publish({"type": "commit", "index": idx, "checkpoint": path})
+                with self._timing_lock:
+                    self._ckpt_timing = timing
             except BaseException as e:  # surfaced on the next report / at shutdown
                 self._commit_err = e
             finally:
@@ -203,8 +292,6 @@ class _Session:
         """Wait for every queued async checkpoint to be committed."""
         if self._committer is not None:
             self._commit_q.join()
-            if self.ctx.world_rank == 0:
-                pass
         if self._commit_err:
             raise self._commit_err
 
@@ -212,6 +299,10 @@ class _Session:
         self.flush()
         if self._committer is not None:
             self._commit_q.put(None)
+        try:
+            self.store.set(self._prog_key, "done")
+        except Exception:
+            pass
 
 
 _session: _Session | None = None
@@ -241,6 +332,15 @@ def get_context() -> TrainContext:
                             int(os.environ.get("LOCAL_WORLD_SIZE", str(ws))), int(os.environ.get("NODE_RANK", "0")),
                             "", "", "", "")
     return s.ctx
+
+
+def report_progress(step: int) -> None:
+    """Publish the training step counter to the supervisor (stall detection) - cheap enough to
+    call every step; also where RTDC_FAIL_AT_STEP / RTDC_HANG_AT_STEP fire.  No-op outside a
+    trainer."""
+    s = _get_session(required=False)
+    if s is not None:
+        s.report_progress(step)
 
 
 def get_checkpoint() -> Checkpoint | None:

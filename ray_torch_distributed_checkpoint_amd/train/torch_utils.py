@@ -41,7 +41,11 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True, parallel_
         model = model.to(dev)
     ws = dist.get_world_size() if dist.is_initialized() else 1
     if ws > 1 and parallel_strategy in ("ddp", None):
-        model = DistributedDataParallel(model, **(parallel_strategy_kwargs or {}))
+        # bucket plan / comm dtype / tail deferral come from the trainer's TorchConfig
+        # (typed knobs); explicit kwargs win
+        kw = dict(get_context().get_torch_config().ddp_kwargs())
+        kw.update(parallel_strategy_kwargs or {})
+        model = DistributedDataParallel(model, **kw)
     elif parallel_strategy not in ("ddp", None):
         raise NotImplementedError(f"parallel_strategy={parallel_strategy!r} (only data parallel is provided)")
     return model

@@ -67,12 +67,17 @@ class TorchTrainer:
         errors = []
 
         def on_report(msg):
-            last["metrics"] = msg["metrics"]
             if msg.get("checkpoint"):
                 last["checkpoint"] = msg["checkpoint"]
+            if msg.get("type") == "commit":
+                if self.run.verbose:
+                    print(f"[rtdc] committed {msg['checkpoint']}", flush=True)
+                return
+            last["metrics"] = msg["metrics"]
             if self.run.verbose:
                 m = {k: v for k, v in msg["metrics"].items()
-                     if k in ("training_iteration", "val_loss", "accuracy", "loss", "time_total_s")}
+                     if k in ("training_iteration", "step", "val_loss", "accuracy", "loss", "samples_per_s",
+                              "time_total_s")}
                 print(f"[rtdc] report {m}", flush=True)
 
         attempts = fail_cfg.max_failures + 1 if fail_cfg.max_failures >= 0 else 10 ** 9
@@ -83,12 +88,13 @@ class TorchTrainer:
                 "fn": self.fn, "config": self.config, "use_gpu": self.scaling.use_gpu,
                 "backend": self.torch_config.backend, "timeout_s": self.torch_config.timeout_s,
                 "experiment_name": exp, "trial_dir": trial_dir, "storage_path": root,
-                "checkpoint_config": ck_cfg, "resume_checkpoint": resume,
+                "checkpoint_config": ck_cfg, "resume_checkpoint": resume, "torch_config": self.torch_config,
             }
             ppath = write_payload(payload)
             try:
                 group.start(ppath, attempt)
-                outcome = group.supervise(attempt, self.run.heartbeat_timeout_s, on_report)
+                outcome = group.supervise(attempt, self.run.heartbeat_timeout_s, on_report,
+                                          self.run.progress_timeout_s)
             finally:
                 shutil.rmtree(os.path.dirname(ppath), ignore_errors=True)
             if outcome.ok:

@@ -8,7 +8,11 @@ Same flags, defaults and step graph (start -> train (gang of N_PARALLEL) -> join
 the reference.  `current.ray_storage_path` is the per-task checkpoint root handed to
 RunConfig(storage_path=...); `--from-task` takes precedence over `--from-run`; the string
 "null" means unset.  Added (optional): --resume_mode best_weights|exact, --num_workers,
---max_failures.
+--max_failures, and the bf16 DDP workloads of BASELINE.json (configs 2-5) through the same
+trainer / storage layout / --from-run path:
+    python train_flow.py run --model gpt2-small --steps 200 --ckpt_every_n_steps 50
+    python train_flow.py run --model gpt2-small --steps 400 --from-run RayTorchTrain/<id> --resume_mode exact
+(--model resnet18 | llama3-8b | *-tiny; sharded DCP checkpoints every N steps, async.)
 """
 from ray_torch_distributed_checkpoint_amd.flow import (FlowSpec, Parameter, Run, Task, current, gpu_profile,
                                                        kubernetes, metaflow_ray, pypi, retry, schedule, step)
@@ -37,6 +41,11 @@ class RayTorchTrain(FlowSpec):
                             help="best_weights (reference warm start) or exact (optimizer/epoch/RNG/sampler).")
     num_workers = Parameter("num_workers", default=0, help="0 = N_PARALLEL*N_GPU_PER_WORKER capped by visible GPUs")
     max_failures = Parameter("max_failures", default=0, help="in-trainer restarts from the latest checkpoint")
+    model = Parameter("model", default="mlp",
+                      help="mlp (the reference workload) | gpt2-small | resnet18 | llama3-8b | gpt2-tiny | ...")
+    steps = Parameter("steps", default=100, help="optimizer steps (bf16 workloads)")
+    ckpt_every_n_steps = Parameter("ckpt_every_n_steps", default=25, help="sharded async checkpoint interval")
+    grad_comm_dtype = Parameter("grad_comm_dtype", default="fp32", help="fp32 | bf16 gradient all-reduce")
 
     @step
     def start(self):
@@ -52,6 +61,8 @@ class RayTorchTrain(FlowSpec):
         import torch
 
         from my_ray_module import train_fashion_mnist
+
+        from ray_torch_distributed_checkpoint_amd.workloads import train_workload
 
         use_gpu = torch.cuda.is_available()
         n = int(self.num_workers) or N_PARALLEL * N_GPU_PER_WORKER
@@ -79,7 +90,16 @@ class RayTorchTrain(FlowSpec):
         else:
             print("Training from newly initialized")
 
-        self.result = train_fashion_mnist(**args)
+        if self.model == "mlp":
+            self.result = train_fashion_mnist(**args)
+        else:
+            mode = "exact" if self.resume_mode == "exact" else "weights"
+            self.result = train_workload(
+                model=self.model, steps=int(self.steps), num_workers=n, use_gpu=use_gpu,
+                batch_size_per_worker=max(1, int(self.global_batch_size) // n) if int(self.global_batch_size) != 32
+                else None, lr=None, ckpt_every_n_steps=int(self.ckpt_every_n_steps),
+                checkpoint_storage_path=current.ray_storage_path, checkpoint=args.get("checkpoint"),
+                resume_mode=mode, max_failures=int(self.max_failures), grad_comm_dtype=self.grad_comm_dtype)
         self.next(self.join)
 
     @step
