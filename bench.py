@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--grad-comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce dtype (fp32 = torch DDP semantics)")
     ap.add_argument("--no-ckpt", action="store_true")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-scope", default="full", choices=["full", "model"],
@@ -100,8 +102,8 @@ def main():
     model, opt = wl["model"], wl["opt"]
     # the last bucket's all-reduce (GPT-2: the tied token table, whose gradient completes at the
     # end of backward) overlaps the fused optimizer's update of every other parameter
-    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, defer_tail_to_optimizer=True) \
-        if world > 1 else model
+    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, defer_tail_to_optimizer=True,
+                                  grad_comm_dtype=args.grad_comm_dtype) if world > 1 else model
     B, T = wl["batch"], wl["seq_len"]
     fwd_loss = wl["loss"]
 
@@ -162,12 +164,28 @@ def main():
     }
     if wl.get("tokens_per_sample"):
         out["tokens_per_sec"] = round(samples_per_s * wl["tokens_per_sample"], 1)
+    # self-description of the communication setup (what ran, on how many ranks)
+    comm = {"world_size": world, "backend": (dist.get_backend() if world > 1 else None),
+            "rccl_version": _rccl_version(), "device": torch.cuda.get_device_name(dev)}
+    if world > 1:
+        comm.update(net.comm_plan())
+        comm["allreduce_GB_per_s_needed_at_this_step_time"] = round(
+            comm["allreduce_bytes_per_step"] * 2 * (world - 1) / world / (ms_per_step / 1e3) / 1e9, 2)
+    out["comm"] = comm
     out.update(ck)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return None
 
 
 def build_workload(args, dev, rank):

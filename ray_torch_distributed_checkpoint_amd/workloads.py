@@ -187,8 +187,8 @@ def build(cfg: WorkloadConfig, device) -> Workload:
     if name.startswith("resnet18"):
         from .models import ResNet18
 
-        widths = (8, 16, 32, 64) if name.endswith("tiny") else (64, 128, 256, 512)
-        model = ResNet18(num_classes=cfg.num_classes, widths=widths).to(device)
+        # "-tiny" = the full network on 32x32 images (the GEMM tiles need >= 64 channels)
+        model = ResNet18(num_classes=cfg.num_classes).to(device)
         opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
         data = SyntheticImages(cfg.dataset_size, S, cfg.num_classes, device, seed=cfg.seed)
         return Workload(model, opt, data, B, S, 0, model.flops_per_sample(S),

@@ -1,0 +1,160 @@
+"""Data-parallel gradient engine on the GPU (bf16 GPT-2-tiny on the native kernels).
+
+* Multi-process DDP gradients (flat buckets, C++ engine, fp32 or bf16 communication) equal
+  the single-process gradient of the concatenated batch.  With >= 2 GPUs this runs over RCCL
+  (one rank per GPU); on a 1-GPU box the same engine runs with two gloo ranks sharing cuda:0,
+  which exercises the GPU side of the engine (bf16 rounding kernel, side-stream widening,
+  event ordering) without RCCL.
+* The bf16-workload trainer loop on one GPU: kill at step K, restart, bit-equal losses.
+"""
+import json
+import os
+import socket
+import sys
+import traceback
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+B, T = 2, 64
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model(dev):
+    from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+
+    torch.manual_seed(0)
+    return GPT2(GPT2Config.named("gpt2-tiny")).to(dev)
+
+
+def _batch(world, dev):
+    g = torch.Generator().manual_seed(7)
+    return torch.randint(0, 1000, (world * B, T + 1), generator=g).to(dev)
+
+
+def _worker(rank, world, port, backend, comm_dtype, q):
+    try:
+        import torch.distributed as dist
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        ngpu = torch.cuda.device_count()
+        dev = torch.device("cuda", rank % ngpu)
+        torch.cuda.set_device(dev)
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+        model = _model(dev)
+        net = DistributedDataParallel(model, grad_comm_dtype=comm_dtype, bucket_cap_mb=0.25, first_bucket_mb=0.05)
+        data = _batch(world, dev)[rank * B:(rank + 1) * B]
+        for _ in range(2):  # second step: buckets reused, fresh-gradient mode
+            net.space.zero_grad(set_to_none=True)
+            loss = net(data[:, :-1], data[:, 1:])
+            loss.backward()
+        torch.cuda.synchronize()
+        # numpy, not tensors: a torch.multiprocessing queue would pass shared-memory fds that
+        # die with this process
+        grads = {n: p.grad.detach().float().cpu().numpy() for n, p in model.named_parameters()}
+        q.put((rank, "ok", (grads, len(net.buckets), net.comm_plan())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _run(world, backend, comm_dtype):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, backend, comm_dtype, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, st, v = q.get(timeout=240)
+            assert st == "ok", v
+            out[r] = v
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+def _reference(world):
+    dev = torch.device("cuda", 0)
+    model = _model(dev)
+    from ray_torch_distributed_checkpoint_amd.optim import FlatParamSpace
+
+    FlatParamSpace(list(reversed(list(model.parameters()))))  # same flat-gradient path as DDP
+    data = _batch(world, dev)
+    loss = model(data[:, :-1], data[:, 1:])
+    loss.backward()
+    return {n: p.grad.detach().float().cpu() for n, p in model.named_parameters()}
+
+
+def _check(out, ref, tol):
+    g0 = {n: torch.from_numpy(v) for n, v in out[0][0].items()}
+    for r in out:  # every rank holds the same averaged gradient
+        for n in g0:
+            assert torch.equal(torch.from_numpy(out[r][0][n]), g0[n]), f"rank {r} differs on {n}"
+    assert out[0][1] > 3  # really bucketed
+    for n, v in ref.items():
+        err = (g0[n] - v).norm() / v.norm().clamp_min(1e-12)
+        assert err < tol, f"{n}: relative error {err:.3e}"
+
+
+@pytest.mark.parametrize("comm_dtype,tol", [("fp32", 2e-2), ("bf16", 3e-2)])
+def test_ddp_gloo_two_ranks_on_gpu_matches_concatenated_batch(comm_dtype, tol):
+    out = _run(2, "gloo", comm_dtype)
+    assert out[0][2]["grad_comm_dtype"] == comm_dtype
+    _check(out, _reference(2), tol)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL DDP needs >= 2 GPUs (one rank per GPU)")
+@pytest.mark.parametrize("comm_dtype,tol", [("fp32", 2e-2), ("bf16", 3e-2)])
+def test_ddp_rccl_matches_concatenated_batch(comm_dtype, tol):
+    world = min(torch.cuda.device_count(), 4)
+    out = _run(world, "nccl", comm_dtype)
+    _check(out, _reference(world), tol)
+
+
+def _losses(path):
+    out = {}
+    for line in open(os.path.join(path, "result.json")):
+        row = json.loads(line)
+        for i, v in enumerate(reversed(row["losses"])):
+            k = row["step"] - i
+            assert out.get(k, v) == v
+            out[k] = v
+    return out
+
+
+@pytest.mark.parametrize("model", ["gpt2-tiny", "resnet18-tiny"])
+def test_workload_trainer_kill_restart_bit_equal_gpu(tmp_path, monkeypatch, model):
+    from ray_torch_distributed_checkpoint_amd import workloads as W
+
+    for k in ("RTDC_FAIL_AT_STEP", "RTDC_HANG_AT_STEP", "RTDC_FORCE_CPU"):
+        monkeypatch.delenv(k, raising=False)
+    kw = dict(steps=6, num_workers=1, use_gpu=True, ckpt_every_n_steps=2, verbose=0)
+    a = W.train_workload(model, checkpoint_storage_path=str(tmp_path / "a"), **kw)
+    monkeypatch.setenv("RTDC_FAIL_AT_STEP", "3")
+    b = W.train_workload(model, checkpoint_storage_path=str(tmp_path / "b"), max_failures=1, **kw)
+    la, lb = _losses(a.path), _losses(b.path)
+    assert sorted(la) == list(range(1, 7))
+    assert la == lb
+    files = sorted(os.listdir(b.checkpoint.path))
+    assert files == [".metadata", "__0_0.distcp"]
