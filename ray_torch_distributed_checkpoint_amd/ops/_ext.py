@@ -69,3 +69,12 @@ def gpu_ext():
 def use_native(t: torch.Tensor) -> bool:
     """True when `t` lives on the GPU: the op must run its HIP kernel."""
     return t.is_cuda
+
+
+def require_dtype(t: torch.Tensor, op: str, allowed=(torch.bfloat16,)) -> None:
+    """GPU tensors must be in a dtype the native kernel implements: raise instead of falling
+    back to MIOpen / SDPA / ATen (the GPU path runs the HIP kernels or nothing)."""
+    if t.dtype not in allowed:
+        names = "/".join(str(d).replace("torch.", "") for d in allowed)
+        raise TypeError(f"{op}: the native gfx950 kernel takes {names} GPU tensors, got {t.dtype} "
+                        f"(cast explicitly; there is no silent eager fallback on the GPU)")

@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import gemm as G
-from ._ext import gpu_ext
+from ._ext import gpu_ext, require_dtype
 
 
 def _qkv_layout(B, T, H, Hkv, Dh):
@@ -154,7 +154,9 @@ def causal_attention(qkv: torch.Tensor, n_head: int, n_kv_head: int | None = Non
     B, T, W = qkv.shape
     Hkv = n_kv_head or n_head
     Dh = W // (n_head + 2 * Hkv)
-    if not qkv.is_cuda or qkv.dtype != torch.bfloat16:
+    if qkv.is_cuda:
+        require_dtype(qkv, "causal_attention")
+    else:
         return causal_attention_ref(qkv, B, T, n_head, Hkv, Dh)
     impl = os.environ.get("RTDC_ATTN", "flash")
     if impl == "flash" and flash_supported(T, Dh):

@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 
 from . import gemm as G
-from ._ext import gpu_ext
+from ._ext import gpu_ext, require_dtype
 from .gradbuf import grad_target
 from .shadow import shadow_of
 
@@ -169,7 +169,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, bn_s
     """NHWC convolution (no bias): x [B, H, W, Cin] -> [B, Ho, Wo, Cout]; w [Cout, Cin, KH, KW].
     bn_stats=True also computes the per-channel BatchNorm statistics of the output inside the
     GEMM epilogue; `batch_norm` on exactly this tensor then skips its statistics pass."""
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "conv2d")
+    else:
         return conv2d_ref(x, w, stride, pad)
     y = _Conv2d.apply(x, w, stride, pad, bn_stats)
     st = getattr(y.grad_fn, "stats", None) if y.grad_fn is not None else None
@@ -248,7 +250,9 @@ def batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentu
 def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
                eps: float = 1e-5, residual=None, relu: bool = False) -> torch.Tensor:
     """y = relu?(BN(x) (+ residual)) over the channel (last) axis of an NHWC tensor."""
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "batch_norm")
+    else:
         return batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
     return _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu)
 
@@ -276,7 +280,9 @@ class _MaxPool(torch.autograd.Function):
 
 
 def max_pool2d(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "max_pool2d")
+    else:
         return F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous()
     return _MaxPool.apply(x, k, s, p)
 
@@ -300,7 +306,9 @@ class _AvgPool(torch.autograd.Function):
 
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     """[B, H, W, C] -> [B, C] mean over the spatial axes."""
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "global_avg_pool")
+    else:
         return x.float().mean(dim=(1, 2)).to(x.dtype)
     return _AvgPool.apply(x)
 
@@ -344,6 +352,8 @@ class _Classifier(torch.autograd.Function):
 
 
 def classifier(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "classifier")
+    else:
         return F.linear(x, w.to(x.dtype), b.to(x.dtype))
     return _Classifier.apply(x, w, b)

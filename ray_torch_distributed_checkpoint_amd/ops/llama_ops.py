@@ -5,7 +5,7 @@ import torch
 import torch.nn.functional as F
 
 from . import gemm as G
-from ._ext import gpu_ext
+from ._ext import gpu_ext, require_dtype
 from .gradbuf import grad_target
 from .shadow import shadow_of
 
@@ -58,7 +58,9 @@ class _RoPE(torch.autograd.Function):
 
 
 def apply_rope(qkv: torch.Tensor, n_head: int, n_kv_head: int, theta: float = 500000.0) -> torch.Tensor:
-    if not qkv.is_cuda or qkv.dtype != torch.bfloat16:
+    if qkv.is_cuda:
+        require_dtype(qkv, "apply_rope")
+    else:
         return rope_ref(qkv, n_head, n_kv_head, theta)
     return _RoPE.apply(qkv, n_head, n_kv_head, theta)
 
@@ -103,7 +105,9 @@ class _SwiGLUMLP(torch.autograd.Function):
 
 
 def swiglu_mlp(x, w13, w2, residual=None):
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "swiglu_mlp")
+    else:
         gu = F.linear(x, w13.to(x.dtype))
         g, u = gu.chunk(2, dim=-1)
         y = F.linear(F.silu(g) * u, w2.to(x.dtype))

@@ -7,7 +7,7 @@ import torch
 import torch.nn.functional as F
 
 from . import gemm as G
-from ._ext import gpu_ext
+from ._ext import gpu_ext, require_dtype
 from .gradbuf import grad_target
 from .shadow import shadow_of
 
@@ -117,14 +117,18 @@ def layer_norm(x, w, b, eps=1e-5, passthrough=False, grad_sum_into=None):
     """LayerNorm over the last axis; passthrough=True returns (y, x) with the residual-stream
     gradient fused into the backward kernel.  grad_sum_into: the bias of the projection that
     produced x; its gradient (= column sums of dx) is then reduced by the backward kernel."""
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "layer_norm")
+    else:
         y = F.layer_norm(x, (x.shape[-1],), w.to(x.dtype), b.to(x.dtype), eps)
         return (y, x) if passthrough else y
     return _LayerNorm.apply(x, w, b, eps, passthrough, grad_sum_into)
 
 
 def rms_norm(x, w, eps=1e-5, passthrough=False):
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if x.is_cuda:
+        require_dtype(x, "rms_norm")
+    else:
         xf = x.float()
         y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
         y = (y * w.float()).to(x.dtype)

@@ -76,3 +76,51 @@ def test_gpt2_checkpoint_resume_bit_equal(tmp_path):
     got = [step(model2, opt2, i) for i in range(K, 8)]
     for r, g in zip(ref, got):
         assert torch.equal(r, g), (ref, got)
+
+
+def test_toy_hipgraph_step_equals_eager_gpu(tmp_path, monkeypatch):
+    """The captured toy step (one hipGraph launch per batch) trains bit-identically to the
+    eager native step: same kernels, same Philox dropout counters."""
+    import my_ray_module as m
+
+    monkeypatch.setenv("RTDC_FMNIST_TRAIN", "2048")
+    monkeypatch.setenv("RTDC_FMNIST_TEST", "512")
+    monkeypatch.delenv("RTDC_FORCE_CPU", raising=False)
+    kw = dict(num_workers=1, use_gpu=True, epochs=2, seed=5, resume_mode="exact")
+    g = m.train_fashion_mnist(checkpoint_storage_path=str(tmp_path / "g"), hipgraph=True, **kw)
+    e = m.train_fashion_mnist(checkpoint_storage_path=str(tmp_path / "e"), hipgraph=False, **kw)
+    rows_g = [json.loads(l) for l in open(os.path.join(g.path, "result.json"))]
+    rows_e = [json.loads(l) for l in open(os.path.join(e.path, "result.json"))]
+    for rg, re_ in zip(rows_g, rows_e):
+        assert rg["val_loss"] == re_["val_loss"] and rg["accuracy"] == re_["accuracy"], (rg, re_)
+
+
+def test_eval_device_pipeline_matches_numpy_path_gpu(tmp_path):
+    """map_batches with the GPU predictor (pinned double buffer, one D2H) returns exactly the
+    per-batch numpy predictor's outputs, in order, for the 10k-row eval set."""
+    import time
+
+    import numpy as np
+
+    import my_ray_module as m
+    from ray_torch_distributed_checkpoint_amd.checkpoint import torchsave
+    from ray_torch_distributed_checkpoint_amd.train import Checkpoint
+
+    torch.manual_seed(3)
+    net = m.NeuralNetwork()
+    torchsave.save({"epoch": 0, "model_state_dict": net.state_dict()}, str(tmp_path / "best_model.pt"))
+    ck = Checkpoint.from_directory(str(tmp_path))
+    ds = m.get_dataloaders(batch_size=512, val_only=True, as_ray_ds=True)
+    pred = m.TorchPredictor(checkpoint=ck)
+    out = ds.map_batches(pred, batch_size=512, concurrency=1, num_gpus=1)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = ds.map_batches(pred, batch_size=512, concurrency=1, num_gpus=1).to_numpy()
+    dt = time.perf_counter() - t0
+    ref = [pred(b) for b in ds.iter_batches(512)]
+    ref_logits = np.concatenate([r["logits"] for r in ref])
+    assert out["logits"].shape == (ds.count(), 10)
+    np.testing.assert_array_equal(out["logits"], ref_logits)
+    np.testing.assert_array_equal(out["predicted_values"], np.concatenate([r["predicted_values"] for r in ref]))
+    print(f"eval pass over {ds.count()} rows: {dt * 1e3:.1f} ms")
+    assert dt < 0.5
