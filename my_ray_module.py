@@ -26,6 +26,7 @@ with these deliberate fixes of reference quirks:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import tempfile
 import time
@@ -136,6 +137,7 @@ def train_func_per_worker(config: Dict):
     use_graph = (device.type == "cuda" and world == 1 and config.get("hipgraph", True) and n_train > 0
                  and n_train % batch_size == 0)
     if use_graph:
+        side = torch.cuda.Stream()
         sx = torch.zeros((batch_size, 1, 28, 28), device=device)
         sy = torch.zeros((batch_size,), dtype=torch.int64, device=device)
 
@@ -168,14 +170,24 @@ def train_func_per_worker(config: Dict):
                 with phase("step"):
                     captured.replay()
                 continue
-            with phase("fwd"):
-                pred = model(X)
-                loss = ops.cross_entropy(pred, y)
-            optimizer.zero_grad()
-            with phase("bwd"):
-                loss.backward()
-            with phase("opt"):
-                optimizer.step()
+            # before a capture, run the eager steps on a side stream (as CapturedStep's warm-up
+            # does): autograd's AccumulateGrad nodes must not belong to the default stream
+            # when the graph is recorded
+            warm = use_graph and captured is None
+            if warm:
+                side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side) if warm else contextlib.nullcontext():
+                with phase("fwd"):
+                    pred = model(X)
+                    loss = ops.cross_entropy(pred, y)
+                optimizer.zero_grad()
+                with phase("bwd"):
+                    loss.backward()
+                with phase("opt"):
+                    optimizer.step()
+            if warm:
+                torch.cuda.current_stream().wait_stream(side)
+            del pred, loss
         train_time = time.time() - t0
 
         model.eval()
