@@ -310,59 +310,72 @@ def read_metadata(checkpoint_id: str) -> Metadata:
         return _SafeUnpickler(f).load()
 
 
-def _zip_data_record(path: str, base: int, length: int) -> tuple[int, int]:
+def _zip_data_record(path: str, base: int, length: int, f=None) -> tuple[int, int]:
     """(absolute data offset, size) of the tensor record '<prefix>/data/0' in a zip slice.
-    Handles ZIP64 (records >= 4 GiB, offsets past 4 GiB, zip64 end-of-central-directory)."""
-    with open(path, "rb") as f:
-        tail_len = min(length, 1 << 16)
+    Handles ZIP64 (records >= 4 GiB, offsets past 4 GiB, zip64 end-of-central-directory).
+    Reads only the archive's tail (a one-tensor archive's central directory is < 1 KiB) and
+    the record's local header; pass an open file `f` to reuse it across items."""
+    if f is None:
+        with open(path, "rb") as fh:
+            return _zip_data_record(path, base, length, fh)
+    tail = b""
+    for tail_len in (min(length, 2048), min(length, 1 << 16)):
         f.seek(base + length - tail_len)
         tail = f.read(tail_len)
         eocd = tail.rfind(b"PK\x05\x06")
-        if eocd < 0:
-            raise IOError(f"{path}@{base}: no zip end record")
-        n, cd_size, cd_off = struct.unpack("<HII", tail[eocd + 10:eocd + 20])
-        if n == 0xFFFF or cd_size == 0xFFFFFFFF or cd_off == 0xFFFFFFFF:
-            loc = eocd - 20
-            if loc < 0 or tail[loc:loc + 4] != b"PK\x06\x07":
-                raise IOError(f"{path}@{base}: zip64 locator missing")
-            (z64_off,) = struct.unpack("<Q", tail[loc + 8:loc + 16])
-            f.seek(base + z64_off)
-            rec = f.read(56)
-            if rec[:4] != b"PK\x06\x06":
-                raise IOError(f"{path}@{base}: bad zip64 end record")
-            n, _n2, cd_size, cd_off = struct.unpack("<QQQQ", rec[24:56])
+        if eocd >= 0:
+            n_, cd_size_, cd_off_ = struct.unpack("<HII", tail[eocd + 10:eocd + 20])
+            z64 = n_ == 0xFFFF or cd_size_ == 0xFFFFFFFF or cd_off_ == 0xFFFFFFFF
+            if z64 or cd_off_ >= length - tail_len:  # central directory inside what was read
+                break
+    if eocd < 0:
+        raise IOError(f"{path}@{base}: no zip end record")
+    n, cd_size, cd_off = struct.unpack("<HII", tail[eocd + 10:eocd + 20])
+    if n == 0xFFFF or cd_size == 0xFFFFFFFF or cd_off == 0xFFFFFFFF:
+        loc = eocd - 20
+        if loc < 0 or tail[loc:loc + 4] != b"PK\x06\x07":
+            raise IOError(f"{path}@{base}: zip64 locator missing")
+        (z64_off,) = struct.unpack("<Q", tail[loc + 8:loc + 16])
+        f.seek(base + z64_off)
+        rec = f.read(56)
+        if rec[:4] != b"PK\x06\x06":
+            raise IOError(f"{path}@{base}: bad zip64 end record")
+        n, _n2, cd_size, cd_off = struct.unpack("<QQQQ", rec[24:56])
+    if cd_off >= length - len(tail):
+        cd = tail[cd_off - (length - len(tail)):cd_off - (length - len(tail)) + cd_size]
+    else:
         f.seek(base + cd_off)
         cd = f.read(cd_size)
-        pos = 0
-        for _ in range(n):
-            (sig,) = struct.unpack("<I", cd[pos:pos + 4])
-            if sig != 0x02014B50:
-                raise IOError(f"{path}@{base}: corrupt central directory")
-            csize, usize = struct.unpack("<II", cd[pos + 20:pos + 28])
-            nlen, elen, clen = struct.unpack("<HHH", cd[pos + 28:pos + 34])
-            lho, = struct.unpack("<I", cd[pos + 42:pos + 46])
-            name = cd[pos + 46:pos + 46 + nlen].decode()
-            if name.endswith("/data/0"):
-                if 0xFFFFFFFF in (csize, usize, lho):
-                    extra = cd[pos + 46 + nlen:pos + 46 + nlen + elen]
-                    e = 0
-                    while e + 4 <= len(extra):
-                        tag, sz = struct.unpack("<HH", extra[e:e + 4])
-                        if tag == 1:
-                            vals = list(struct.unpack("<" + "Q" * (sz // 8), extra[e + 4:e + 4 + sz]))
-                            if usize == 0xFFFFFFFF:
-                                usize = vals.pop(0)
-                            if csize == 0xFFFFFFFF:
-                                csize = vals.pop(0)
-                            if lho == 0xFFFFFFFF:
-                                lho = vals.pop(0)
-                            break
-                        e += 4 + sz
-                f.seek(base + lho)
-                lh = f.read(30)
-                lnlen, lelen = struct.unpack("<HH", lh[26:30])
-                return base + lho + 30 + lnlen + lelen, csize
-            pos += 46 + nlen + elen + clen
+    pos = 0
+    for _ in range(n):
+        (sig,) = struct.unpack("<I", cd[pos:pos + 4])
+        if sig != 0x02014B50:
+            raise IOError(f"{path}@{base}: corrupt central directory")
+        csize, usize = struct.unpack("<II", cd[pos + 20:pos + 28])
+        nlen, elen, clen = struct.unpack("<HHH", cd[pos + 28:pos + 34])
+        lho, = struct.unpack("<I", cd[pos + 42:pos + 46])
+        name = cd[pos + 46:pos + 46 + nlen].decode()
+        if name.endswith("/data/0"):
+            if 0xFFFFFFFF in (csize, usize, lho):
+                extra = cd[pos + 46 + nlen:pos + 46 + nlen + elen]
+                e = 0
+                while e + 4 <= len(extra):
+                    tag, sz = struct.unpack("<HH", extra[e:e + 4])
+                    if tag == 1:
+                        vals = list(struct.unpack("<" + "Q" * (sz // 8), extra[e + 4:e + 4 + sz]))
+                        if usize == 0xFFFFFFFF:
+                            usize = vals.pop(0)
+                        if csize == 0xFFFFFFFF:
+                            csize = vals.pop(0)
+                        if lho == 0xFFFFFFFF:
+                            lho = vals.pop(0)
+                        break
+                    e += 4 + sz
+            f.seek(base + lho)
+            lh = f.read(30)
+            lnlen, lelen = struct.unpack("<HH", lh[26:30])
+            return base + lho + 30 + lnlen + lelen, csize
+        pos += 46 + nlen + elen + clen
     raise IOError(f"{path}@{base}: no tensor data record")
 
 
@@ -401,6 +414,7 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
     my = [k for k in tensor_fqns if reader[k] == rank]
     # ---- read my items: (dest tensor, chunk offsets, chunk sizes, file, data offset, nbytes)
     reqs = []
+    handles: dict = {}
     for k in my:
         dest = flat[k]
         mdt = md.state_dict_metadata[k]
@@ -408,12 +422,17 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
             raise ValueError(f"{k}: checkpoint shape {tuple(mdt.size)} != destination {tuple(dest.shape)}")
         for idx, info in chunks_of[k]:
             path = os.path.join(checkpoint_id, info.relative_path)
-            off, n = _zip_data_record(path, info.offset, info.length)
+            fh = handles.get(path)
+            if fh is None:
+                fh = handles[path] = open(path, "rb", buffering=0)
+            off, n = _zip_data_record(path, info.offset, info.length, fh)
             csizes = None
             for c in mdt.chunks:
                 if tuple(c.offsets) == tuple(idx.offset):
                     csizes = tuple(c.sizes)
             reqs.append((dest, tuple(idx.offset), csizes or tuple(dest.shape), path, off, n, mdt.properties.dtype))
+    for fh in handles.values():
+        fh.close()
     # device destinations whose region is one contiguous run of the same dtype stream straight
     # from the file: native pread -> pinned ring -> H2D on the engine's copy stream, pipelined
     # (torchsave.get_engine().read_to_device); anything else (host destinations, resharded

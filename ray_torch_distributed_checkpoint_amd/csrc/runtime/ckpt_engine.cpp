@@ -113,8 +113,14 @@ static std::string local_header(const Record& r, uint64_t size) {
   return h;
 }
 
-// Assign offsets; data of every record starts 64-B aligned.
-static uint64_t layout_records(std::vector<Record>& recs, uint64_t base) {
+// Records at least this large get their data at a 4 KiB-aligned FILE offset, so their
+// slot-sized pieces can be written and read with O_DIRECT (DMA between the pinned ring and
+// the device, no page-cache copy); smaller records are 64-B aligned like PyTorchStreamWriter.
+static constexpr uint64_t kDirectMin = 1ull << 16, kPage = 4096;
+
+// Assign archive-relative offsets; `abs_base` is the archive's file offset (for the 4 KiB
+// alignment of big records).
+static uint64_t layout_records(std::vector<Record>& recs, uint64_t base, uint64_t abs_base = 0) {
   uint64_t off = base;
   for (auto& r : recs) {
     r.header_off = off;
@@ -122,8 +128,9 @@ static uint64_t layout_records(std::vector<Record>& recs, uint64_t base) {
     const uint64_t z = r.z64_size ? 20 : 0;
     uint64_t hdr = 30 + r.name.size() + z;
     uint64_t data = off + hdr;
-    uint64_t pad = (64 - (data % 64)) % 64;
-    if (pad > 0 && pad < 4) pad += 64;  // extra field needs >= 4 bytes
+    const uint64_t align = (r.src && r.nbytes >= kDirectMin) ? kPage : 64;
+    uint64_t pad = (align - ((abs_base + data) % align)) % align;
+    if (pad > 0 && pad < 4) pad += align;  // extra field needs >= 4 bytes
     r.extra_len = (uint16_t)(z + pad);
     r.data_off = data + pad;
     off = r.data_off + rec_size(r);
@@ -335,7 +342,7 @@ static uint64_t layout_archives(std::vector<Archive>& arcs) {
       a.data_end = n;
       a.size = n;
     } else {
-      a.data_end = layout_records(a.recs, 0);
+      a.data_end = layout_records(a.recs, 0, off);
       a.size = a.data_end + cd_size(a.recs, a.data_end);
     }
     off += a.size;
@@ -347,6 +354,7 @@ struct FileJob {
   std::string path;
   std::vector<Archive> archives;
   int fd = -1;
+  int dfd = -1;  // O_DIRECT descriptor of the same file (-1: filesystem refuses O_DIRECT)
   uint64_t total = 0;
   std::atomic<int> pending{0};
   // per big-record ordered piece CRCs, key = (archive << 24) | record
@@ -376,8 +384,8 @@ static double now_s() {
 
 class Engine {
  public:
-  Engine(size_t nslots, size_t slot_bytes, int nwriters, int device)
-      : ring_(nslots, slot_bytes), device_(device) {
+  Engine(size_t nslots, size_t slot_bytes, int nwriters, int device, bool direct_io = true)
+      : ring_(nslots, slot_bytes), device_(device), direct_io_(direct_io) {
     if (g_have_gpu()) {
       hipSetDevice(device_);
       hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
@@ -467,6 +475,10 @@ class Engine {
       throw std::runtime_error("read_to_device: offs/lens/dsts length mismatch");
     int fd = ::open(path.c_str(), O_RDONLY);
     if (fd < 0) throw std::runtime_error("open failed: " + path + ": " + strerror(errno));
+    // page-aligned pieces are read with O_DIRECT straight into the (page-aligned) pinned slot
+    int dfd = direct_io_ ? ::open(path.c_str(), O_RDONLY | O_DIRECT) : -1;
+    struct stat stt;
+    const uint64_t fsize = ::fstat(fd, &stt) == 0 ? (uint64_t)stt.st_size : 0;
     struct P { uint64_t off, len; char* dst; };
     std::vector<P> pieces;
     const uint64_t S = ring_.slot_bytes();
@@ -487,7 +499,14 @@ class Engine {
         }
         const int s = ring_.acquire();
         try {
-          pread_all(fd, ring_.ptr(s), pieces[k].len, pieces[k].off);
+          const P& pc = pieces[k];
+          const uint64_t rl = (pc.len + kPage - 1) / kPage * kPage;  // round up: O_DIRECT length
+          bool done = false;
+          if (dfd >= 0 && pc.off % kPage == 0 && rl <= S && pc.off + pc.len <= fsize) {
+            ssize_t r = ::pread(dfd, ring_.ptr(s), rl, (off_t)pc.off);
+            if (r >= (ssize_t)pc.len) done = true;  // may stop short of rl at end of file
+          }
+          if (!done) pread_all(fd, ring_.ptr(s), pieces[k].len, pieces[k].off);
           hipError_t e;
           {
             std::lock_guard<std::mutex> lk(cmu);
@@ -508,6 +527,7 @@ class Engine {
     for (int i = 0; i < nt; ++i) ts.emplace_back(work);
     for (auto& t : ts) t.join();
     ::close(fd);
+    if (dfd >= 0) ::close(dfd);
     if (err.empty() && hipStreamSynchronize(stream_) != hipSuccess) err = "restore: copy stream failed";
     if (!err.empty()) throw std::runtime_error(err);
   }
@@ -551,6 +571,7 @@ class Engine {
     for (auto& f : job->files) {
       f->fd = ::open(f->path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
       if (f->fd < 0) throw std::runtime_error("open failed: " + f->path + ": " + strerror(errno));
+      if (direct_io_) f->dfd = ::open(f->path.c_str(), O_WRONLY | O_DIRECT);
       int pieces = 1;  // the headers / small records / central directories (finalize)
       for (auto& a : f->archives)
         for (auto& r : a.recs)
@@ -645,7 +666,7 @@ class Engine {
           }
           uint32_t c = 0;
           if (f.crc_on) c = (uint32_t)crc32(0L, (const Bytef*)src, (uInt)w.len);
-          pwrite_all(f.fd, src, w.len, w.off);
+          write_piece(f, src, w.len, w.off);
           if (w.slot >= 0) ring_.release(w.slot);
           w.slot = -1;
           std::lock_guard<std::mutex> lk(f.mu);
@@ -661,6 +682,34 @@ class Engine {
         if (w.job->files_left.fetch_sub(1) == 1) finish_job(w.job);
       }
     }
+  }
+
+  // Page-aligned runs of a piece go through the O_DIRECT descriptor (pinned slot -> device,
+  // no page-cache copy); an unaligned remainder (a record's last bytes) through the buffered
+  // one.  The two never touch the same 4 KiB page, and fsync on the file covers both.
+  static void write_piece(FileJob& f, const void* src, uint64_t len, uint64_t off) {
+    const char* p = (const char*)src;
+    if (f.dfd >= 0 && off % kPage == 0 && ((uintptr_t)p % kPage) == 0) {
+      const uint64_t a = len / kPage * kPage;
+      if (a > 0) {
+        ssize_t w = ::pwrite(f.dfd, p, a, (off_t)off);
+        if (w == (ssize_t)a) {
+          p += a;
+          off += a;
+          len -= a;
+        } else if (w < 0 && errno == EINVAL) {  // filesystem refuses: stay buffered from here
+          ::close(f.dfd);
+          f.dfd = -1;
+        } else if (w < 0) {
+          throw std::runtime_error(std::string("pwrite(O_DIRECT) failed: ") + strerror(errno));
+        } else {  // short direct write: finish buffered
+          p += w;
+          off += (uint64_t)w;
+          len -= (uint64_t)w;
+        }
+      }
+    }
+    if (len) pwrite_all(f.fd, p, len, off);
   }
 
   void finalize_file(FileJob& f) {
@@ -698,6 +747,10 @@ class Engine {
       }
     }
     if (f.fsync_on) ::fsync(f.fd);
+    if (f.dfd >= 0) {
+      ::close(f.dfd);
+      f.dfd = -1;
+    }
     ::close(f.fd);
     f.fd = -1;
   }
@@ -708,6 +761,10 @@ class Engine {
       if (f->fd >= 0) {
         ::close(f->fd);
         f->fd = -1;
+      }
+      if (f->dfd >= 0) {
+        ::close(f->dfd);
+        f->dfd = -1;
       }
     }
     {
@@ -720,6 +777,7 @@ class Engine {
 
   PinnedRing ring_;
   int device_;
+  bool direct_io_;
   hipStream_t stream_ = nullptr;
   std::vector<std::thread> writers_;
   std::thread enqueuer_;
