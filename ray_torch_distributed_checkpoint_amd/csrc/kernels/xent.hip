@@ -8,7 +8,9 @@
 // row (L2-resident: one 100 KB GPT-2 row per block) and writes scale*(softmax - onehot);
 // padded vocabulary columns [V, ld) get exactly 0.  Rows whose target is ignore_index get a
 // zero loss and zero gradient.
-#include "common.h"
+#include "gemm_common.h"
+
+#include <cstdlib>
 
 namespace rtdc {
 
@@ -187,15 +189,197 @@ __global__ __launch_bounds__(256) void xent_kernel(const T* logits, T* dlogits,
   }
 }
 
+// Register-resident variant for bf16 training rows that fit in the block's registers
+// (GPT-2: 50304 columns = 25 x 16 B per thread at 256 threads): the row is loaded ONCE,
+// max / argmax and sum-exp are two exact block reductions over the registers, and the
+// gradient is written from the same registers - one HBM read + one write of the logits
+// instead of read, re-read (L2 misses at 16 K rows of 100 KB in flight), write.
+template <int NT>
+__device__ __forceinline__ float block_max_arg(float m, int& arg, float* sred, int* sarg) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(m, off, 64);
+    const int oa = __shfl_xor(arg, off, 64);
+    if (om > m || (om == m && oa < arg)) {
+      m = om;
+      arg = oa;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sred[w] = m;
+    sarg[w] = arg;
+  }
+  __syncthreads();
+  m = sred[0];
+  arg = sarg[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i)
+    if (sred[i] > m || (sred[i] == m && sarg[i] < arg)) {
+      m = sred[i];
+      arg = sarg[i];
+    }
+  return m;
+}
+
+template <int NT>
+__device__ __forceinline__ float block_sum2(float s, float* sred) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // sred reuse after block_max_arg
+  if ((threadIdx.x & 63) == 0) sred[w] = s;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += sred[i];
+  return r;
+}
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// Keep the row as packed bf16: without this the compiler keeps the 8 unpacked floats of every
+// chunk alive from the max pass to the sum / gradient passes (4x the registers, 1 wave/SIMD).
+template <int NCH>
+__device__ __forceinline__ void opaque(uint32_t (&v)[NCH][4]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(v[c][i]));
+}
+
+template <int NT, int NCH, bool ARG>
+__global__ __launch_bounds__(NT) void xent_reg_kernel(const bf16_t* logits, bf16_t* dlogits,
+                                                     const int64_t* __restrict__ target, float* __restrict__ loss,
+                                                     float* __restrict__ lse_out, int64_t* __restrict__ argmax,
+                                                     int M, int V, int ld, float grad_scale, int ignore_index) {
+  __shared__ float sred[NT / 64];
+  __shared__ int sarg[NT / 64];
+  const int row = blockIdx.x;
+  const bf16_t* x = logits + (long long)row * ld;
+  const int tid = threadIdx.x;
+  // target logit read before any write of this row (dlogits may alias logits)
+  const int64_t tgt = target ? target[row] : -1;
+  const bool valid = target && tgt != ignore_index && tgt >= 0 && tgt < V;
+  const float xt = (tid == 0 && valid) ? bf2f(x[tgt]) : 0.f;
+  // the row, 8 bf16 per 16-B chunk, chunk c of thread t at column (c*NT + t)*8; columns >= V
+  // (vocabulary padding, and chunks past the row) become -inf, so exp() zeroes them below
+  // buffer loads: one VGPR offset (tid * 16) + a scalar per-chunk offset; chunks past the row
+  // read 0 through the descriptor's range check and are masked below like the padding
+  const auto rx = make_rsrc(x, 0, (long long)ld * 2);
+  uint32_t v[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * NT + tid) * 8;
+    const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rx, tid * 16, c * NT * 16, 0);
+    v[c][0] = q[0];
+    v[c][1] = q[1];
+    v[c][2] = q[2];
+    v[c][3] = q[3];
+    if (col + 8 > V) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (col + e >= V) v[c][e >> 1] = e & 1 ? (v[c][e >> 1] & 0x0000ffffu) | 0xff800000u
+                                               : (v[c][e >> 1] & 0xffff0000u) | 0x0000ff80u;
+    }
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m = fmaxf(m, fmaxf(bf_lo(v[c][i]), bf_hi(v[c][i])));
+  int arg = 0x7fffffff;
+  if constexpr (ARG) {  // first column holding the maximum (per thread columns ascend with c, e)
+    const float mt = m;
+#pragma unroll
+    for (int c = NCH - 1; c >= 0; --c)
+#pragma unroll
+      for (int e = 7; e >= 0; --e) {
+        const float f = e & 1 ? bf_hi(v[c][e >> 1]) : bf_lo(v[c][e >> 1]);
+        if (f == mt) arg = (c * NT + tid) * 8 + e;
+      }
+  }
+  m = block_max_arg<NT>(m, arg, sred, sarg);
+  opaque(v);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += __expf(bf_lo(v[c][i]) - m) + __expf(bf_hi(v[c][i]) - m);
+  s = block_sum2<NT>(s, sred);
+  const float lse = m + __logf(s);
+  if (tid == 0) {
+    if (loss) loss[row] = valid ? lse - xt : 0.f;
+    if (lse_out) lse_out[row] = lse;
+    if (argmax) argmax[row] = arg;
+  }
+  if (!dlogits) return;
+  __syncthreads();  // every thread's reads of the row precede any overwrite (in-place dlogits)
+  opaque(v);
+  const auto rd = make_rsrc(dlogits + (long long)row * ld, 0, (long long)ld * 2);
+  const float sc = valid ? grad_scale : 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * NT + tid) * 8;
+    {
+      float g[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        g[2 * i] = sc * __expf(bf_lo(v[c][i]) - lse);
+        g[2 * i + 1] = sc * __expf(bf_hi(v[c][i]) - lse);
+      }
+      const int o = (int)(tgt - col);
+      if (valid && (unsigned)o < 8u) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (e == o) g[e] -= sc;
+      }
+      // stores past the row are dropped by the descriptor's range check
+      __builtin_amdgcn_raw_buffer_store_b128(pack8bf(g), rd, tid * 16, c * NT * 16, 0);
+    }
+  }
+}
+
 }  // namespace rtdc
 
 using namespace rtdc;
+
+// register-resident launch for bf16 rows of at most NT*NCH*8 columns (returns false if none fits)
+static bool launch_xent_reg(const void* logits, void* dlogits, const int64_t* target, float* loss, float* lse,
+                            int64_t* argmax, int M, int V, int ld, float grad_scale, int ignore_index,
+                            hipStream_t st) {
+  if (ld % 8 != 0 || getenv("RTDC_XENT_TWO_PASS")) return false;
+#define XR(NT, NCH)                                                                                          \
+  if (ld <= NT * NCH * 8) {                                                                                 \
+    if (argmax)                                                                                              \
+      hipLaunchKernelGGL((xent_reg_kernel<NT, NCH, true>), dim3(M), dim3(NT), 0, st, (const bf16_t*)logits,  \
+                         (bf16_t*)dlogits, target, loss, lse, argmax, M, V, ld, grad_scale, ignore_index);  \
+    else                                                                                                     \
+      hipLaunchKernelGGL((xent_reg_kernel<NT, NCH, false>), dim3(M), dim3(NT), 0, st, (const bf16_t*)logits, \
+                         (bf16_t*)dlogits, target, loss, lse, argmax, M, V, ld, grad_scale, ignore_index);  \
+    return true;                                                                                             \
+  }
+  // NT x NCH x 8 columns; one wave per SIMD per block so several blocks share a CU and one
+  // block's write phase overlaps the next block's loads (GPT-2: 256 x 25)
+  XR(256, 4)
+  XR(256, 8)
+  XR(256, 16)
+  XR(256, 25)
+  XR(512, 16)
+  XR(1024, 16)
+#undef XR
+  return false;
+}
 
 extern "C" int rtdc_xent(const void* logits, void* dlogits, const int64_t* target, float* loss,
                          float* lse, int64_t* argmax, int M, int V, int ld, float grad_scale,
                          int ignore_index, int is_bf16, hipStream_t st) {
   dim3 grid(M), block(256);
   const bool vec = (ld % 8 == 0);
+  if (is_bf16 && launch_xent_reg(logits, dlogits, target, loss, lse, argmax, M, V, ld, grad_scale, ignore_index,
+                                 st))
+    return hipGetLastError() == hipSuccess ? 0 : 2;
   if (is_bf16) {
     if (vec)
       hipLaunchKernelGGL((xent_kernel<bf16_t, true>), grid, block, 0, st, (const bf16_t*)logits,

@@ -272,7 +272,9 @@ def test_layernorm_bwd_offers_dx_colsum():
     _close(G.colsum(dx.view(M, D)), 2 * ref, 1e-3)
 
 
-@pytest.mark.parametrize("dtype,V,ld",[(torch.float32, 10, 10), (torch.bfloat16, 1000, 1024), (torch.float32, 333, 333)])
+@pytest.mark.parametrize("dtype,V,ld",[(torch.float32, 10, 10), (torch.bfloat16, 1000, 1024), (torch.float32, 333, 333),
+                                        (torch.bfloat16, 1000, 1000), (torch.bfloat16, 50257, 50257),
+                                        (torch.bfloat16, 128256, 128256)])
 def test_cross_entropy(dtype, V, ld):
     from ray_torch_distributed_checkpoint_amd.ops import cross_entropy, xent_metrics
 
