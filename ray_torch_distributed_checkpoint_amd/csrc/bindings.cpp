@@ -499,6 +499,22 @@ static std::vector<rtdc_ckpt::Archive> to_archives(const py::list& arcs) {
   return out;
 }
 
+// Per-step gradient bookkeeping of a flat parameter space, in one C++ pass instead of ~300
+// Python property reads (`p.grad`, `data_ptr()`) between the end of backward and the
+// optimizer launch: for each parameter, 0 = no gradient, 1 = gradient already is its slice of
+// the flat buffer at `base + 4*offset`, 2 = gradient lives elsewhere (must be folded in).
+static std::vector<int8_t> grad_status(const std::vector<at::Tensor>& params, int64_t base,
+                                       const std::vector<int64_t>& offsets) {
+  TORCH_CHECK(params.size() == offsets.size(), "grad_status: one offset per parameter");
+  std::vector<int8_t> st(params.size(), 0);
+  for (size_t i = 0; i < params.size(); ++i) {
+    const at::Tensor& g = params[i].grad();
+    if (!g.defined()) continue;
+    st[i] = (reinterpret_cast<int64_t>(g.data_ptr()) == base + 4 * offsets[i]) ? 1 : 2;
+  }
+  return st;
+}
+
 // -> (file_size, [(archive_base, archive_size, [(abs_data_offset, size), ...]), ...])
 static py::tuple plan_layout(const py::list& arcs) {
   auto a = to_archives(arcs);
@@ -568,6 +584,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool", &avgpool);
 
+  m.def("grad_status", &grad_status, "per-parameter gradient placement: 0 none, 1 flat slice, 2 elsewhere");
   m.def("have_gpu", &rtdc_ckpt::g_have_gpu);
   m.def("plan_layout", &plan_layout, "file layout of a list of (raw, records) archives");
   m.def("crc32", [](py::bytes b) {

@@ -6,7 +6,7 @@
 // dgamma/dbeta rows to a workspace that a second kernel reduces in a fixed order, so the
 // parameter gradients are bitwise reproducible (no float atomics, MI355X_MICROARCH.md §Global
 // float atomics).
-#include "common.h"
+#include "gemm_common.h"
 
 namespace rtdc {
 
@@ -117,29 +117,44 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     if (c < nch) ld8(g + c * 8, gg[i]);
   }
 
-  for (int row = gw; row < M; row += nw) {
-    const float mean = RMS ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
-    const bf16_t* xr = x + (long long)row * D;
-    const bf16_t* dyr = dy + (long long)row * D;
-    float xh[CPL][8], dxh[CPL][8];
-    // the residual-gradient row is loaded with x and dy (one memory round trip per row, not two)
-    uint4 rraw[CPL];
-    if (dres) {
+  // rows are software-pipelined: the next row's x / dy / dres (and its statistics) are in
+  // flight while this row is reduced and written (a wave owns M/nw rows in sequence)
+  uint4 px[CPL], pd[CPL], pr[CPL];
+  float pmean = 0.f, prstd = 0.f;
+  auto fetch = [&](int r) {
 #pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nch) rraw[i] = *(const uint4*)(dres + (long long)row * D + c * 8);
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        px[i] = *(const uint4*)(x + (long long)r * D + c * 8);
+        pd[i] = *(const uint4*)(dy + (long long)r * D + c * 8);
+        if (dres) pr[i] = *(const uint4*)(dres + (long long)r * D + c * 8);
       }
     }
+    pmean = RMS ? 0.f : mean_in[r];
+    prstd = rstd_in[r];
+  };
+  if (gw < M) fetch(gw);
+  for (int row = gw; row < M; row += nw) {
+    const float mean = pmean;
+    const float rstd = prstd;
+    uint4 cx[CPL], cd[CPL], rraw[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      cx[i] = px[i];
+      cd[i] = pd[i];
+      rraw[i] = pr[i];
+    }
+    if (row + nw < M) fetch(row + nw);
+    float xh[CPL][8], dxh[CPL][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c = lane + 64 * i;
       if (c < nch) {
         float xv[8], dv[8];
-        ld8(xr + c * 8, xv);
-        ld8(dyr + c * 8, dv);
+        unpack8bf(u32x4{cx[i].x, cx[i].y, cx[i].z, cx[i].w}, xv);
+        unpack8bf(u32x4{cd[i].x, cd[i].y, cd[i].z, cd[i].w}, dv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           xh[i][e] = (xv[e] - mean) * rstd;

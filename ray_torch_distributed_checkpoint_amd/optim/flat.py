@@ -72,6 +72,7 @@ class FlatParamSpace:
             self.shadow = torch.empty(off, dtype=shadow_dtype, device=self.device)
             self.refresh_shadows()
         self.grad_scale = 1.0
+        self._offsets = None
         self._chunk_cache: dict = {}
         # (flat offset, wait fn) of a gradient slice whose all-reduce is still in flight
         # (DistributedDataParallel(defer_tail_to_optimizer=True)); everything below the offset
@@ -123,20 +124,39 @@ class FlatParamSpace:
             if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                 p.grad = v
 
-    def ensure_grad_views(self):
-        """Fold gradients that autograd allocated outside the flat buffer back into it.
-        Parameters without a gradient stay `None` (the optimizers skip them, like torch)."""
+    def ensure_grad_views(self) -> list:
+        """Fold gradients that autograd allocated outside the flat buffer back into it and
+        return the parameters that have a gradient this step (the optimizers skip the rest,
+        like torch).  One native pass over the parameters when the extension is loaded."""
         if self.grad is None:
-            return
+            return [p for p in self.params if p.grad is not None]
         base = self.grad.data_ptr()
-        for p, s in zip(self.params, self.segments):
-            g = p.grad
-            if g is None or g.data_ptr() == base + 4 * s.offset:
+        st = self._grad_status(base)
+        have = []
+        for p, s, k in zip(self.params, self.segments, st):
+            if k == 0:
+                continue
+            have.append(p)
+            if k == 1:
                 continue
             self.wait_pending_tail()  # never write into a slice a collective still owns
             v = self.view(self.grad, s)
-            v.copy_(g)
+            v.copy_(p.grad)
             p.grad = v
+        return have
+
+    def _grad_status(self, base: int):
+        from ..ops import _ext
+
+        if _ext.available():
+            if self._offsets is None:
+                self._offsets = [s.offset for s in self.segments]
+            return _ext.ext().grad_status(self.params, base, self._offsets)
+        out = []
+        for p, s in zip(self.params, self.segments):
+            g = p.grad
+            out.append(0 if g is None else (1 if g.data_ptr() == base + 4 * s.offset else 2))
+        return out
 
     def attach_grad_views(self):
         """Point every parameter's `.grad` at its flat slice (after a data-parallel reduce

@@ -33,6 +33,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._bufs: dict[str, torch.Tensor] = {}
         self._steps: dict = {}  # param -> number of optimizer steps taken (host int)
         self._bound: set = set()
+        self._have = None  # parameters with a gradient this step (set by the native step)
 
     # -- flat setup ------------------------------------------------------------------------
     def _all_params(self):
@@ -163,9 +164,11 @@ class _FlatOptimizer(torch.optim.Optimizer):
         ps = self._all_params()
         return bool(ps) and ps[0].is_cuda
 
-    @staticmethod
-    def _with_grad(group) -> list:
-        return [p for p in group["params"] if p.grad is not None]
+    def _with_grad(self, group) -> list:
+        have = self._have
+        if have is None:
+            return [p for p in group["params"] if p.grad is not None]
+        return [p for p in group["params"] if p in have]
 
     @property
     def flat_space(self):
@@ -207,7 +210,8 @@ class FusedAdamW(_FlatOptimizer):
                 raise RuntimeError("FusedAdamW computes bias corrections on the host per step: not graph-capturable "
                                    "(use eager steps, or FusedSGD inside utils.graphs.CapturedStep)")
             sp = self._ensure_space()
-            sp.ensure_grad_views()
+            have = sp.ensure_grad_views()
+            self._have = None if len(have) == len(sp.params) else set(have)
             ext = gpu_ext()
             launches = []
             for group in self.param_groups:
@@ -271,7 +275,8 @@ class FusedSGD(_FlatOptimizer):
                 loss = closure()
         if self._use_native():
             sp = self._ensure_space()
-            sp.ensure_grad_views()
+            have = sp.ensure_grad_views()
+            self._have = None if len(have) == len(sp.params) else set(have)
             ext = gpu_ext()
             launches = []
             for group in self.param_groups:
