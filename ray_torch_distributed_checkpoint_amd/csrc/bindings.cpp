@@ -68,7 +68,8 @@ int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho,
 int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, long long N, int C, float eps, float momentum, int training,
                 int relu, float* ws, int nblk, const float* pmean, const float* pm2, int p_nblk, int p_R,
-                hipStream_t st);
+                long long* nbt, hipStream_t st);
+int rtdc_conv_w_flip_t(const void* w, void* out, int Cout, int KH, int KW, int C, hipStream_t st);
 int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
                 void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu, float* ws, int nblk,
                 hipStream_t st);
@@ -417,7 +418,11 @@ static void col2im(Tensor dcols, Tensor dx, int64_t Ho, int64_t Wo, int64_t KH, 
 static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta,
                    c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var, double eps, double momentum,
                    bool training, bool relu, Tensor ws, int64_t nblk, c10::optional<Tensor> pmean,
-                   c10::optional<Tensor> pm2, int64_t p_R) {
+                   c10::optional<Tensor> pm2, int64_t p_R, c10::optional<Tensor> num_batches_tracked) {
+  if (num_batches_tracked.has_value())
+    TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong && num_batches_tracked->is_cuda() &&
+                    num_batches_tracked->numel() == 1,
+                "bn_fwd: num_batches_tracked must be a 1-element int64 GPU tensor");
   const int64_t C = x.size(-1), N = x.numel() / C;
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "bn_fwd: contiguous tensors expected");
   TORCH_CHECK(!training || ws.numel() >= 2 * nblk * C, "bn_fwd: workspace too small");
@@ -428,8 +433,20 @@ static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, T
                        (float)momentum, training, relu, ws.data_ptr<float>(), (int)nblk,
                        pmean.has_value() ? pmean->data_ptr<float>() : nullptr,
                        pm2.has_value() ? pm2->data_ptr<float>() : nullptr,
-                       pmean.has_value() ? (int)pmean->size(0) : 0, (int)p_R, cur_stream()),
+                       pmean.has_value() ? (int)pmean->size(0) : 0, (int)p_R,
+                       num_batches_tracked.has_value() ? (long long*)num_batches_tracked->data_ptr<int64_t>() : nullptr,
+                       cur_stream()),
            "bn_fwd");
+}
+// W'[c][kh'][kw'][co] = W[co][KH-1-kh'][KW-1-kw'][c] (stride-1 conv dgrad operand), bf16
+static void conv_w_flip_t(Tensor w, Tensor out, int64_t KH, int64_t KW) {
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && w.is_contiguous() &&
+                  out.is_contiguous() && w.numel() == out.numel() && w.dim() == 2,
+              "conv_w_flip_t: contiguous bf16 [Cout, KH*KW*C] -> [C, KH*KW*Cout]");
+  const int64_t Cout = w.size(0), C = w.size(1) / (KH * KW);
+  TORCH_CHECK(C * KH * KW == w.size(1), "conv_w_flip_t: bad kernel size");
+  check_rc(rtdc_conv_w_flip_t(w.data_ptr(), out.data_ptr(), (int)Cout, (int)KH, (int)KW, (int)C, cur_stream()),
+           "conv_w_flip_t");
 }
 static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor dx,
                    c10::optional<Tensor> dres, Tensor dgamma, Tensor dbeta, bool relu, Tensor ws, int64_t nblk) {
@@ -580,6 +597,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("col2im", &col2im);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("conv_w_flip_t", &conv_w_flip_t);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool", &avgpool);

@@ -234,8 +234,11 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
 __global__ __launch_bounds__(64) void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                         int nblk, long long N, int R, int C, float eps, float momentum,
                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                        float* running_mean, float* running_var) {
+                                                        float* running_mean, float* running_var,
+                                                        long long* __restrict__ num_batches_tracked) {
   const int c = blockIdx.x, l = threadIdx.x;
+  // BatchNorm2d.num_batches_tracked += 1 (one thread of the grid, no separate ATen add)
+  if (num_batches_tracked && c == 0 && l == 0) *num_batches_tracked += 1;
   float n = 0.f, mean = 0.f, m2 = 0.f;
   for (int b = l; b < nblk; b += 64) {
     const float nb = (float)max(0LL, min((long long)R, N - (long long)b * R));
@@ -495,11 +498,11 @@ extern "C" int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int
 extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma,
                            const float* beta, float* running_mean, float* running_var, long long N, int C, float eps,
                            float momentum, int training, int relu, float* ws, int nblk, const float* pmean,
-                           const float* pm2, int p_nblk, int p_R, hipStream_t st) {
+                           const float* pm2, int p_nblk, int p_R, long long* nbt, hipStream_t st) {
   if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
   if (training && pmean) {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(64), 0, st, pmean, pm2, p_nblk, N, p_R, C, eps, momentum, mean,
-                       rstd, running_mean, running_var);
+                       rstd, running_mean, running_var, nbt);
   } else if (training) {
     const int R = (int)((N + nblk - 1) / nblk);
     hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)nullptr,
@@ -507,7 +510,7 @@ extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean,
                        ws + (long long)nblk * C);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
                        (const float*)(ws + (long long)nblk * C), nblk, N, R, C, eps, momentum, mean, rstd, running_mean,
-                       running_var);
+                       running_var, nbt);
   }
   hipLaunchKernelGGL(bn_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)res,
                      (bf16_t*)y, (const float*)mean, (const float*)rstd, gamma, beta, N, C, relu);
@@ -527,6 +530,32 @@ extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const f
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
                      (const bf16_t*)x, mean, rstd, gamma, (const float*)dbeta, (const float*)dgamma, (bf16_t*)dx,
                      (bf16_t*)dres, N, C, relu);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// dgrad operand of a stride-1 convolution: W'[c][kh'][kw'][co] = W[co][KH-1-kh'][KW-1-kw'][c]
+// from the forward's bf16 [Cout][KH][KW][Cin] matrix (one launch instead of ATen's flip +
+// permute + contiguous copy per conv per step).  Output-linear indexing: coalesced writes.
+__global__ __launch_bounds__(256) void conv_w_flip_t_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+                                                           int Cout, int KH, int KW, int C) {
+  const long long n = (long long)Cout * KH * KW * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    long long t = i;
+    const int co = (int)(t % Cout); t /= Cout;
+    const int kw = (int)(t % KW); t /= KW;
+    const int kh = (int)(t % KH); t /= KH;
+    const int c = (int)t;
+    out[i] = w[(((long long)co * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * C + c];
+  }
+}
+
+extern "C" int rtdc_conv_w_flip_t(const void* w, void* out, int Cout, int KH, int KW, int C, hipStream_t st) {
+  const long long n = (long long)Cout * KH * KW * C;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(conv_w_flip_t_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)w, (bf16_t*)out,
+                     Cout, KH, KW, C);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -17,6 +17,7 @@ forward and they are part of the DCP checkpoint.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -38,10 +39,9 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
     def forward(self, x, residual=None, relu: bool = False):
-        if self.training:
-            self.num_batches_tracked.add_(1)
         return cnn.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                              self.momentum, self.eps, residual=residual, relu=relu)
+                              self.momentum, self.eps, residual=residual, relu=relu,
+                              num_batches_tracked=self.num_batches_tracked)
 
     def extra_repr(self):
         return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, layout=NHWC"
@@ -51,8 +51,13 @@ class Conv2d(nn.Module):
     def __init__(self, cin: int, cout: int, k: int, stride: int = 1, pad: int = 0):
         super().__init__()
         self.stride, self.pad = stride, pad
-        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
-        nn.init.kaiming_normal_(self.weight, mode="fan_out", nonlinearity="relu")
+        # channels-last weight ([O][KH][KW][I] in memory, [O, I, KH, KW] logically, like any
+        # Conv2d state dict): its bf16 shadow is the implicit-GEMM operand as it stands
+        w = torch.empty(cout, cin, k, k)
+        nn.init.kaiming_normal_(w, mode="fan_out", nonlinearity="relu")  # same values in either layout
+        if os.environ.get("RTDC_CONV_WEIGHT_CL", "1") == "1":
+            w = w.to(memory_format=torch.channels_last)
+        self.weight = nn.Parameter(w)
 
     def forward(self, x):
         # every convolution of the network feeds a BatchNorm: its statistics come out of the

@@ -40,13 +40,29 @@ def _out_hw(H, W, KH, KW, stride, pad):
 
 
 def _weight_matrix(w: torch.Tensor, Kp: int) -> torch.Tensor:
-    """bf16 GEMM operand [Cout, Kp] with k = (kh*KW + kw)*Cin + c (zero-padded columns)."""
+    """bf16 GEMM operand [Cout, Kp] with k = (kh*KW + kw)*Cin + c (zero-padded columns).  A
+    channels-last weight's bf16 shadow already is this matrix (a view: no copy per step)."""
     s = shadow_of(w)
     Cout = s.shape[0]
-    m = s.permute(0, 2, 3, 1).reshape(Cout, -1)
+    m = s.permute(0, 2, 3, 1)
+    if m.is_contiguous() and m[0].numel() == Kp:
+        return m.reshape(Cout, Kp)
+    m = m.reshape(Cout, -1)
     if m.shape[1] != Kp:
         m = F.pad(m, (0, Kp - m.shape[1]))
     return m.contiguous()
+
+
+def _grad_matrix(w: torch.Tensor, K: int):
+    """The flat-buffer gradient slot of a channels-last conv weight as the [Cout, K] fp32 matrix
+    the weight-gradient GEMM writes (None: allocate and copy)."""
+    tw = grad_target(w)
+    if tw is None:
+        return None, None
+    m = tw.permute(0, 2, 3, 1)
+    if not m.is_contiguous():
+        return tw, None
+    return tw, m.reshape(tw.shape[0], K)
 
 
 def _rows_padded(t: torch.Tensor, Mp: int) -> torch.Tensor:
@@ -118,12 +134,15 @@ class _Conv2d(torch.autograd.Function):
         if mode == "implicit":
             x = saved
             if ctx.needs_input_grad[1]:
-                dwm = torch.empty((Cout, K), dtype=torch.float32, device=dy.device)
+                tw, direct = _grad_matrix(ctx.w, K)
+                dwm = direct if direct is not None else torch.empty((Cout, K), dtype=torch.float32, device=dy.device)
                 ws = G.workspace(dy.device, G.SPLITK_WS_ELEMS, "splitk")
                 gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws, None, None)
-                dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2)
-                tw = grad_target(ctx.w)
-                dw = tw.copy_(dw) if tw is not None else dw.contiguous()
+                if direct is not None:
+                    dw = tw  # written in place into the flat gradient buffer
+                else:
+                    dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2)
+                    dw = tw.copy_(dw) if tw is not None else dw.contiguous()
             if ctx.needs_input_grad[0]:
                 if stride == 1 and _implicit_ok(Cout, B * H * W):
                     # stride-1 dgrad is itself a convolution of dY with the flipped, transposed
@@ -156,8 +175,10 @@ class _Conv2d(torch.autograd.Function):
 
 def shadow_of_w(ctx, wm, Cout, C, KH, KW):
     """dgrad operand W'[c][(kh', kw', co)] = W[co][c][KH-1-kh'][KW-1-kw'] from the forward's
-    [Cout, (kh, kw, c)] matrix (bf16, built once per backward)."""
-    return wm.view(Cout, KH, KW, C).flip(1, 2).permute(3, 1, 2, 0).reshape(C, KH * KW * Cout).contiguous()
+    [Cout, (kh, kw, c)] matrix (bf16, one native flip-transpose launch per backward)."""
+    out = torch.empty((C, KH * KW * Cout), dtype=torch.bfloat16, device=wm.device)
+    gpu_ext().conv_w_flip_t(wm.contiguous(), out, KH, KW)
+    return out
 
 
 def conv2d_ref(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
@@ -187,7 +208,8 @@ def _bn_blocks(N: int, C: int) -> int:
 
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
+                num_batches_tracked=None):
         C = x.shape[-1]
         x = x.contiguous()
         N = x.numel() // C
@@ -209,7 +231,7 @@ class _BatchNorm(torch.autograd.Function):
         res = residual.contiguous() if residual is not None else None
         gpu_ext().bn_fwd(x, res, y, mean, rstd, weight, bias, running_mean if training else None,
                          running_var if training else None, eps, momentum, training, relu, ws, nblk, pmean, pm2,
-                         p_rows)
+                         p_rows, num_batches_tracked if training else None)
         ctx.save_for_backward(x, y if relu else None, mean, rstd, weight)
         ctx.params = (weight, bias)
         ctx.relu = relu
@@ -233,7 +255,7 @@ class _BatchNorm(torch.autograd.Function):
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
         gpu_ext().bn_bwd(dy, y if ctx.relu else x, x, mean, rstd, weight, dx, dres, dgamma, dbeta, ctx.relu, ws, nblk)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 
 def batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5,
@@ -248,13 +270,17 @@ def batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentu
 
 
 def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
-               eps: float = 1e-5, residual=None, relu: bool = False) -> torch.Tensor:
-    """y = relu?(BN(x) (+ residual)) over the channel (last) axis of an NHWC tensor."""
+               eps: float = 1e-5, residual=None, relu: bool = False, num_batches_tracked=None) -> torch.Tensor:
+    """y = relu?(BN(x) (+ residual)) over the channel (last) axis of an NHWC tensor.  In training
+    mode `num_batches_tracked` (int64 buffer) is incremented by the statistics kernel."""
     if x.is_cuda:
         require_dtype(x, "batch_norm")
     else:
+        if training and num_batches_tracked is not None:
+            num_batches_tracked.add_(1)
         return batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
-    return _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu)
+    return _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
+                            num_batches_tracked)
 
 
 class _MaxPool(torch.autograd.Function):

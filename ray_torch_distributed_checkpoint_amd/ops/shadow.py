@@ -22,7 +22,10 @@ def shadow_of(p: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
         if s is None or s.device != p.device or s.shape != p.shape:
             s = torch.empty(p.shape, dtype=dtype, device=p.device)
         with torch.no_grad():
-            if p.is_cuda and dtype == torch.bfloat16 and p.dtype == torch.float32:
+            if (p.is_cuda and dtype == torch.bfloat16 and p.dtype == torch.float32 and s.stride() == p.stride()
+                    and (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last))):
+                gpu_ext().f32_to_bf16(p.detach(), s)  # same memory order (e.g. channels-last): raw conversion
+            elif p.is_cuda and dtype == torch.bfloat16 and p.dtype == torch.float32 and s.is_contiguous():
                 gpu_ext().f32_to_bf16(p.detach().contiguous(), s)
             else:
                 s.copy_(p.detach())

@@ -28,6 +28,11 @@ class Segment:
     offset: int
     numel: int
     shape: tuple
+    channels_last: bool = False  # 4-D parameter stored [O][KH][KW][I] (conv weight = GEMM operand)
+
+
+def _is_channels_last(p: torch.Tensor) -> bool:
+    return p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(memory_format=torch.channels_last)
 
 
 class FlatParamSpace:
@@ -52,14 +57,17 @@ class FlatParamSpace:
         off = 0
         for i, p in enumerate(uniq):
             assert p.dtype == torch.float32, "FlatParamSpace holds fp32 master parameters"
-            self.segments.append(Segment(i, off, p.numel(), tuple(p.shape)))
+            # channels-last 4-D parameters (ResNet conv weights) keep that memory order in the
+            # flat buffers: their bf16 shadow slice IS the [O, KH*KW*I] implicit-GEMM operand and
+            # the weight-gradient GEMM writes its [O, KH*KW*I] output straight into the slice
+            self.segments.append(Segment(i, off, p.numel(), tuple(p.shape), _is_channels_last(p)))
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
         self._seg_of = {id(p): s for p, s in zip(uniq, self.segments)}
         self.data = torch.zeros(off, dtype=torch.float32, device=self.device)
         with torch.no_grad():
             for p, s in zip(uniq, self.segments):
-                self.data[s.offset:s.offset + s.numel].copy_(p.detach().reshape(-1))
+                self.view(self.data, s).copy_(p.detach())
                 p.data = self.view(self.data, s)
                 p._rtdc_space = self
         self.grad = None
@@ -87,7 +95,11 @@ class FlatParamSpace:
 
     @staticmethod
     def view(buf: torch.Tensor, s: Segment) -> torch.Tensor:
-        return buf[s.offset:s.offset + s.numel].view(s.shape)
+        flat = buf[s.offset:s.offset + s.numel]
+        if s.channels_last:
+            o, i, kh, kw = s.shape
+            return flat.view(o, kh, kw, i).permute(0, 3, 1, 2)
+        return flat.view(s.shape)
 
     def segment_of(self, p) -> Segment:
         s = self._seg_of.get(id(p))
