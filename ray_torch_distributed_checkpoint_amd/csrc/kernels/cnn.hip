@@ -135,6 +135,14 @@ __global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ 
 // (the block's first row) so sum/sum-of-squares do not cancel; lanes are combined in LDS in a
 // fixed order.  Stage 2 merges the block partials in fixed order (Chan) -> mean, rstd, running
 // stats.  No atomics anywhere: statistics are bitwise reproducible run to run.
+__device__ __forceinline__ void unpack8(const uint4& q, float* v) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
 __device__ __forceinline__ void ld8f(const bf16_t* p, float* v) {
   uint4 x = *(const uint4*)p;
   uint32_t w[4] = {x.x, x.y, x.z, x.w};
@@ -174,7 +182,51 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
           r8[e] = rstd[c + e];
         }
       }
-      for (long long r = r0 + lane; r < r1; r += rl) {
+      // U rows per iteration with every load issued before any use: 3U 16-B loads in flight
+      // per thread instead of 3 (the reduction was latency-bound at half the HBM rate)
+      constexpr int U = 4;
+      long long r = r0 + lane;
+      for (; r + (U - 1) * rl < r1; r += U * rl) {
+        uint4 va[U], vx[U], vy[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) va[u] = *(const uint4*)(a + (r + u * rl) * C + c);
+        if (mode != 0) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) vx[u] = *(const uint4*)(xb + (r + u * rl) * C + c);
+          if (yb) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) vy[u] = *(const uint4*)(yb + (r + u * rl) * C + c);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float v[8];
+          unpack8(va[u], v);
+          if (mode == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float d = v[e] - piv[e];
+              s1[e] += d;
+              s2[e] += d * d;
+            }
+          } else {
+            float xv[8];
+            unpack8(vx[u], xv);
+            if (yb) {
+              float yv[8];
+              unpack8(vy[u], yv);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = yv[e] > 0.f ? v[e] : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += v[e];
+              s2[e] += v[e] * (xv[e] - m8[e]) * r8[e];
+            }
+          }
+        }
+      }
+      for (; r < r1; r += rl) {
         float v[8];
         ld8f(a + r * C + c, v);
         if (mode == 0) {
@@ -231,37 +283,42 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
 
 // one wave per channel: lanes merge block partials b = lane, lane+64, ... (Chan), then a fixed
 // xor-shuffle tree merges the 64 lane states.
-__global__ __launch_bounds__(64) void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2,
-                                                        int nblk, long long N, int R, int C, float eps, float momentum,
-                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                        float* running_mean, float* running_var,
-                                                        long long* __restrict__ num_batches_tracked) {
+// Merge the per-tile (mean, M2) partials of one channel (block = channel, 256 threads): with
+// the grand mean known the merge is two plain sums - mean = sum(n_b m_b) / n, then
+// M2 = sum(M2_b + n_b (m_b - mean)^2) - so the loops carry no division chain (the serial
+// Welford merge over ~6k GEMM-tile partials ran 13 us per BatchNorm).  Fixed reduction order.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                         int nblk, long long N, int R, int C, float eps, float momentum,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                         float* running_mean, float* running_var,
+                                                         long long* __restrict__ num_batches_tracked) {
+  __shared__ float red[4];
   const int c = blockIdx.x, l = threadIdx.x;
   // BatchNorm2d.num_batches_tracked += 1 (one thread of the grid, no separate ATen add)
   if (num_batches_tracked && c == 0 && l == 0) *num_batches_tracked += 1;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int b = l; b < nblk; b += 64) {
+  float snm = 0.f;
+  for (int b = l; b < nblk; b += 256) {
     const float nb = (float)max(0LL, min((long long)R, N - (long long)b * R));
-    if (nb <= 0.f) break;
-    const float mb = pmean[(long long)b * C + c], m2b = pm2[(long long)b * C + c];
-    const float tot = n + nb, d = mb - mean;
-    mean += d * nb / tot;
-    m2 += m2b + d * d * n * nb / tot;
-    n = tot;
+    snm += nb * pmean[(long long)b * C + c];
   }
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float n2 = __shfl_xor(n, o, 64), mean2 = __shfl_xor(mean, o, 64), m22 = __shfl_xor(m2, o, 64);
-    const float tot = n + n2;
-    if (tot > 0.f) {
-      // symmetric form so both partners compute the identical result
-      const float d = mean2 - mean;
-      const float nm = (n * mean + n2 * mean2) / tot;
-      m2 = m2 + m22 + d * d * (n * n2 / tot);
-      mean = nm;
-      n = tot;
-    }
+  const float n = (float)N;
+  const float mean = block_sum256(snm, red) / n;
+  float sm2 = 0.f;
+  for (int b = l; b < nblk; b += 256) {
+    const float nb = (float)max(0LL, min((long long)R, N - (long long)b * R));
+    const float d = pmean[(long long)b * C + c] - mean;
+    sm2 += pm2[(long long)b * C + c] + nb * d * d;
   }
+  const float m2 = block_sum256(sm2, red);
   if (l == 0) {
     const float var = m2 / n;
     mean_out[c] = mean;
@@ -274,31 +331,63 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(const float* __restrict
 }
 
 // y = act((x - mean) * rstd * gamma + beta (+ res)); 8 channels per thread (C % 8 == 0).
+// The grid stride (gridDim.x * 256 threads) is a multiple of C/8 whenever 256 % (C/8) == 0, so
+// each thread keeps ONE group of 8 channels for its whole grid-stride loop: the per-channel
+// affine coefficients are computed once per thread (not 32 scalar parameter loads per 16-B
+// group), and two rows are processed per iteration so two loads are in flight per stream.
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                       const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, long long N, int C, int relu) {
   const int cg = C / 8;
-  const int total = (int)(N * cg);
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-    const int row = i / cg, c = (i - row * cg) * 8;
-    const size_t off = (size_t)row * C + c;
-    uint4 v = *(const uint4*)(x + off);
-    uint32_t u[4] = {v.x, v.y, v.z, v.w};
-    float o[8], rr[8];
-    if (res) {
-      uint4 q = *(const uint4*)(res + off);
-      uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        rr[2 * e] = __uint_as_float(w[e] << 16);
-        rr[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-      }
-    }
+  const long long total = N * cg;
+  const long long i0 = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
+  if (stride % cg == 0) {
+    const int c = (int)(i0 % cg) * 8;
+    float ka[8], kb[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float xv = e & 1 ? __uint_as_float(u[e >> 1] & 0xffff0000u) : __uint_as_float(u[e >> 1] << 16);
-      float t = (xv - mean[c + e]) * rstd[c + e] * gamma[c + e] + beta[c + e];
+      ka[e] = rstd[c + e] * gamma[c + e];
+      kb[e] = beta[c + e] - mean[c + e] * ka[e];
+    }
+    for (long long i = i0; i < total; i += 2 * stride) {
+      const bool two = i + stride < total;
+      const uint4 v0 = *(const uint4*)(x + i * 8);
+      uint4 v1 = v0, q0 = v0, q1 = v0;
+      if (two) v1 = *(const uint4*)(x + (i + stride) * 8);
+      if (res) {
+        q0 = *(const uint4*)(res + i * 8);
+        if (two) q1 = *(const uint4*)(res + (i + stride) * 8);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        float xv[8], rr[8], o[8];
+        unpack8(h ? v1 : v0, xv);
+        if (res) unpack8(h ? q1 : q0, rr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = fmaf(xv[e], ka[e], kb[e]);
+          if (res) t += rr[e];
+          if (relu) t = fmaxf(t, 0.f);
+          o[e] = t;
+        }
+        *(uint4*)(y + (i + h * stride) * 8) =
+            make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
+      }
+    }
+    return;
+  }
+  for (long long i = i0; i < total; i += stride) {
+    const long long row = i / cg;
+    const int c = (int)(i - row * cg) * 8;
+    const size_t off = (size_t)row * C + c;
+    float xv[8], rr[8], o[8];
+    unpack8(*(const uint4*)(x + off), xv);
+    if (res) unpack8(*(const uint4*)(res + off), rr);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = (xv[e] - mean[c + e]) * rstd[c + e] * gamma[c + e] + beta[c + e];
       if (res) t += rr[e];
       if (relu) t = fmaxf(t, 0.f);
       o[e] = t;
@@ -325,6 +414,9 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __rest
 }
 
 // dx = gamma*rstd/N * (N*g - sum(g) - xhat*sum(g*xhat)); dres = g (when res given). 8 ch/thread.
+// dx = gamma*rstd*(g - dbeta/N - xhat*dgamma/N) = A*g + B*x + D per channel (g: dy masked by
+// y > 0 when the forward fused a ReLU); dres = g.  Coefficients hoisted per thread as in
+// bn_apply_kernel.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                           const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -332,25 +424,38 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long N,
                                                           int C, int relu) {
   const int cg = C / 8;
-  const int total = (int)(N * cg);
+  const long long total = N * cg;
   const float invN = 1.f / (float)N;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-    const int row = i / cg, c = (i - row * cg) * 8;
-    const size_t off = (size_t)row * C + c;
+  const long long i0 = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
+  const bool hoist = stride % cg == 0;
+  float kA[8], kB[8], kD[8];
+  auto coef = [&](int c) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float r = rstd[c + e], gr = gamma[c + e] * r;
+      kA[e] = gr;
+      kB[e] = -gr * r * dgamma[c + e] * invN;
+      kD[e] = -gr * dbeta[c + e] * invN - kB[e] * mean[c + e];
+    }
+  };
+  if (hoist) coef((int)(i0 % cg) * 8);
+  for (long long i = i0; i < total; i += stride) {
+    if (!hoist) coef((int)(i % cg) * 8);
+    const size_t off = (size_t)i * 8;
+    const uint4 g4 = *(const uint4*)(dy + off), x4 = *(const uint4*)(x + off);
+    uint4 y4 = g4;
+    if (relu) y4 = *(const uint4*)(y + off);
     float gv[8], xv[8], o[8];
-    ld8f(dy + off, gv);
-    ld8f(x + off, xv);
+    unpack8(g4, gv);
+    unpack8(x4, xv);
     if (relu) {
       float yv[8];
-      ld8f(y + off, yv);
+      unpack8(y4, yv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float xh = (xv[e] - mean[c + e]) * rstd[c + e];
-      o[e] = gamma[c + e] * rstd[c + e] * (gv[e] - dbeta[c + e] * invN - xh * dgamma[c + e] * invN);
-    }
+    for (int e = 0; e < 8; ++e) o[e] = fmaf(kA[e], gv[e], fmaf(kB[e], xv[e], kD[e]));
     *(uint4*)(dx + off) = make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
     if (dres)
       *(uint4*)(dres + off) =
@@ -501,14 +606,14 @@ extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean,
                            const float* pm2, int p_nblk, int p_R, long long* nbt, hipStream_t st) {
   if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
   if (training && pmean) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(64), 0, st, pmean, pm2, p_nblk, N, p_R, C, eps, momentum, mean,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, pmean, pm2, p_nblk, N, p_R, C, eps, momentum, mean,
                        rstd, running_mean, running_var, nbt);
   } else if (training) {
     const int R = (int)((N + nblk - 1) / nblk);
     hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)nullptr,
                        (const bf16_t*)nullptr, (const float*)nullptr, (const float*)nullptr, N, C, R, 0, ws,
                        ws + (long long)nblk * C);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)ws,
                        (const float*)(ws + (long long)nblk * C), nblk, N, R, C, eps, momentum, mean, rstd, running_mean,
                        running_var, nbt);
   }
