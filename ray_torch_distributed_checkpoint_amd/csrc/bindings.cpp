@@ -354,7 +354,8 @@ static void swiglu_bwd(Tensor gu, Tensor dh, Tensor dgu) {
 // [ceil(M/128)][N] fp32; returns the rows per statistics tile (128 or 256).
 static int64_t conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K,
                          int64_t ld_other, int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad,
-                         c10::optional<Tensor> ws, c10::optional<Tensor> stats_mean, c10::optional<Tensor> stats_m2) {
+                         c10::optional<Tensor> ws, c10::optional<Tensor> stats_mean, c10::optional<Tensor> stats_m2,
+                         c10::optional<Tensor> accumulate) {
   check_dev(X, "X");
   check_dev(other, "other");
   TORCH_CHECK(X.is_contiguous() && X.dim() == 4 && X.scalar_type() == at::kBFloat16, "conv_gemm: X must be NHWC bf16");
@@ -392,6 +393,13 @@ static int64_t conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t
                 "conv_gemm: statistics buffers too small");
     a.stats_mean = stats_mean->data_ptr<float>();
     a.stats_m2 = stats_m2->data_ptr<float>();
+  }
+  if (accumulate.has_value()) {  // C = conv(...) + accumulate (mode 1: a residual-path gradient)
+    TORCH_CHECK(mode == 1 && accumulate->scalar_type() == C.scalar_type() && accumulate->is_contiguous() &&
+                    accumulate->numel() == C.numel(),
+                "conv_gemm: accumulate must match C (mode 1)");
+    a.Cin = accumulate->data_ptr();
+    a.beta = 1.f;
   }
   check_rc(rtdc_conv_gemm(&a, (int)mode, cur_stream()), "conv_gemm");
   return bm;

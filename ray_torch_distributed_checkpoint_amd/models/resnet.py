@@ -38,10 +38,10 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(num_features))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
-    def forward(self, x, residual=None, relu: bool = False):
+    def forward(self, x, residual=None, relu: bool = False, residual_grad_to=None):
         return cnn.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                               self.momentum, self.eps, residual=residual, relu=relu,
-                              num_batches_tracked=self.num_batches_tracked)
+                              num_batches_tracked=self.num_batches_tracked, residual_grad_to=residual_grad_to)
 
     def extra_repr(self):
         return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, layout=NHWC"
@@ -59,10 +59,10 @@ class Conv2d(nn.Module):
             w = w.to(memory_format=torch.channels_last)
         self.weight = nn.Parameter(w)
 
-    def forward(self, x):
+    def forward(self, x, grad_accum=None):
         # every convolution of the network feeds a BatchNorm: its statistics come out of the
         # GEMM epilogue (training mode), the BN then skips its own pass over the activation
-        return cnn.conv2d(x, self.weight, self.stride, self.pad, bn_stats=self.training)
+        return cnn.conv2d(x, self.weight, self.stride, self.pad, bn_stats=self.training, grad_accum=grad_accum)
 
     def extra_repr(self):
         o, i, k, _ = self.weight.shape
@@ -86,6 +86,12 @@ class BasicBlock(nn.Module):
         self.downsample = Downsample(cin, cout, stride) if (stride != 1 or cin != cout) else None
 
     def forward(self, x):
+        if self.downsample is None and x.is_cuda and torch.is_grad_enabled():
+            # identity shortcut: its gradient (bn2's residual gradient) is added inside conv1's
+            # dgrad GEMM epilogue instead of by an autograd add over the block input
+            stash = cnn.GradStash()
+            h = self.bn1(self.conv1(x, grad_accum=stash), relu=True)
+            return self.bn2(self.conv2(h), residual=x, relu=True, residual_grad_to=stash)
         h = self.bn1(self.conv1(x), relu=True)
         sc = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
         return self.bn2(self.conv2(h), residual=sc, relu=True)

@@ -79,7 +79,8 @@ def _implicit_ok(C: int, M: int) -> bool:
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, bn_stats=False):
+    def forward(ctx, x, w, stride, pad, bn_stats=False, stash=None):
+        ctx.stash = stash
         B, H, W, C = x.shape
         Cout, Cin, KH, KW = w.shape
         assert Cin == C, (x.shape, w.shape)
@@ -96,7 +97,7 @@ class _Conv2d(torch.autograd.Function):
                 nt = (M + 127) // 128
                 smean = torch.empty((nt, Cout), dtype=torch.float32, device=x.device)
                 sm2 = torch.empty((nt, Cout), dtype=torch.float32, device=x.device)
-            bm = gpu_ext().conv_gemm(x, wm, y, 1, M, Cout, K, K, Ho, Wo, KW, stride, pad, None, smean, sm2)
+            bm = gpu_ext().conv_gemm(x, wm, y, 1, M, Cout, K, K, Ho, Wo, KW, stride, pad, None, smean, sm2, None)
             ctx.save_for_backward(x, wm)
             ctx.w = w
             ctx.geom = (B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, K, M, M, "implicit")
@@ -137,7 +138,7 @@ class _Conv2d(torch.autograd.Function):
                 tw, direct = _grad_matrix(ctx.w, K)
                 dwm = direct if direct is not None else torch.empty((Cout, K), dtype=torch.float32, device=dy.device)
                 ws = G.workspace(dy.device, G.SPLITK_WS_ELEMS, "splitk")
-                gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws, None, None)
+                gpu_ext().conv_gemm(x, dy2, dwm, 2, Cout, K, Mp, Cout, Ho, Wo, KW, stride, pad, ws, None, None, None)
                 if direct is not None:
                     dw = tw  # written in place into the flat gradient buffer
                 else:
@@ -150,13 +151,17 @@ class _Conv2d(torch.autograd.Function):
                     s = shadow_of_w(ctx, wm, Cout, C, KH, KW)
                     dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                     Kt = KH * KW * Cout
+                    acc = ctx.stash.take() if ctx.stash is not None else None
                     gpu_ext().conv_gemm(dy, s, dx.view(B * H * W, C), 1, B * H * W, C, Kt, Kt, H, W, KW, 1,
-                                        KH - 1 - pad, None, None, None)
+                                        KH - 1 - pad, None, None, None,
+                                        None if acc is None else acc.contiguous().view(B * H * W, C))
                 else:
                     dcols = G.linear_dgrad(dy2, wm)  # [Mp, K]
                     dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                     gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
-            return dx, dw, None, None, None
+                    if ctx.stash is not None and ctx.stash.t is not None:
+                        dx = dx + ctx.stash.take()
+            return dx, dw, None, None, None, None
         cols = saved
         if ctx.needs_input_grad[1]:
             dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
@@ -170,7 +175,9 @@ class _Conv2d(torch.autograd.Function):
             else:
                 dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                 gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
-        return dx, dw, None, None, None
+            if ctx.stash is not None and ctx.stash.t is not None:
+                dx = dx + ctx.stash.take()
+        return dx, dw, None, None, None, None
 
 
 def shadow_of_w(ctx, wm, Cout, C, KH, KW):
@@ -186,15 +193,34 @@ def conv2d_ref(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) 
     return y.permute(0, 2, 3, 1).contiguous()
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, bn_stats: bool = False) -> torch.Tensor:
+class GradStash:
+    """Hand-off of a residual-branch gradient between two autograd nodes of one residual block
+    (`batch_norm(..., residual_grad_to=stash)` -> `conv2d(x, ..., grad_accum=stash)`): the
+    shortcut's gradient is added inside the convolution's dgrad GEMM epilogue (C = dgrad + dres)
+    instead of by a separate autograd add kernel over the activation."""
+
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+    def take(self):
+        t, self.t = self.t, None
+        return t
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, bn_stats: bool = False,
+           grad_accum: GradStash | None = None) -> torch.Tensor:
     """NHWC convolution (no bias): x [B, H, W, Cin] -> [B, Ho, Wo, Cout]; w [Cout, Cin, KH, KW].
     bn_stats=True also computes the per-channel BatchNorm statistics of the output inside the
-    GEMM epilogue; `batch_norm` on exactly this tensor then skips its statistics pass."""
+    GEMM epilogue; `batch_norm` on exactly this tensor then skips its statistics pass.
+    grad_accum: a GradStash whose tensor (x's gradient from another consumer) is added to this
+    convolution's input gradient."""
     if x.is_cuda:
         require_dtype(x, "conv2d")
     else:
         return conv2d_ref(x, w, stride, pad)
-    y = _Conv2d.apply(x, w, stride, pad, bn_stats)
+    y = _Conv2d.apply(x, w, stride, pad, bn_stats, grad_accum)
     st = getattr(y.grad_fn, "stats", None) if y.grad_fn is not None else None
     if st is not None:
         y._rtdc_bn_stats = st  # (mean [tiles, C], M2 [tiles, C], rows per tile)
@@ -209,7 +235,8 @@ def _bn_blocks(N: int, C: int) -> int:
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
-                num_batches_tracked=None):
+                num_batches_tracked=None, res_stash=None):
+        ctx.res_stash = res_stash
         C = x.shape[-1]
         x = x.contiguous()
         N = x.numel() // C
@@ -255,7 +282,10 @@ class _BatchNorm(torch.autograd.Function):
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
         gpu_ext().bn_bwd(dy, y if ctx.relu else x, x, mean, rstd, weight, dx, dres, dgamma, dbeta, ctx.relu, ws, nblk)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        if dres is not None and ctx.res_stash is not None:
+            ctx.res_stash.t = dres  # added by the block's first convolution (its dgrad epilogue)
+            dres = None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 def batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5,
@@ -270,7 +300,8 @@ def batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentu
 
 
 def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
-               eps: float = 1e-5, residual=None, relu: bool = False, num_batches_tracked=None) -> torch.Tensor:
+               eps: float = 1e-5, residual=None, relu: bool = False, num_batches_tracked=None,
+               residual_grad_to: GradStash | None = None) -> torch.Tensor:
     """y = relu?(BN(x) (+ residual)) over the channel (last) axis of an NHWC tensor.  In training
     mode `num_batches_tracked` (int64 buffer) is incremented by the statistics kernel."""
     if x.is_cuda:
@@ -280,7 +311,7 @@ def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, trainin
             num_batches_tracked.add_(1)
         return batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
     return _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
-                            num_batches_tracked)
+                            num_batches_tracked, residual_grad_to)
 
 
 class _MaxPool(torch.autograd.Function):

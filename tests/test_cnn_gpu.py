@@ -163,7 +163,7 @@ def _bf16_emulated_grads(model, x, t):
     from ray_torch_distributed_checkpoint_amd.ops import cnn
 
     oc, ob = cnn.conv2d, cnn.batch_norm
-    R.cnn.conv2d = lambda x_, w, s=1, p=0, bn_stats=False: oc(x_, w.bfloat16().float(), s, p).bfloat16().float()
+    R.cnn.conv2d = lambda x_, w, s=1, p=0, bn_stats=False, grad_accum=None: oc(x_, w.bfloat16().float(), s, p).bfloat16().float()
     R.cnn.batch_norm = lambda *a, **k: ob(*a, **k).bfloat16().float()
     try:
         F.cross_entropy(model(x), t).backward()
