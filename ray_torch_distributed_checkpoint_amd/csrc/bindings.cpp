@@ -63,8 +63,8 @@ int rtdc_swiglu_fwd(const void* gu, void* h, long long M, int F, hipStream_t st)
 int rtdc_swiglu_bwd(const void* gu, const void* dh, void* dgu, long long M, int F, hipStream_t st);
 int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
                 int pad, int K, int Kp, hipStream_t st);
-int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
-                int pad, int K, int Kp, hipStream_t st);
+int rtdc_col2im(const void* dcols, void* dx, const void* addend, int B, int H, int W, int C, int Ho, int Wo, int KH,
+                int KW, int stride, int pad, int K, int Kp, hipStream_t st);
 int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma, const float* beta,
                 float* running_mean, float* running_var, long long N, int C, float eps, float momentum, int training,
                 int relu, float* ws, int nblk, const float* pmean, const float* pm2, int p_nblk, int p_R,
@@ -415,11 +415,18 @@ static void im2col(Tensor x, Tensor cols, int64_t Ho, int64_t Wo, int64_t KH, in
            "im2col");
 }
 static void col2im(Tensor dcols, Tensor dx, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride,
-                   int64_t pad) {
+                   int64_t pad, c10::optional<Tensor> addend) {
   TORCH_CHECK(dx.is_contiguous() && dcols.is_contiguous() && dx.dim() == 4, "col2im: contiguous NHWC expected");
   const int64_t B = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3), K = KH * KW * C, Kp = dcols.size(1);
   TORCH_CHECK(dcols.size(0) == B * Ho * Wo && Kp >= K, "col2im: bad cols shape");
-  check_rc(rtdc_col2im(dcols.data_ptr(), dx.data_ptr(), (int)B, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH,
+  TORCH_CHECK(dcols.scalar_type() == at::kBFloat16 && dx.scalar_type() == at::kBFloat16, "col2im: bf16 expected");
+  const void* add = nullptr;
+  if (addend.has_value()) {
+    TORCH_CHECK(addend->scalar_type() == at::kBFloat16 && addend->is_contiguous() && addend->numel() == dx.numel(),
+                "col2im: addend must be a contiguous bf16 tensor shaped like dx");
+    add = addend->data_ptr();
+  }
+  check_rc(rtdc_col2im(dcols.data_ptr(), dx.data_ptr(), add, (int)B, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH,
                        (int)KW, (int)stride, (int)pad, (int)K, (int)Kp, cur_stream()),
            "col2im");
 }

@@ -100,8 +100,9 @@ __device__ __forceinline__ uint4 pack8(const float* o) {
 
 // dx[b,h,w,c] = sum_{kh,kw} dcols[(b,ho,wo)][(kh,kw,c)] over taps with ho*s - p + kh = h.
 // 8 channels per thread (C % 8 == 0).
+// addend (nullable, same layout as dx): the input's gradient from another consumer, summed in.
 __global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx,
-                                                    ConvGeom g) {
+                                                    const bf16_t* __restrict__ addend, ConvGeom g) {
   const int cg = g.C / 8;
   const int total = g.B * g.H * g.W * cg;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
@@ -109,6 +110,7 @@ __global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ 
     const int q = pix / g.W, w = pix - q * g.W;
     const int b = q / g.H, h = q - b * g.H;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (addend) acc8(acc, *(const uint4*)(addend + (size_t)pix * g.C + c));
     for (int kh = 0; kh < g.KH; ++kh) {
       const int hs = h + g.pad - kh;
       if (hs < 0) break;
@@ -589,12 +591,12 @@ extern "C" int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-extern "C" int rtdc_col2im(const void* dcols, void* dx, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW,
-                           int stride, int pad, int K, int Kp, hipStream_t st) {
+extern "C" int rtdc_col2im(const void* dcols, void* dx, const void* addend, int B, int H, int W, int C, int Ho,
+                           int Wo, int KH, int KW, int stride, int pad, int K, int Kp, hipStream_t st) {
   if (C % 8 != 0 || (long long)B * Ho * Wo * Kp >= (1LL << 31) || (long long)B * H * W * C >= (1LL << 31)) return 1;
   ConvGeom g{B, H, W, C, Ho, Wo, KH, KW, stride, pad, K, Kp};
   hipLaunchKernelGGL(col2im_kernel, dim3(gsz((long long)B * H * W * (C / 8))), dim3(256), 0, st,
-                     (const bf16_t*)dcols, (bf16_t*)dx, g);
+                     (const bf16_t*)dcols, (bf16_t*)dx, (const bf16_t*)addend, g);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -86,12 +86,15 @@ class BasicBlock(nn.Module):
         self.downsample = Downsample(cin, cout, stride) if (stride != 1 or cin != cout) else None
 
     def forward(self, x):
-        if self.downsample is None and x.is_cuda and torch.is_grad_enabled():
-            # identity shortcut: its gradient (bn2's residual gradient) is added inside conv1's
-            # dgrad GEMM epilogue instead of by an autograd add over the block input
-            stash = cnn.GradStash()
+        if x.is_cuda and torch.is_grad_enabled():
+            # the block input's two gradients (conv1's and the shortcut's) are summed inside the
+            # dgrad kernel of whichever backward runs last, not by an autograd add over x
+            stash = cnn.GradStash(2)
             h = self.bn1(self.conv1(x, grad_accum=stash), relu=True)
-            return self.bn2(self.conv2(h), residual=x, relu=True, residual_grad_to=stash)
+            if self.downsample is None:
+                return self.bn2(self.conv2(h), residual=x, relu=True, residual_grad_to=stash)
+            sc = self.downsample[1](self.downsample[0](x, grad_accum=stash))
+            return self.bn2(self.conv2(h), residual=sc, relu=True)
         h = self.bn1(self.conv1(x), relu=True)
         sc = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
         return self.bn2(self.conv2(h), residual=sc, relu=True)

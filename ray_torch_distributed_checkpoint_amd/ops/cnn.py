@@ -145,22 +145,21 @@ class _Conv2d(torch.autograd.Function):
                     dw = dwm.view(Cout, KH, KW, C).permute(0, 3, 1, 2)
                     dw = tw.copy_(dw) if tw is not None else dw.contiguous()
             if ctx.needs_input_grad[0]:
+                acc = _arrive(ctx.stash)
+                dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                 if stride == 1 and _implicit_ok(Cout, B * H * W):
                     # stride-1 dgrad is itself a convolution of dY with the flipped, transposed
-                    # kernel (padding KH-1-pad): implicit GEMM again, no column matrix
+                    # kernel (padding KH-1-pad): implicit GEMM again, no column matrix; a pending
+                    # gradient of x from its other consumer is added in the epilogue (beta = 1)
                     s = shadow_of_w(ctx, wm, Cout, C, KH, KW)
-                    dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                     Kt = KH * KW * Cout
-                    acc = ctx.stash.take() if ctx.stash is not None else None
                     gpu_ext().conv_gemm(dy, s, dx.view(B * H * W, C), 1, B * H * W, C, Kt, Kt, H, W, KW, 1,
                                         KH - 1 - pad, None, None, None,
-                                        None if acc is None else acc.contiguous().view(B * H * W, C))
+                                        None if acc is None else acc.view(B * H * W, C))
                 else:
                     dcols = G.linear_dgrad(dy2, wm)  # [Mp, K]
-                    dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
-                    gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
-                    if ctx.stash is not None and ctx.stash.t is not None:
-                        dx = dx + ctx.stash.take()
+                    gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad, acc)
+                dx = _depart(ctx.stash, dx)
             return dx, dw, None, None, None, None
         cols = saved
         if ctx.needs_input_grad[1]:
@@ -169,15 +168,38 @@ class _Conv2d(torch.autograd.Function):
             tw = grad_target(ctx.w)
             dw = tw.copy_(dw) if tw is not None else dw.contiguous()
         if ctx.needs_input_grad[0]:
+            acc = _arrive(ctx.stash)
             dcols = G.linear_dgrad(dy2, wm)  # [Mp, Kp] bf16
             if mode == "direct":
                 dx = dcols.view(B, H, W, C)
+                if acc is not None:
+                    dx = dx + acc
             else:
                 dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
-                gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad)
-            if ctx.stash is not None and ctx.stash.t is not None:
-                dx = dx + ctx.stash.take()
+                gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad, acc)
+            dx = _depart(ctx.stash, dx)
         return dx, dw, None, None, None, None
+
+
+def _arrive(stash):
+    """A contributor to a joined input gradient starts its backward: returns the gradient the
+    other contributors already left (to be summed into this one's output), or None."""
+    if stash is None:
+        return None
+    stash.left -= 1
+    if stash.left > 0:
+        return None
+    t = stash.take()
+    return None if t is None else t.contiguous()
+
+
+def _depart(stash, dx):
+    """...and ends it: a contributor that is not the last leaves its gradient in the stash and
+    returns None to autograd; the last one returns the complete sum."""
+    if stash is None or stash.left == 0:
+        return dx
+    stash.t = dx if stash.t is None else stash.t + dx
+    return None
 
 
 def shadow_of_w(ctx, wm, Cout, C, KH, KW):
@@ -194,15 +216,17 @@ def conv2d_ref(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0) 
 
 
 class GradStash:
-    """Hand-off of a residual-branch gradient between two autograd nodes of one residual block
-    (`batch_norm(..., residual_grad_to=stash)` -> `conv2d(x, ..., grad_accum=stash)`): the
-    shortcut's gradient is added inside the convolution's dgrad GEMM epilogue (C = dgrad + dres)
-    instead of by a separate autograd add kernel over the activation."""
+    """Join of the gradient of ONE tensor consumed by `parts` native ops of a residual block
+    (`batch_norm(..., residual_grad_to=stash)` / `conv2d(x, ..., grad_accum=stash)`): whichever
+    contributor's backward runs last adds the gradients the others left inside its own output
+    kernel (the dgrad GEMM epilogue with beta = 1, or col2im's addend), and autograd never runs
+    an add over the activation.  Works in any backward order; one stash per forward."""
 
-    __slots__ = ("t",)
+    __slots__ = ("t", "left")
 
-    def __init__(self):
+    def __init__(self, parts: int = 2):
         self.t = None
+        self.left = parts
 
     def take(self):
         t, self.t = self.t, None
@@ -283,8 +307,12 @@ class _BatchNorm(torch.autograd.Function):
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
         gpu_ext().bn_bwd(dy, y if ctx.relu else x, x, mean, rstd, weight, dx, dres, dgamma, dbeta, ctx.relu, ws, nblk)
         if dres is not None and ctx.res_stash is not None:
-            ctx.res_stash.t = dres  # added by the block's first convolution (its dgrad epilogue)
-            dres = None
+            # the shortcut's gradient: normally added by the block's convolution(s) of the same
+            # input inside their dgrad kernels
+            acc = _arrive(ctx.res_stash)
+            if acc is not None:
+                dres = dres + acc
+            dres = _depart(ctx.res_stash, dres)
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 

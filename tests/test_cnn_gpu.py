@@ -226,3 +226,38 @@ def test_conv_fused_bn_statistics(B, H, C, Cout, s):
     _close(out_fused, out_ref, 0.01, "y")
     _close(rm1, rm2, 1e-4, "running_mean")
     _close(rv1, rv2, 1e-4, "running_var")
+
+
+@pytest.mark.parametrize("shortcut", ["identity", "downsample"])
+def test_grad_join_matches_autograd_add(shortcut):
+    """GradStash: the block input's two gradients summed inside the dgrad kernels (implicit GEMM
+    epilogue / col2im addend / BN residual) == autograd's own add, in either backward order."""
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(0)
+    B, H, C = 4, 16, 64
+    Cout = C if shortcut == "identity" else 128
+    s = 1 if shortcut == "identity" else 2
+    x0 = torch.randn(B, H, H, C, device=DEV).bfloat16()
+    w1 = (torch.randn(Cout, C, 3, 3, device=DEV) * 0.05)
+    wd = (torch.randn(Cout, C, 1, 1, device=DEV) * 0.1)
+    g = torch.ones(Cout, device=DEV)
+    b = torch.zeros(Cout, device=DEV)
+    dy = torch.randn(B, H // s, H // s, Cout, device=DEV).bfloat16()
+
+    def run(join):
+        x = x0.clone().requires_grad_(True)
+        st = cnn.GradStash(2) if join else None
+        h = cnn.conv2d(x, w1, s, 1, grad_accum=st)
+        rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+        if shortcut == "identity":
+            y = cnn.batch_norm(h, g, b, rm, rv, True, residual=x, relu=True, residual_grad_to=st)
+        else:
+            sc = cnn.conv2d(x, wd, s, 0, grad_accum=st)
+            y = cnn.batch_norm(h, g, b, rm, rv, True, residual=sc, relu=True)
+        y.backward(dy)
+        return x.grad.float()
+
+    ref, got = run(False), run(True)
+    err = (got - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
