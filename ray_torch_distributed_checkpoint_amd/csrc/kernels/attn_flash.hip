@@ -55,7 +55,18 @@ struct Args {
   bf16_t* dqkv;       // [B, T, W]
   int B, T, H, Hkv;
   float scale;
+  int xcd_remap;  // 1: the blocks of one head share an XCD (and its L2)
 };
+
+// (block-in-head, head) of this workgroup
+__device__ __forceinline__ void grid_pos(const Args& a, int& x, int& y) {
+  if (a.xcd_remap) {
+    xcd_grid(x, y);
+  } else {
+    x = blockIdx.x;
+    y = blockIdx.y;
+  }
+}
 
 // [64 rows][DH] bf16 LDS image, 16-B chunks XOR-swizzled per row (bank-conflict-free
 // ds_read_b128 row reads; 2-way on the transposing reads).
@@ -186,8 +197,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   const int nqb = a.T / BQ;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest (longest causal prefix) blocks first
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int bx, bh;
+  grid_pos(a, bx, bh);
+  const int qb = nqb - 1 - bx;  // heaviest (longest causal prefix) blocks first
+  const int b = bh / a.H, h = bh % a.H;
   const int grp = a.H / a.Hkv, kvh = h / grp;
   const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
   const bf16_t* base = a.qkv + (long long)b * a.T * W;
@@ -324,8 +337,10 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   const int nqb = a.T / BQ2;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest (longest causal prefix) blocks first
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int bx, bh;
+  grid_pos(a, bx, bh);
+  const int qb = nqb - 1 - bx;  // heaviest (longest causal prefix) blocks first
+  const int b = bh / a.H, h = bh % a.H;
   const int grp = a.H / a.Hkv, kvh = h / grp;
   const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
   const bf16_t* base = a.qkv + (long long)b * a.T * W;
@@ -518,8 +533,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   const int nkb = a.T / BKV;
-  const int kb = (int)blockIdx.x;  // key block
-  const int bk = blockIdx.y, b = bk / a.Hkv, kvh = bk % a.Hkv;
+  int kb, bk;
+  grid_pos(a, kb, bk);  // key block, (batch, kv-head)
+  const int b = bk / a.Hkv, kvh = bk % a.Hkv;
   const int grp = a.H / a.Hkv;
   const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
   const bf16_t* base = a.qkv + (long long)b * a.T * W;
@@ -637,8 +653,10 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   const int nqb = a.T / BQ;
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int bx, bh;
+  grid_pos(a, bx, bh);
+  const int qb = nqb - 1 - bx;
+  const int b = bh / a.H, h = bh % a.H;
   const int grp = a.H / a.Hkv, kvh = h / grp;
   const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
   const bf16_t* base = a.qkv + (long long)b * a.T * W;
@@ -745,6 +763,11 @@ using namespace rtdc;
 // every extra slot costs a co-resident block per CU (32 / 48 / 64 KiB of LDS per block), and
 // at these 8-16-step loops occupancy hides more HBM latency than a deeper ring.  Dh = 128
 // stays at 2 (a third slot leaves one block per CU).
+static int fa_xcd() {
+  static const int v = getenv("RTDC_FA_XCD") ? atoi(getenv("RTDC_FA_XCD")) : 1;
+  return v;
+}
+
 static int fa_ns(int Dh) {
   static const int forced = getenv("RTDC_FA_NS") ? atoi(getenv("RTDC_FA_NS")) : 0;
   if (Dh == 128) return 2;
@@ -763,7 +786,7 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.lse = lse;
-  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
+  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd();
   // measured (benchmarks/attn_bench.py, before the DMA ring): 32 rows/wave wins at Dh = 128
   // (Llama: 101 vs 108 us), 16 rows/wave at Dh = 64 (GPT-2: 100 vs 109 us); RTDC_FA_FWD=1|2
   // forces one
@@ -796,7 +819,7 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta;
   a.dqkv = (bf16_t*)dqkv;
-  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale;
+  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd();
   dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H);
   const int ns = fa_ns(Dh);
   if (Dh == 64) {

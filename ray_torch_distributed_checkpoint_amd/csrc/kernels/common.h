@@ -36,6 +36,20 @@ __device__ __forceinline__ bf16x4 ds_tr16(const char* p) {
   return r;
 }
 
+// XCD-aware bijective remap of a 2-D grid (cdna_hip_programming.md T1): the hardware deals
+// consecutive workgroups round-robin to the 8 XCDs (flat id % 8), each with its own L2.  Returns
+// the logical (x, y) such that each XCD receives a CONTIGUOUS run of the x-fastest logical order:
+// the blocks of one y (e.g. all query blocks of one attention head) share one L2 instead of
+// pulling the same K/V through all eight.
+__device__ __forceinline__ void xcd_grid(int& x, int& y) {
+  const int nx = gridDim.x, n = nx * gridDim.y;
+  const int bid = blockIdx.x + blockIdx.y * nx;
+  const int xcd = bid & 7, q = n >> 3, r = n & 7;
+  const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  y = l / nx;
+  x = l - y * nx;
+}
+
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ bf16x8 tr_use(TrPair& f) {
