@@ -55,13 +55,14 @@ struct Args {
   bf16_t* dqkv;       // [B, T, W]
   int B, T, H, Hkv;
   float scale;
-  int xcd_remap;  // 1: the blocks of one head share an XCD (and its L2)
+  int xcd_remap;  // 1: the blocks of one head share an XCD (and its L2); 2: + heavy blocks first
+                  // across all the XCD's heads
 };
 
 // (block-in-head, head) of this workgroup
 __device__ __forceinline__ void grid_pos(const Args& a, int& x, int& y) {
   if (a.xcd_remap) {
-    xcd_grid(x, y);
+    xcd_grid(x, y, a.xcd_remap == 2);
   } else {
     x = blockIdx.x;
     y = blockIdx.y;
@@ -189,9 +190,11 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 }
 
 // ------------------------------------------------------------------------------ forward
-template <int DH, int NS>
+// DBV: output column blocks of 16 whose V fragments are read per batch (registers vs LDS
+// latency per batch)
+template <int DH, int NS, int DBV = 4>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
-  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2, PER = DH / 16;
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < DBV ? DT : DBV, TILE = 64 * DH * 2, PER = DH / 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE];  // K[NS], V[NS]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -271,8 +274,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
         s[t][r] = v;
         mx = fmaxf(mx, v);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_rows4(mx);
     // lazy rescale: the running max moves (and O, l are rescaled) only when some row of the
     // wave would otherwise see probabilities above 2^8 - after the first key blocks the max
     // rarely grows that much, so the 4*DT+4 multiplies and the exp are skipped (wave-uniform)
@@ -423,8 +425,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
             sc[qg][t][r] = v;
             mx = fmaxf(mx, v);
           }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = max_rows4(mx);
         const float mn = fmaxf(m[qg], mx * c);
         const float alpha = fexp2(m[qg] - mn);
         m[qg] = mn;
@@ -473,9 +474,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
 #undef VT
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
-    float lt = l[qg];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = sum_rows4(l[qg]);
     const float inv = 1.f / lt;
     bf16_t* orow = a.out + ((long long)b * a.T + myq[qg]) * C + h * DH;
 #pragma unroll
@@ -799,7 +798,9 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
     else FA_DISPATCH(fa::fwd2_kernel, 128, ns, grid, a);
   } else {
     dim3 grid(T / 64, B * H);
-    if (Dh == 64) FA_DISPATCH(fa::fwd_kernel, 64, ns, grid, a);
+    static const int db = getenv("RTDC_FA_DB") ? atoi(getenv("RTDC_FA_DB")) : 4;
+    if (Dh == 64 && ns == 2 && db == 2) hipLaunchKernelGGL((fa::fwd_kernel<64, 2, 2>), grid, dim3(256), 0, st, a);
+    else if (Dh == 64) FA_DISPATCH(fa::fwd_kernel, 64, ns, grid, a);
     else FA_DISPATCH(fa::fwd_kernel, 128, ns, grid, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;

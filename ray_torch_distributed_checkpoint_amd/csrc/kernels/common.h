@@ -36,15 +36,50 @@ __device__ __forceinline__ bf16x4 ds_tr16(const char* p) {
   return r;
 }
 
+// max without fmaxf's NaN-canonicalising v_max x,x,x on each operand
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// all-reduce max over the lanes l, l^16, l^32, l^48 (the 4 rows of 16 lanes of a wave64) with the
+// gfx950 VALU row swaps - no LDS round trip (a __shfl_xor is a ds_bpermute plus its lgkm wait).
+// permlane16_swap(x, x) leaves rows (0,0,2,2) in one result and (1,1,3,3) in the other, and
+// permlane32_swap(x, x) the halves (lo,lo) / (hi,hi): the max of each pair is the xor-16 /
+// xor-32 reduction.
+__device__ __forceinline__ float max_rows4(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = vmax_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return vmax_raw(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
+__device__ __forceinline__ float sum_rows4(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 // XCD-aware bijective remap of a 2-D grid (cdna_hip_programming.md T1): the hardware deals
 // consecutive workgroups round-robin to the 8 XCDs (flat id % 8), each with its own L2.  Returns
 // the logical (x, y) such that each XCD receives a CONTIGUOUS run of the x-fastest logical order:
 // the blocks of one y (e.g. all query blocks of one attention head) share one L2 instead of
 // pulling the same K/V through all eight.
-__device__ __forceinline__ void xcd_grid(int& x, int& y) {
+// x_major: when every XCD gets whole rows (gridDim.y % 8 == 0), walk the XCD's rows x-major
+// instead (x = 0 of all its rows first, then x = 1, ...): with x ordered heaviest-first this
+// starts every long block early instead of leaving the last row's long block as the tail.
+__device__ __forceinline__ void xcd_grid(int& x, int& y, bool x_major = false) {
   const int nx = gridDim.x, n = nx * gridDim.y;
   const int bid = blockIdx.x + blockIdx.y * nx;
   const int xcd = bid & 7, q = n >> 3, r = n & 7;
+  if (x_major && (gridDim.y & 7) == 0) {
+    const int rows = gridDim.y >> 3, local = bid >> 3;  // this XCD: rows [xcd*rows, +rows)
+    x = local / rows;
+    y = xcd * rows + (local - x * rows);
+    return;
+  }
   const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   y = l / nx;
   x = l - y * nx;
