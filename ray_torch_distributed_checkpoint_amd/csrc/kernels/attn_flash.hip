@@ -20,7 +20,8 @@
 //   bwd_dq  : block = 64 query rows; loops over key blocks up to the diagonal.  Recomputing
 //             P here instead of accumulating dQ with float atomics keeps the backward
 //             bitwise reproducible (MI355X_MICROARCH.md §Global float atomics).
-//   delta   : D[b,h,t] = sum_d dO * O (the softmax-backward row term).
+//   delta   : D[b,h,t] = sum_d dO * O (the softmax-backward row term), computed by bwd_dq
+//             in its prologue (bwd_dq runs first); delta_kernel is the standalone form.
 // Requires T % 64 == 0 and Dh in {64, 128}.
 //
 // Pipelining (all three loops): the streamed tiles (K/V for fwd and dQ; Q, dO and the 64
@@ -51,12 +52,13 @@ struct Args {
   bf16_t* out;        // [B, T, H*Dh]
   float* lse;         // [B*H, T] row log-sum-exp of the scaled scores, base 2 (log2 domain)
   const bf16_t* dout; // [B, T, H*Dh]
-  const float* delta; // [B*H, T]
+  float* delta;       // [B*H, T] (written by bwd_dq, read by bwd_dkdv)
   bf16_t* dqkv;       // [B, T, W]
   int B, T, H, Hkv;
   float scale;
   int xcd_remap;  // 1: the blocks of one head share an XCD (and its L2); 2: + heavy blocks first
                   // across all the XCD's heads
+  int diag;       // timing-only builds (wrong results): bit 1 skips the loop's DMA waits
 };
 
 // (block-in-head, head) of this workgroup
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
         o[d0 + d] = mfma(tr_use(vq[d][1]), p1, o[d0 + d]);
       }
     }
-    if (kb + 1 < nkb) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    if (kb + 1 < nkb && !(a.diag & 1)) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
     step_barrier();
   }
 #undef KT
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
         }
       }
     }
-    if (kb + 1 < nkb) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    if (kb + 1 < nkb && !(a.diag & 1)) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
     step_barrier();
   }
 #undef KT
@@ -631,7 +633,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
         dk[e0 + d] = mfma(tr_use(fq[d][1]), d1, dk[e0 + d]);
       }
     }
-    if (it + 1 < total) wait_vm_upto(PER * (min(it + NS - 1, total - 1) - it - 1));
+    if (it + 1 < total && !(a.diag & 1)) wait_vm_upto(PER * (min(it + NS - 1, total - 1) - it - 1));
     step_barrier();
   }
   bf16_t* krow = a.dqkv + ((long long)b * a.T + mykey) * W;
@@ -681,14 +683,28 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
     of[ks] = gload8(a.dout + ((long long)b * a.T + myq) * C + h * DH + ks * 32 + g * 8);
   }
-  const float lse2 = a.lse[r], del = a.delta[r];
+  // delta = sum_d dO * O of this row (the softmax-backward row term): the lane's 8*KS columns
+  // of O against its dO fragment, summed over the 4 lane rows; stored for the dK/dV kernel,
+  // which runs after this one
+  bf16x8 ofw[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) ofw[ks] = gload8(a.out + ((long long)b * a.T + myq) * C + h * DH + ks * 32 + g * 8);
+  const float lse2 = a.lse[r];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     settle(qf[ks]);
     settle(of[ks]);
+    settle(ofw[ks]);
   }
   settle(lse2);
-  settle(del);
+  float dsum = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      dsum = fmaf(bf2f((bf16_t)of[ks][e]), bf2f((bf16_t)ofw[ks][e]), dsum);
+  const float del = sum_rows4(dsum);
+  if (g == 0) a.delta[r] = del;
   step_barrier();
 
   f32x4 dq[DT];
@@ -740,7 +756,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
         dq[e0 + d] = mfma(tr_use(fk[d][1]), d1, dq[e0 + d]);
       }
     }
-    if (kb + 1 < nkb) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    if (kb + 1 < nkb && !(a.diag & 1)) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
     step_barrier();
   }
 #undef KT
@@ -762,8 +778,15 @@ using namespace rtdc;
 // every extra slot costs a co-resident block per CU (32 / 48 / 64 KiB of LDS per block), and
 // at these 8-16-step loops occupancy hides more HBM latency than a deeper ring.  Dh = 128
 // stays at 2 (a third slot leaves one block per CU).
+static int fa_diag() {
+  static const int v = getenv("RTDC_FA_DIAG") ? atoi(getenv("RTDC_FA_DIAG")) : 0;
+  return v;
+}
+
 static int fa_xcd() {
-  static const int v = getenv("RTDC_FA_XCD") ? atoi(getenv("RTDC_FA_XCD")) : 1;
+  // 2 (default): one head's blocks share an XCD and each XCD runs the long blocks of all its
+  // heads first (GPT-2 fwd 84 -> 48 us vs the plain grid order 0); 1: XCD grouping only
+  static const int v = getenv("RTDC_FA_XCD") ? atoi(getenv("RTDC_FA_XCD")) : 2;
   return v;
 }
 
@@ -785,7 +808,7 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.lse = lse;
-  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd();
+  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd(); a.diag = fa_diag();
   // measured (benchmarks/attn_bench.py, before the DMA ring): 32 rows/wave wins at Dh = 128
   // (Llama: 101 vs 108 us), 16 rows/wave at Dh = 64 (GPT-2: 100 vs 109 us); RTDC_FA_FWD=1|2
   // forces one
@@ -809,26 +832,20 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
 extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
                               void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st) {
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
-  const long long rows = (long long)B * T * H;
-  const long long dthreads = rows * (Dh / 8);
-  if (Dh == 64)
-    hipLaunchKernelGGL(fa::delta_kernel<64>, dim3((unsigned)((dthreads + 255) / 256)), dim3(256), 0, st,
-                       (const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
-  else
-    hipLaunchKernelGGL(fa::delta_kernel<128>, dim3((unsigned)((dthreads + 255) / 256)), dim3(256), 0, st,
-                       (const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
+  // dQ first: it also computes the row terms delta = rowsum(dO * O) that dK/dV read
   fa::Args a{};
-  a.qkv = (const bf16_t*)qkv; a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta;
+  a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.dout = (const bf16_t*)dout; a.lse = (float*)lse;
+  a.delta = delta;
   a.dqkv = (bf16_t*)dqkv;
-  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd();
+  a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd(); a.diag = fa_diag();
   dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H);
   const int ns = fa_ns(Dh);
   if (Dh == 64) {
-    FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
     FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
+    FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
   } else {
-    FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
     FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
+    FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
