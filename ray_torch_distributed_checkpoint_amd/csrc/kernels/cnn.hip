@@ -290,8 +290,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
 // M2 = sum(M2_b + n_b (m_b - mean)^2) - so the loops carry no division chain (the serial
 // Welford merge over ~6k GEMM-tile partials ran 13 us per BatchNorm).  Fixed reduction order.
 __device__ __forceinline__ float block_sum256(float v, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();

@@ -110,17 +110,31 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Wave64 all-reduces entirely in the VALU: DPP within each 16-lane row (quad_perm xor 1 and
+// xor 2, row_half_mirror, row_mirror pair every lane with one from the other quad / half), then
+// the gfx950 row swaps across rows (max_rows4 above).  __shfl_xor lowers to ds_bpermute: six
+// dependent LDS round trips with an lgkm wait each.  Every lane ends with the bitwise-same value
+// (each step adds a commutative pair).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
   return v;
 }
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+__device__ __forceinline__ float row16_max(float v) {
+  v = vmax_raw(v, dpp_f<0xB1>(v));
+  v = vmax_raw(v, dpp_f<0x4E>(v));
+  v = vmax_raw(v, dpp_f<0x141>(v));
+  v = vmax_raw(v, dpp_f<0x140>(v));
   return v;
 }
+__device__ __forceinline__ float wave_sum(float v) { return sum_rows4(row16_sum(v)); }
+__device__ __forceinline__ float wave_max(float v) { return max_rows4(row16_max(v)); }
 
 // Block reduction for blockDim.x == NT (multiple of 64).  `red` must hold NT/64 floats.
 template <int NT>

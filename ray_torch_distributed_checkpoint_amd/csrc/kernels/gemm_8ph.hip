@@ -231,12 +231,7 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
       for (int c = 0; c < TNQ; ++c) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          float t = cs[c][r];
-          t += __shfl_xor(t, 1);
-          t += __shfl_xor(t, 2);
-          t += __shfl_xor(t, 4);
-          t += __shfl_xor(t, 8);
-          cs[c][r] = t;
+          cs[c][r] = row16_sum(cs[c][r]);
         }
         const int n = nrun + cno(c);
         if ((lane & 15) == 0 && n < a.N) {

@@ -224,8 +224,7 @@ __device__ __forceinline__ float block_max_arg(float m, int& arg, float* sred, i
 
 template <int NT>
 __device__ __forceinline__ float block_sum2(float s, float* sred) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  s = wave_sum(s);
   const int w = threadIdx.x >> 6;
   __syncthreads();  // sred reuse after block_max_arg
   if ((threadIdx.x & 63) == 0) sred[w] = s;
