@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--grad-comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce dtype (fp32 = torch DDP semantics)")
+    ap.add_argument("--p2p-kb", type=float, default=0.0,
+                    help="buckets <= this many KiB use the one-shot hipIpc all-reduce (0 = all on RCCL)")
     ap.add_argument("--no-ckpt", action="store_true")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-scope", default="full", choices=["full", "model"],
@@ -103,7 +105,7 @@ def main():
     # the last bucket's all-reduce (GPT-2: the tied token table, whose gradient completes at the
     # end of backward) overlaps the fused optimizer's update of every other parameter
     net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, defer_tail_to_optimizer=True,
-                                  grad_comm_dtype=args.grad_comm_dtype) if world > 1 else model
+                                  grad_comm_dtype=args.grad_comm_dtype, p2p_max_kb=args.p2p_kb) if world > 1 else model
     B, T = wl["batch"], wl["seq_len"]
     fwd_loss = wl["loss"]
 

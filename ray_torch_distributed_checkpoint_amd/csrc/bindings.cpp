@@ -580,7 +580,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("num_buckets", &rtdc_ddp::GradBucketEngine::num_buckets)
       .def("launched", &rtdc_ddp::GradBucketEngine::launched)
       .def("steps", &rtdc_ddp::GradBucketEngine::steps)
-      .def("bucket_bytes", &rtdc_ddp::GradBucketEngine::bucket_bytes);
+      .def("bucket_bytes", &rtdc_ddp::GradBucketEngine::bucket_bytes)
+      .def("set_p2p", &rtdc_ddp::GradBucketEngine::set_p2p, py::arg("comm"), py::arg("max_bytes"))
+      .def("p2p_buckets", &rtdc_ddp::GradBucketEngine::p2p_buckets);
+  py::class_<rtdc_p2p::P2PComm, std::shared_ptr<rtdc_p2p::P2PComm>>(m, "P2PComm")
+      .def(py::init<int, int, long long, int, double, int>(), py::arg("rank"), py::arg("world"),
+           py::arg("capacity_bytes"), py::arg("device"), py::arg("timeout_s") = 30.0, py::arg("blocks") = 32)
+      .def("handle", &rtdc_p2p::P2PComm::handle)
+      .def("open", &rtdc_p2p::P2PComm::open)
+      .def("allreduce_", &rtdc_p2p::P2PComm::allreduce_, py::arg("tensor"), py::arg("average") = true)
+      .def("error", &rtdc_p2p::P2PComm::error)
+      .def("capacity", &rtdc_p2p::P2PComm::capacity)
+      .def("epoch", &rtdc_p2p::P2PComm::epoch)
+      .def_property_readonly("world", &rtdc_p2p::P2PComm::world)
+      .def_property_readonly("rank", &rtdc_p2p::P2PComm::rank);
 
   m.doc() = "MI355X (gfx950) kernels and native checkpoint engine";
   m.def("gemm_bf16", &gemm_bf16);

@@ -27,6 +27,10 @@
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
 
+#include <memory>
+
+#include "p2p_comm.cpp"
+
 extern "C" {
 int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st);
 int rtdc_bf16_to_f32(const void* x, float* y, long long n, float scale, hipStream_t st);
@@ -86,6 +90,10 @@ class GradBucketEngine {
   ~GradBucketEngine() {
     for (auto e : events_)
       if (e) hipEventDestroy(e);
+    for (auto e : p2p_ready_)
+      if (e) hipEventDestroy(e);
+    for (auto e : p2p_done_)
+      if (e) hipEventDestroy(e);
   }
 
   void finalize(bool defer_last = false) {
@@ -96,12 +104,19 @@ class GradBucketEngine {
     for (size_t i = 0; i < marked_.size(); ++i)
       if (!marked_[i]) flat_.slice(0, seg_[i].first, seg_[i].first + seg_[i].second).zero_();
     while (next_ < works_.size()) launch(next_++);
-    const bool defer = defer_last && works_.size() > 1;
+    const bool defer = defer_last && works_.size() > 1 && !is_p2p(works_.size() - 1);
     const size_t nwait = works_.size() - (defer ? 1 : 0);
+    if (p2p_) {
+      hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+      for (size_t b = 0; b < nwait; ++b)
+        if (is_p2p(b)) TORCH_CHECK(hipStreamWaitEvent(cur, p2p_done_[b], 0) == hipSuccess, "hipStreamWaitEvent");
+    }
     if (side_) {
       // the widened fp32 slices are final once the side stream passed each bucket's event
       hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
-      if (nwait > 0) TORCH_CHECK(hipStreamWaitEvent(cur, events_[nwait - 1], 0) == hipSuccess, "hipStreamWaitEvent");
+      size_t last = nwait;
+      while (last > 0 && is_p2p(last - 1)) --last;  // the side stream handled buckets < last
+      if (last > 0) TORCH_CHECK(hipStreamWaitEvent(cur, events_[last - 1], 0) == hipSuccess, "hipStreamWaitEvent");
     } else {
       {
         pybind11::gil_scoped_release nogil;
@@ -140,6 +155,33 @@ class GradBucketEngine {
     tail_.reset();
     works_[last].reset();
   }
+  // Route buckets of at most max_bytes (communicated bytes) through the one-shot hipIpc
+  // all-reduce (runtime/p2p_comm.cpp) on a dedicated stream instead of RCCL; the rest stay on
+  // the process group.  Collective order is unchanged (bucket order), so every rank routes the
+  // same buckets.
+  void set_p2p(std::shared_ptr<rtdc_p2p::P2PComm> comm, int64_t max_bytes) {
+    TORCH_CHECK(flat_.is_cuda(), "p2p all-reduce needs a device gradient buffer");
+    p2p_ = std::move(comm);
+    p2p_max_bytes_ = max_bytes;
+    const size_t nb = works_.size();
+    if (!p2p_stream_)
+      p2p_stream_.emplace(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true, flat_.device().index()));
+    if (p2p_ready_.empty()) {
+      p2p_ready_.resize(nb, nullptr);
+      p2p_done_.resize(nb, nullptr);
+      for (size_t b = 0; b < nb; ++b) {
+        TORCH_CHECK(hipEventCreateWithFlags(&p2p_ready_[b], hipEventDisableTiming) == hipSuccess, "hipEventCreate");
+        TORCH_CHECK(hipEventCreateWithFlags(&p2p_done_[b], hipEventDisableTiming) == hipSuccess, "hipEventCreate");
+      }
+    }
+    via_p2p_.assign(nb, false);
+    for (size_t b = 0; b < nb; ++b) {
+      const int64_t bytes = (bounds_[b + 1] - bounds_[b]) * (lp_.defined() ? 2 : 4);
+      via_p2p_[b] = p2p_ && bytes <= p2p_max_bytes_ && bytes <= p2p_->capacity() && bytes % 16 == 0;
+    }
+  }
+  std::vector<bool> p2p_buckets() const { return via_p2p_; }
+
   int64_t comm_bytes_per_step() const {
     return (bounds_.back() - bounds_.front()) * (lp_.defined() ? 2 : 4);
   }
@@ -161,10 +203,31 @@ class GradBucketEngine {
     while (next_ < works_.size() && pending_[next_] <= 0) launch(next_++);
   }
 
+  bool is_p2p(size_t b) const { return p2p_ && b < via_p2p_.size() && via_p2p_[b]; }
+
   void launch(size_t b) {
     const int64_t lo = bounds_[b], hi = bounds_[b + 1];
     at::Tensor src = flat_.slice(0, lo, hi);
     std::vector<at::Tensor> t{src};
+    if (is_p2p(b)) {
+      hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+      at::Tensor buf = src;
+      if (lp_.defined()) {
+        buf = lp_.slice(0, lo, hi);
+        TORCH_CHECK(rtdc_f32_to_bf16(src.data_ptr<float>(), buf.data_ptr(), hi - lo, cur) == 0, "f32->bf16");
+      }
+      TORCH_CHECK(hipEventRecord(p2p_ready_[b], cur) == hipSuccess, "hipEventRecord");
+      TORCH_CHECK(hipStreamWaitEvent(p2p_stream_->stream(), p2p_ready_[b], 0) == hipSuccess, "hipStreamWaitEvent");
+      {
+        c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*p2p_stream_);
+        // SUM when the process group has no AVG (gloo): the engine's post-scale then covers it
+        p2p_->allreduce_(buf, use_avg_);
+        if (lp_.defined()) widen(b);
+        TORCH_CHECK(hipEventRecord(p2p_done_[b], p2p_stream_->stream()) == hipSuccess, "hipEventRecord");
+      }
+      launched_[b] = true;
+      return;
+    }
     if (lp_.defined()) {
       at::Tensor dst = lp_.slice(0, lo, hi);
       if (flat_.is_cuda()) {
@@ -216,6 +279,11 @@ class GradBucketEngine {
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
   c10::intrusive_ptr<c10d::Work> tail_;
   std::vector<bool> launched_, marked_;
+  std::shared_ptr<rtdc_p2p::P2PComm> p2p_;
+  int64_t p2p_max_bytes_ = 0;
+  std::vector<bool> via_p2p_;
+  c10::optional<c10::hip::HIPStreamMasqueradingAsCUDA> p2p_stream_;
+  std::vector<hipEvent_t> p2p_ready_, p2p_done_;
   size_t next_ = 0;
   int64_t steps_ = 0;
 };

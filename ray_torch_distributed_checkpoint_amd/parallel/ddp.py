@@ -57,7 +57,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 2.0, broadcast_buffers: bool = True, device_ids=None,
                  output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 defer_tail_to_optimizer: bool = False, grad_comm_dtype: str = "fp32"):
+                 defer_tail_to_optimizer: bool = False, grad_comm_dtype: str = "fp32", p2p_max_kb: float = 0.0):
         super().__init__()
         if grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
@@ -135,11 +135,14 @@ class DistributedDataParallel(nn.Module):
         self._check = os.environ.get("RTDC_COLLECTIVE_CHECK", "0") == "1"
         self._steps = 0
         self._comm = None
+        self.p2p = None
+        self.p2p_max_bytes = 0
         if self.world_size > 1 and grad_comm_dtype == "bf16":
             self._comm = torch.empty(self.space.numel, dtype=torch.bfloat16, device=dev)
         if self.world_size > 1:
             self._verify_plan_across_ranks()
             self._engine = self._native_engine(process_group)
+            self._attach_p2p(process_group, p2p_max_kb)
             for p in self.space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
 
@@ -179,6 +182,26 @@ class DistributedDataParallel(nn.Module):
         return mod.GradBucketEngine(self.space.grad, bounds, param_bucket, segs, pg, self._use_avg,
                                     1.0 / self.world_size, self._comm)
 
+    def _attach_p2p(self, process_group, max_kb: float) -> None:
+        """Buckets of at most max_kb KiB (communicated bytes) go through the one-shot hipIpc
+        all-reduce (parallel/p2p.py) instead of RCCL: latency-bound small buckets (the toy MLP's
+        1-2 MB, every model's small first bucket) take one xGMI hop to all peers at once.
+        Opt-in (0 = off); needs the native engine, device gradients and <= 8 ranks."""
+        self.p2p = None
+        self.p2p_max_bytes = 0
+        if max_kb <= 0 or self._engine is None or self.space.device.type != "cuda" or self.world_size > 8:
+            return
+        from .p2p import P2PAllReduce
+
+        esz = 2 if self.grad_comm_dtype == "bf16" else 4
+        small = [(b.end - b.start) * esz for b in self.buckets if (b.end - b.start) * esz <= max_kb * 1024]
+        if not small:
+            return
+        cap_mb = max(small) / (1 << 20) + 0.01
+        self.p2p = P2PAllReduce(process_group, capacity_mb=cap_mb, device=self.space.device)
+        self.p2p_max_bytes = int(max_kb * 1024)
+        self._engine.set_p2p(self.p2p.comm, self.p2p_max_bytes)
+
     def comm_plan(self) -> dict:
         """Self-description of the gradient all-reduce (what a multi-GPU bench reports)."""
         sizes = self.bucket_sizes_bytes()
@@ -187,7 +210,9 @@ class DistributedDataParallel(nn.Module):
                 "bucket_mb": [round(b / (1 << 20), 2) for b in sizes],
                 "allreduce_bytes_per_step": int(sum(sizes)),
                 "engine": "native" if self._engine is not None else "python",
-                "defer_tail_to_optimizer": self.defer_tail}
+                "defer_tail_to_optimizer": self.defer_tail,
+                "p2p_buckets": ([i for i, v in enumerate(self._engine.p2p_buckets()) if v]
+                                if getattr(self, "p2p", None) is not None else [])}
 
     # ------------------------------------------------------------------ buffers
     def _sync_buffers(self):

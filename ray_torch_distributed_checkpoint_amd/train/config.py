@@ -105,11 +105,17 @@ class TorchConfig:
     # framework's fused optimizers (they wait for it before its slice) - stock torch optimizers
     # would read that slice un-reduced, so it is off unless the training loop opts in
     defer_tail_to_optimizer: bool = False
+    # buckets of at most this many KiB use the one-shot hipIpc all-reduce (parallel/p2p.py)
+    # instead of RCCL; 0 = off (opt-in: it needs every rank's GPU on one node)
+    p2p_max_kb: float = 0.0
 
     def __post_init__(self):
         if self.grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
+        if self.p2p_max_kb < 0:
+            raise ValueError("p2p_max_kb must be >= 0")
 
     def ddp_kwargs(self) -> dict:
         return dict(bucket_cap_mb=self.bucket_cap_mb, first_bucket_mb=self.first_bucket_mb,
-                    grad_comm_dtype=self.grad_comm_dtype, defer_tail_to_optimizer=self.defer_tail_to_optimizer)
+                    grad_comm_dtype=self.grad_comm_dtype, defer_tail_to_optimizer=self.defer_tail_to_optimizer,
+                    p2p_max_kb=self.p2p_max_kb)

@@ -1,0 +1,148 @@
+"""One-shot hipIpc all-reduce (parallel/p2p.py, csrc/kernels/p2p_allreduce.hip).
+
+On a 1-GPU box two ranks share cuda:0 (two processes, gloo for the handle exchange): the IPC
+mapping, the epoch-flag protocol, the rank-ordered sum and the double-buffered staging all run;
+only the xGMI hop is not exercised.  With >= 2 GPUs the same test maps real peers.
+* raw communicator: fp32 and bf16 sums/means over many epochs equal the host reference, bitwise
+  identical on every rank;
+* DDP: buckets routed through P2P give bitwise the same gradients as the gloo path.
+"""
+import os
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dev
+
+
+def _raw_worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+
+        dev = _init(rank, world, port)
+        from ray_torch_distributed_checkpoint_amd.parallel.p2p import P2PAllReduce
+
+        comm = P2PAllReduce(capacity_mb=1.0, device=dev, timeout_s=20.0, blocks=8)
+        outs = []
+        for it in range(7):  # odd count: both staging parities, reused
+            for dtype, n in ((torch.float32, 4096 * 8 + 4 * it), (torch.bfloat16, 8192 + 8 * it)):
+                g = torch.Generator().manual_seed(100 * it + rank)
+                x = torch.randn(n, generator=g).to(dtype).to(dev)
+                comm.all_reduce_(x, average=(it % 2 == 0))
+                outs.append(x.float().cpu().numpy())
+        torch.cuda.synchronize()
+        q.put((rank, "ok", (outs, comm.error())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _ddp_worker(rank, world, port, p2p_kb, comm_dtype, q):
+    try:
+        import torch.distributed as dist
+
+        dev = _init(rank, world, port)
+        from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+        from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config.named("gpt2-tiny")).to(dev)
+        net = DistributedDataParallel(model, bucket_cap_mb=0.25, first_bucket_mb=0.05, p2p_max_kb=p2p_kb,
+                                      grad_comm_dtype=comm_dtype)
+        g = torch.Generator().manual_seed(7)
+        data = torch.randint(0, 1000, (2 * world, 65), generator=g).to(dev)[2 * rank:2 * rank + 2]
+        for _ in range(3):
+            net.space.zero_grad(set_to_none=True)
+            net(data[:, :-1], data[:, 1:]).backward()
+        torch.cuda.synchronize()
+        grads = {n: p.grad.detach().float().cpu().numpy() for n, p in model.named_parameters()}
+        q.put((rank, "ok", (grads, net.comm_plan())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _spawn(target, world, *args):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, st, v = q.get(timeout=180)
+            if st != "ok" and "hipIpc" in v:
+                pytest.skip(f"hipIpc peer mapping unavailable here: {v.splitlines()[-1]}")
+            assert st == "ok", v
+            out[r] = v
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+def _world():
+    return max(2, min(torch.cuda.device_count(), 4))
+
+
+def test_p2p_allreduce_matches_reference_on_every_rank():
+    world = _world()
+    out = _spawn(_raw_worker, world)
+    k = 0
+    for it in range(7):
+        for dtype, n in ((torch.float32, 4096 * 8 + 4 * it), (torch.bfloat16, 8192 + 8 * it)):
+            xs = [torch.randn(n, generator=torch.Generator().manual_seed(100 * it + r)).to(dtype).float()
+                  for r in range(world)]
+            ref = sum(xs[1:], xs[0])
+            if it % 2 == 0:
+                ref = ref / world
+            got0 = out[0][0][k]
+            for r in range(world):
+                assert out[r][1] == 0, "a wait timed out"
+                assert np.array_equal(out[r][0][k], got0), f"rank {r} differs (call {k})"
+            tol = 1e-6 if dtype == torch.float32 else 1e-2
+            np.testing.assert_allclose(got0, ref.to(dtype).float().numpy(), rtol=tol, atol=tol)
+            k += 1
+
+
+@pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
+def test_ddp_buckets_over_p2p_equal_the_process_group_path(comm_dtype):
+    world = 2
+    base = _spawn(_ddp_worker, world, 0.0, comm_dtype)
+    p2p = _spawn(_ddp_worker, world, 64.0, comm_dtype)
+    assert p2p[0][1]["p2p_buckets"], "no bucket was routed through P2P"
+    assert not base[0][1]["p2p_buckets"]
+    for n, v in base[0][0].items():
+        for r in range(world):
+            assert np.array_equal(p2p[r][0][n], v), f"{n} differs on rank {r}"
