@@ -86,6 +86,58 @@ __global__ __launch_bounds__(256) void im2col_small_kernel(const bf16_t* __restr
   }
 }
 
+// Stem im2col (C = 3, 7x7, stride 2) through LDS: one block per output row (b, ho).  The 7
+// input rows it needs are staged with aligned 16-B loads into zero-padded LDS rows (16 leading
+// + 16 trailing elements cover pad = 3 pixels), then every 16-B column chunk is assembled from
+// LDS with 2-B reads: for a tap row kh the 21 (kw, c) values of a pixel are contiguous, at
+// kh*ROW + 16 + (2*wo - 3)*3 + (k - 21*kh).  Global traffic: the input once per block (from
+// L2) and the column matrix once, all 16-B - the old per-element gathers were load-bound.
+template <int W, int Kp>
+__global__ __launch_bounds__(256) void im2col_stem_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ cols,
+                                                         int H, int Ho, int Wo) {
+  constexpr int C = 3, KH = 7, KW = 7, S = 2, PAD = 3, K = KH * KW * C;
+  constexpr int ROW = 16 + W * C + 16;  // elements per staged row
+  constexpr int NCH = W * C / 8;        // 16-B chunks per input row
+  static_assert((W * C) % 8 == 0, "row must be whole 16-B chunks");
+  __shared__ __attribute__((aligned(16))) bf16_t rows[KH * ROW];
+  const int bo = blockIdx.x;  // b * Ho + ho
+  const int b = bo / Ho, ho = bo - b * Ho;
+  const int h0 = ho * S - PAD;
+  for (int i = threadIdx.x; i < KH * (ROW / 8); i += 256) {
+    const int kh = i / (ROW / 8), c8 = i - kh * (ROW / 8);  // 16-B chunk c8 of staged row kh
+    const int h = h0 + kh;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    const int src = c8 - 2;  // the data starts 16 elements (2 chunks) into the row
+    if (src >= 0 && src < NCH && (unsigned)h < (unsigned)H)
+      v = *(const uint4*)(x + (((size_t)b * H + h) * W) * C + src * 8);
+    *(uint4*)(rows + kh * ROW + c8 * 8) = v;
+  }
+  __syncthreads();
+  constexpr int PER = Kp / 8;
+  bf16_t* out = cols + (size_t)bo * Wo * Kp;
+  for (int i = threadIdx.x; i < Wo * PER; i += 256) {
+    const int wo = i / PER, k0 = (i - wo * PER) * 8;
+    const int base = 16 + (wo * S - PAD) * C;
+    uint32_t u[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      uint32_t pair = 0;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int k = k0 + 2 * e2 + h2;
+        uint32_t v = 0;
+        if (k < K) {
+          const int kh = k / (KW * C);
+          v = rows[kh * ROW + base + (k - kh * KW * C)];
+        }
+        pair |= v << (16 * h2);
+      }
+      u[e2] = pair;
+    }
+    *(uint4*)(out + (size_t)wo * Kp + k0) = make_uint4(u[0], u[1], u[2], u[3]);
+  }
+}
+
 __device__ __forceinline__ void acc8(float* acc, uint4 v) {
   uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -543,6 +595,52 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// 3x3 / stride 2 / pad 1 (the ResNet stem pool) backward, gather form with the window algebra
+// resolved at compile time: input row h is covered by output row h/2 (tap 1) when h is even,
+// by rows (h+1)/2 (tap 0) and (h-1)/2 (tap 2) when odd - same for columns - so a thread visits
+// its 1, 2 or 4 windows directly instead of testing 9 taps with runtime divisions.
+template <int C>
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                            const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
+                                                            int B, int H, int W, int Ho, int Wo) {
+  constexpr int CG = C / 8;
+  const int total = B * H * W * CG;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / CG, c = (i - pix * CG) * 8;
+    const int q = pix / W, w = pix - q * W;
+    const int b = q / H, h = q - b * H;
+    int hos[2], khs[2], nh = 0, wos[2], kws[2], nw = 0;
+    if (h & 1) {
+      if ((h + 1) / 2 < Ho) { hos[nh] = (h + 1) / 2; khs[nh++] = 0; }
+      hos[nh] = (h - 1) / 2; khs[nh++] = 2;
+    } else {
+      if (h / 2 < Ho) { hos[nh] = h / 2; khs[nh++] = 1; }
+    }
+    if (w & 1) {
+      if ((w + 1) / 2 < Wo) { wos[nw] = (w + 1) / 2; kws[nw++] = 0; }
+      wos[nw] = (w - 1) / 2; kws[nw++] = 2;
+    } else {
+      if (w / 2 < Wo) { wos[nw] = w / 2; kws[nw++] = 1; }
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < nh; ++a)
+      for (int bb = 0; bb < nw; ++bb) {
+        const size_t o = ((size_t)(b * Ho + hos[a]) * Wo + wos[bb]) * C + c;
+        const uint2 a8 = *(const uint2*)(arg + o);
+        const uint4 g4 = *(const uint4*)(dy + o);
+        const uint32_t tap = khs[a] * 3 + kws[bb];
+        const uint32_t gw[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ae = ((e < 4 ? a8.x : a8.y) >> (8 * (e & 3))) & 0xffu;
+          const float g = __uint_as_float((e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] << 16));
+          if (ae == tap) acc[e] += g;
+        }
+      }
+    *(uint4*)(dx + (size_t)pix * C + c) = pack8(acc);
+  }
+}
+
 // global average pool [B][HW][C] -> [B][C] (fp32 accumulate, bf16 out)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
                                                          int HW, int C) {
@@ -581,6 +679,11 @@ extern "C" int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C
   const int vec = (C % 8 == 0 && Kp % 8 == 0) ? 1 : 0;
   const long long work = (long long)B * Ho * Wo * (vec ? Kp / 8 : Kp);
   if (work >= (1LL << 31) || (long long)B * H * W * C >= (1LL << 31)) return 1;
+  if (C == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && W == 224 && Kp == 192 && Wo == 112) {
+    hipLaunchKernelGGL((im2col_stem_kernel<224, 192>), dim3(B * Ho), dim3(256), 0, st, (const bf16_t*)x,
+                       (bf16_t*)cols, H, Ho, Wo);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   if (C == 3 && KW == 7 && Kp % 8 == 0) {
     hipLaunchKernelGGL((im2col_small_kernel<3, 7>), dim3(gsz((long long)B * Ho * Wo * (Kp / 8))), dim3(256), 0, st,
                        (const bf16_t*)x, (bf16_t*)cols, g);
@@ -671,6 +774,9 @@ extern "C" int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, v
   if (!backward)
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(gsz((long long)B * Ho * Wo * C / 8)), dim3(256), 0, st, (const bf16_t*)x,
                        (bf16_t*)y, (uint8_t*)arg, B, H, W, C, Ho, Wo, K, s, p);
+  else if (K == 3 && s == 2 && p == 1 && C == 64 && Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1)
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<64>, dim3(gsz((long long)B * H * W * C / 8)), dim3(256), 0, st,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, B, H, W, Ho, Wo);
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(gsz((long long)B * H * W * C / 8)), dim3(256), 0, st, (const bf16_t*)dy,
                        (const uint8_t*)arg, (bf16_t*)dx, B, H, W, C, Ho, Wo, K, s, p);

@@ -27,6 +27,7 @@ def _nhwc(x):
         (2, 16, 64, 128, 3, 2, 1),  # strided stage entry
         (2, 16, 64, 128, 1, 2, 0),  # projection shortcut
         (2, 32, 3, 64, 7, 2, 3),  # stem (C=3: scalar im2col, K padded 147 -> 192)
+        (2, 224, 3, 64, 7, 2, 3),  # ImageNet stem: LDS-staged im2col (224 wide)
         (4, 8, 128, 64, 1, 1, 0),  # 1x1/s1: direct (no im2col)
         (1, 7, 64, 64, 3, 1, 1),  # M = 49: rows padded to 64
         (2, 14, 128, 256, 3, 1, 1),  # implicit GEMM, 128x128 tiles
@@ -119,16 +120,17 @@ def test_pools_and_classifier():
     from ray_torch_distributed_checkpoint_amd.ops import cnn
 
     torch.manual_seed(5)
-    x = torch.randn(4, 64, 28, 28, device=DEV).to(torch.bfloat16)
-    xr = x.float().requires_grad_(True)
-    ref = F.max_pool2d(xr, 3, 2, 1)
-    gy = torch.randn_like(ref)
-    ref.backward(gy)
-    xi = _nhwc(x).requires_grad_(True)
-    y = cnn.max_pool2d(xi, 3, 2, 1)
-    _close(y, _nhwc(ref), 1e-6, "maxpool")
-    y.backward(_nhwc(gy).to(torch.bfloat16))
-    _close(xi.grad, _nhwc(xr.grad), 0.01, "maxpool dx")
+    for hw in (28, 27):  # even / odd size (the odd one has a partial last window)
+        x = torch.randn(4, 64, hw, hw, device=DEV).to(torch.bfloat16)
+        xr = x.float().requires_grad_(True)
+        ref = F.max_pool2d(xr, 3, 2, 1)
+        gy = torch.randn_like(ref)
+        ref.backward(gy)
+        xi = _nhwc(x).requires_grad_(True)
+        y = cnn.max_pool2d(xi, 3, 2, 1)
+        _close(y, _nhwc(ref), 1e-6, "maxpool")
+        y.backward(_nhwc(gy).to(torch.bfloat16))
+        _close(xi.grad, _nhwc(xr.grad), 0.01, "maxpool dx")
 
     xa = torch.randn(6, 7, 7, 512, device=DEV).to(torch.bfloat16)
     xar = xa.float().requires_grad_(True)
