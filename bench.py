@@ -109,9 +109,11 @@ def main():
     B, T = wl["batch"], wl["seq_len"]
     fwd_loss = wl["loss"]
 
+    seed = torch.ones((), dtype=torch.float32, device=dev)  # d(loss)/d(loss): no fill kernel per step
+
     def step(i):
         loss = fwd_loss(net, i)
-        loss.backward()
+        loss.backward(seed)
         opt.step()
         opt.zero_grad()
         return loss

@@ -63,6 +63,11 @@ int rtdc_swiglu_fwd(const void* gu, void* h, long long M, int F, hipStream_t st)
 int rtdc_swiglu_bwd(const void* gu, const void* dh, void* dgu, long long M, int F, hipStream_t st);
 int rtdc_im2col(const void* x, void* cols, int B, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
                 int pad, int K, int Kp, hipStream_t st);
+int rtdc_xent_finalize(const float* loss, const int64_t* target, int M, float fixed_n, int ignore, float* out,
+                       hipStream_t st);
+int rtdc_xent_alpha(const float* g, const float* den, float* out, hipStream_t st);
+int rtdc_scale_dev(const void* x, void* y, long long n, int is_bf16, const float* g, const float* den, hipStream_t st);
+int rtdc_nchw_to_nhwc_bf16(const float* x, void* y, int B, int C, long long HW, hipStream_t st);
 int rtdc_col2im(const void* dcols, void* dx, const void* addend, int B, int H, int W, int C, int Ho, int Wo, int KH,
                 int KW, int stride, int pad, int K, int Kp, hipStream_t st);
 int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma, const float* beta,
@@ -473,6 +478,61 @@ static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tens
                        dbeta.data_ptr<float>(), N, (int)C, relu, ws.data_ptr<float>(), (int)nblk, cur_stream()),
            "bn_bwd");
 }
+// mean cross-entropy from per-row losses: out[0] = loss, out[1] = divisor (device count of
+// non-ignored targets, or fixed_n when target is None)
+static void xent_finalize(Tensor loss, c10::optional<Tensor> target, double fixed_n, Tensor out) {
+  check_dev(loss, "loss");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.is_contiguous() && out.scalar_type() == at::kFloat &&
+                  out.numel() >= 2 && out.is_contiguous(),
+              "xent_finalize: fp32 loss rows / fp32 out[2]");
+  const int64_t* t = nullptr;
+  if (target.has_value()) {
+    TORCH_CHECK(target->scalar_type() == at::kLong && target->is_contiguous() && target->numel() == loss.numel(),
+                "xent_finalize: int64 target per row");
+    t = target->data_ptr<int64_t>();
+  }
+  check_rc(rtdc_xent_finalize(loss.data_ptr<float>(), t, (int)loss.numel(), (float)fixed_n, -100,
+                              out.data_ptr<float>(), cur_stream()),
+           "xent_finalize");
+}
+static void xent_alpha(Tensor g, Tensor den, Tensor out) {
+  TORCH_CHECK(g.scalar_type() == at::kFloat && den.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat,
+              "xent_alpha: fp32 scalars");
+  check_rc(rtdc_xent_alpha(g.data_ptr<float>(), den.data_ptr<float>(), out.data_ptr<float>(), cur_stream()),
+           "xent_alpha");
+}
+static void scale_dev(Tensor x, Tensor y, Tensor g, Tensor den) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() && x.scalar_type() == y.scalar_type() &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "scale_dev: matching contiguous bf16/fp32 tensors");
+  TORCH_CHECK(g.scalar_type() == at::kFloat && den.scalar_type() == at::kFloat, "scale_dev: fp32 scalars");
+  check_rc(rtdc_scale_dev(x.data_ptr(), y.data_ptr(), x.numel(), x.scalar_type() == at::kBFloat16 ? 1 : 0,
+                          g.data_ptr<float>(), den.data_ptr<float>(), cur_stream()),
+           "scale_dev");
+}
+static void nchw_to_nhwc_bf16(Tensor x, Tensor y) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4, "nchw_to_nhwc_bf16: contiguous NCHW fp32");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.numel() == x.numel(), "nchw_to_nhwc_bf16: bf16 out");
+  check_rc(rtdc_nchw_to_nhwc_bf16(x.data_ptr<float>(), y.data_ptr(), (int)x.size(0), (int)x.size(1),
+                                  x.size(2) * x.size(3), cur_stream()),
+           "nchw_to_nhwc_bf16");
+}
+// rows x row_bytes from src (pitch src_pitch bytes) to dst (pitch dst_pitch) on the current
+// stream: a DMA-engine copy for padded-operand staging (no ATen kernel)
+static void copy2d(Tensor dst, Tensor src, int64_t rows, int64_t row_bytes, int64_t dst_pitch, int64_t src_pitch) {
+  TORCH_CHECK(dst.is_cuda() && src.is_cuda(), "copy2d: device tensors");
+  TORCH_CHECK(row_bytes <= dst_pitch && row_bytes <= src_pitch && rows >= 0, "copy2d: bad geometry");
+  TORCH_CHECK((rows - 1) * dst_pitch + row_bytes <= (int64_t)(dst.numel() * dst.element_size()) &&
+                  (rows - 1) * src_pitch + row_bytes <= (int64_t)(src.numel() * src.element_size()),
+              "copy2d: out of bounds");
+  if (rows == 0) return;
+  TORCH_CHECK(hipMemcpy2DAsync(dst.data_ptr(), (size_t)dst_pitch, src.data_ptr(), (size_t)src_pitch, (size_t)row_bytes,
+                               (size_t)rows, hipMemcpyDeviceToDevice, cur_stream()) == hipSuccess,
+              "hipMemcpy2DAsync");
+}
+
 static void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t K, int64_t s, int64_t p) {
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && arg.scalar_type() == torch::kUInt8, "maxpool_fwd: bad args");
   check_rc(rtdc_maxpool(x.data_ptr(), y.data_ptr(), arg.data_ptr(), nullptr, nullptr, (int)x.size(0), (int)x.size(1),
@@ -627,6 +687,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("conv_w_flip_t", &conv_w_flip_t);
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("xent_finalize", &xent_finalize);
+  m.def("xent_alpha", &xent_alpha);
+  m.def("scale_dev", &scale_dev);
+  m.def("nchw_to_nhwc_bf16", &nchw_to_nhwc_bf16);
+  m.def("copy2d", &copy2d);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool", &avgpool);
 

@@ -641,6 +641,35 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
   }
 }
 
+// Network input NCHW fp32 -> NHWC bf16 in one pass (the permute + cast + contiguous of ATen
+// are three): a thread takes 8 consecutive pixels of one image - 2 x 16-B loads per channel,
+// C x 16-B stores of the interleaved row (HW % 8 == 0).
+template <int C>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                               int B, long long HW) {
+  const long long per = HW / 8, groups = (long long)B * per;
+  for (long long gi = blockIdx.x * 256LL + threadIdx.x; gi < groups; gi += (long long)gridDim.x * 256) {
+    const long long b = gi / per, p0 = (gi - b * per) * 8;
+    float v[C][8];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float4* src = (const float4*)(x + (b * C + c) * HW + p0);
+      const float4 a = src[0], d = src[1];
+      v[c][0] = a.x; v[c][1] = a.y; v[c][2] = a.z; v[c][3] = a.w;
+      v[c][4] = d.x; v[c][5] = d.y; v[c][6] = d.z; v[c][7] = d.w;
+    }
+    uint32_t o[4 * C];
+#pragma unroll
+    for (int j = 0; j < 4 * C; ++j) {
+      const int e0 = 2 * j, e1 = 2 * j + 1;  // interleaved index p * C + c
+      o[j] = pack_bf2(v[e0 % C][e0 / C], v[e1 % C][e1 / C]);
+    }
+    uint4* dst = (uint4*)(y + (b * HW + p0) * C);
+#pragma unroll
+    for (int q = 0; q < C; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
+}
+
 // global average pool [B][HW][C] -> [B][C] (fp32 accumulate, bf16 out)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
                                                          int HW, int C) {
@@ -791,5 +820,12 @@ extern "C" int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int ba
   else
     hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(gsz((long long)B * HW * C)), dim3(256), 0, st, (const bf16_t*)x,
                        (bf16_t*)y, B, HW, C);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_nchw_to_nhwc_bf16(const float* x, void* y, int B, int C, long long HW, hipStream_t st) {
+  if (HW % 8 != 0 || C != 3) return 1;
+  const long long groups = (long long)B * HW / 8;
+  hipLaunchKernelGGL(nchw_to_nhwc_bf16_kernel<3>, dim3(gsz(groups)), dim3(256), 0, st, x, (bf16_t*)y, B, HW);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

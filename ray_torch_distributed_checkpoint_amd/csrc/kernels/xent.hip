@@ -396,3 +396,83 @@ extern "C" int rtdc_xent(const void* logits, void* dlogits, const int64_t* targe
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// ---- loss finalisation without ATen reductions: one block sums the per-row losses and counts
+// the non-ignored targets in a fixed order; out[0] = mean loss, out[1] = divisor (count clamped
+// to >= 1, or the caller's fixed divisor when target is null).
+namespace rtdc {
+__global__ __launch_bounds__(1024) void xent_finalize_kernel(const float* __restrict__ loss,
+                                                            const int64_t* __restrict__ target, int M, float fixed_n,
+                                                            int ignore, float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < M; i += 1024) {
+    s += loss[i];
+    if (target) c += target[i] != ignore ? 1.f : 0.f;
+  }
+  s = block_sum<1024>(s, red);
+  c = block_sum<1024>(c, red);
+  if (threadIdx.x == 0) {
+    const float n = target ? fmaxf(c, 1.f) : fixed_n;
+    out[0] = s / n;
+    out[1] = n;
+  }
+}
+
+// out[0] = g[0] / den[0]: the upstream loss gradient over the divisor, as a device alpha
+__global__ void xent_alpha_kernel(const float* __restrict__ g, const float* __restrict__ den, float* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = g[0] / den[0];
+}
+
+// y = x * (g[0] / den[0]) (bf16 or fp32 x, 8 elements per thread)
+template <typename T>
+__global__ __launch_bounds__(256) void scale_dev_kernel(const T* __restrict__ x, T* __restrict__ y, long long n,
+                                                       const float* __restrict__ g, const float* __restrict__ den) {
+  const float a = g[0] / den[0];
+  const long long n8 = n / 8;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    if constexpr (sizeof(T) == 2) {
+      const uint4 q = ((const uint4*)x)[i];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = pack_bf2(__uint_as_float(w[e] << 16) * a, __uint_as_float(w[e] & 0xffff0000u) * a);
+      ((uint4*)y)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+      const float4 p = ((const float4*)x)[2 * i], q = ((const float4*)x)[2 * i + 1];
+      ((float4*)y)[2 * i] = make_float4(p.x * a, p.y * a, p.z * a, p.w * a);
+      ((float4*)y)[2 * i + 1] = make_float4(q.x * a, q.y * a, q.z * a, q.w * a);
+    }
+  }
+  // tail (n % 8)
+  for (long long i = n8 * 8 + blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    if constexpr (sizeof(T) == 2) y[i] = f2bf(bf2f(x[i]) * a);
+    else y[i] = x[i] * a;
+  }
+}
+}  // namespace rtdc
+
+extern "C" int rtdc_xent_finalize(const float* loss, const int64_t* target, int M, float fixed_n, int ignore, float* out,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(rtdc::xent_finalize_kernel, dim3(1), dim3(1024), 0, st, loss, target, M, fixed_n, ignore, out);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_xent_alpha(const float* g, const float* den, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(rtdc::xent_alpha_kernel, dim3(1), dim3(64), 0, st, g, den, out);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_scale_dev(const void* x, void* y, long long n, int is_bf16, const float* g, const float* den,
+                              hipStream_t st) {
+  long long blocks = (n / 8 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  if (is_bf16)
+    hipLaunchKernelGGL(rtdc::scale_dev_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)x,
+                       (bf16_t*)y, n, g, den);
+  else
+    hipLaunchKernelGGL(rtdc::scale_dev_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)x,
+                       (float*)y, n, g, den);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

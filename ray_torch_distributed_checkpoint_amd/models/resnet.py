@@ -120,7 +120,7 @@ class ResNet18(nn.Module):
     def forward(self, x):
         """x: NCHW images (any float dtype).  Returns [B, num_classes] logits."""
         if x.is_cuda:
-            h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+            h = cnn.to_nhwc_bf16(x)
         else:
             h = x.permute(0, 2, 3, 1).float().contiguous()
         h = self.bn1(self.conv1(h), relu=True)

@@ -39,6 +39,26 @@ def _out_hw(H, W, KH, KW, stride, pad):
     return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
 
 
+_padded: dict = {}
+
+
+def _padded_buffer(key, shape, dtype, device) -> torch.Tensor:
+    """A persistent zero-initialised operand buffer: only its leading block is ever rewritten,
+    so the padding stays zero without a fill per step."""
+    k = (key, tuple(shape), dtype, str(device))
+    t = _padded.get(k)
+    if t is None:
+        t = torch.zeros(shape, dtype=dtype, device=device)
+        _padded[k] = t
+    return t
+
+
+def _copy_rows(dst: torch.Tensor, src: torch.Tensor, rows: int, cols: int) -> None:
+    """dst[:rows, :cols] = src[:rows, :cols] (2-D row-major tensors, same dtype) as one DMA copy."""
+    es = src.element_size()
+    gpu_ext().copy2d(dst, src, rows, cols * es, dst.stride(0) * es, src.stride(0) * es)
+
+
 def _weight_matrix(w: torch.Tensor, Kp: int) -> torch.Tensor:
     """bf16 GEMM operand [Cout, Kp] with k = (kh*KW + kw)*Cin + c (zero-padded columns).  A
     channels-last weight's bf16 shadow already is this matrix (a view: no copy per step)."""
@@ -48,9 +68,23 @@ def _weight_matrix(w: torch.Tensor, Kp: int) -> torch.Tensor:
     if m.is_contiguous() and m[0].numel() == Kp:
         return m.reshape(Cout, Kp)
     m = m.reshape(Cout, -1)
+    if m.shape[1] != Kp and m.is_contiguous() and s.is_cuda:
+        out = _padded_buffer(("wmat", id(w)), (Cout, Kp), m.dtype, m.device)
+        _copy_rows(out, m, Cout, m.shape[1])
+        return out
     if m.shape[1] != Kp:
         m = F.pad(m, (0, Kp - m.shape[1]))
     return m.contiguous()
+
+
+def to_nhwc_bf16(x: torch.Tensor) -> torch.Tensor:
+    """NCHW images -> NHWC bf16 network input (one native pass for 3-channel fp32 input)."""
+    if x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 3 and x.is_contiguous() \
+            and (x.shape[2] * x.shape[3]) % 8 == 0:
+        y = torch.empty((x.shape[0], x.shape[2], x.shape[3], 3), dtype=torch.bfloat16, device=x.device)
+        gpu_ext().nchw_to_nhwc_bf16(x, y)
+        return y
+    return x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
 
 
 def _grad_matrix(w: torch.Tensor, K: int):
@@ -164,9 +198,13 @@ class _Conv2d(torch.autograd.Function):
         cols = saved
         if ctx.needs_input_grad[1]:
             dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
-            dw = dwm[:, :K].view(Cout, KH, KW, C).permute(0, 3, 1, 2)
-            tw = grad_target(ctx.w)
-            dw = tw.copy_(dw) if tw is not None else dw.contiguous()
+            tw, direct = _grad_matrix(ctx.w, K)
+            if direct is not None:  # channels-last gradient slot = [Cout, K]: one strided DMA copy
+                _copy_rows(direct, dwm, Cout, K)
+                dw = tw
+            else:
+                dw = dwm[:, :K].view(Cout, KH, KW, C).permute(0, 3, 1, 2)
+                dw = tw.copy_(dw) if tw is not None else dw.contiguous()
         if ctx.needs_input_grad[0]:
             acc = _arrive(ctx.stash)
             dcols = G.linear_dgrad(dy2, wm)  # [Mp, Kp] bf16
@@ -409,30 +447,55 @@ class _Classifier(torch.autograd.Function):
         N = w.shape[0]
         Np, Mp = _ceil(N, 64), _ceil(Bn, 64)
         ws = shadow_of(w)
-        wp = F.pad(ws, (0, 0, 0, Np - N)) if Np != N else ws
-        bp = F.pad(b, (0, Np - N)) if Np != N else b
-        xp = _rows_padded(x.contiguous(), Mp)
-        y = G.linear_fwd(xp, wp.contiguous(), bias=bp.contiguous())
+        # padded operands live in persistent zero buffers: one DMA copy of the live rows each
+        wp, bp = ws, b
+        if Np != N:
+            wp = _padded_buffer(("fc_w", id(w)), (Np, K), ws.dtype, ws.device)
+            _copy_rows(wp, ws, N, K)
+            bp = _padded_buffer(("fc_b", id(b)), (Np, 1), b.dtype, b.device)
+            _copy_rows(bp, b.view(N, 1), N, 1)
+            bp = bp.view(Np)
+        xp = x.contiguous()
+        if Mp != Bn:
+            xp = _padded_buffer(("fc_x", Bn), (Mp, K), x.dtype, x.device)
+            _copy_rows(xp, x.contiguous(), Bn, K)
+        y = G.linear_fwd(xp, wp, bias=bp)
         ctx.save_for_backward(xp, wp)
         ctx.meta = (Bn, N, Np, Mp)
         ctx.params = (w, b)
-        return y[:Bn, :N].contiguous()
+        if Np == N and Mp == Bn:
+            return y
+        out = torch.empty((Bn, N), dtype=y.dtype, device=y.device)
+        _copy_rows(out, y, Bn, N)
+        return out
 
     @staticmethod
     def backward(ctx, dy):
         xp, wp = ctx.saved_tensors
         Bn, N, Np, Mp = ctx.meta
-        dyp = torch.zeros((Mp, Np), dtype=torch.bfloat16, device=dy.device)
-        dyp[:Bn, :N].copy_(dy)
+        dy = dy.contiguous()
+        dyp = dy
+        if Np != N or Mp != Bn:
+            dyp = _padded_buffer(("fc_dy", Bn, N), (Mp, Np), torch.bfloat16, dy.device)
+            _copy_rows(dyp, dy, Bn, N)
         w, b = ctx.params
         dx = G.linear_dgrad(dyp, wp)[:Bn] if ctx.needs_input_grad[0] else None
-        dw = G.linear_wgrad(dyp, xp)[:N] if ctx.needs_input_grad[1] else None
-        db = G.colsum(dyp)[:N] if ctx.needs_input_grad[2] else None
         tw, tb = grad_target(w), grad_target(b)
-        if dw is not None and tw is not None:
-            dw = tw.copy_(dw)
-        if db is not None and tb is not None:
-            db = tb.copy_(db)
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            dwp = G.linear_wgrad(dyp, xp)  # [Np, K] fp32
+            if tw is not None:
+                _copy_rows(tw, dwp, N, tw.shape[1])
+                dw = tw
+            else:
+                dw = dwp[:N].contiguous()
+        if ctx.needs_input_grad[2]:
+            dbp = G.colsum(dyp)  # [Np]
+            if tb is not None:
+                _copy_rows(tb.view(N, 1), dbp.view(Np, 1), N, 1)
+                db = tb
+            else:
+                db = dbp[:N].contiguous()
         return dx, dw, db
 
 

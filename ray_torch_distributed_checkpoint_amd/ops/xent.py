@@ -23,11 +23,6 @@ from .shadow import shadow_of
 IGNORE_INDEX = -100
 
 
-def _valid_count(target: torch.Tensor) -> torch.Tensor:
-    """Number of non-ignored rows as a 1-element fp32 device tensor (no host sync)."""
-    return (target.reshape(-1) != IGNORE_INDEX).sum(dtype=torch.float32).clamp_min(1.0).reshape(1)
-
-
 def _check_target(target: torch.Tensor) -> None:
     if target.dtype != torch.int64:
         raise TypeError(f"cross_entropy: int64 class targets expected, got {target.dtype}")
@@ -41,20 +36,21 @@ class _CrossEntropy(torch.autograd.Function):
         lg = logits.contiguous()
         loss = torch.empty(M, dtype=torch.float32, device=lg.device)
         grad = torch.empty_like(lg)
-        scale = 1.0 / n_valid if n_valid is not None else 1.0
-        gpu_ext().xent(lg, grad, target.contiguous(), loss, None, None, M, V, V, scale, IGNORE_INDEX)
-        if n_valid is None:
-            cnt = _valid_count(target)
-            ctx.save_for_backward(grad, cnt)
-            return (loss.sum() / cnt).reshape(())
-        ctx.save_for_backward(grad, None)
-        return loss.sum() / n_valid
+        tgt = target.contiguous()
+        # unscaled softmax gradient; the mean and the 1/divisor (device count of non-ignored
+        # rows, or n_valid) come out of one native reduction - no ATen kernels in the step
+        gpu_ext().xent(lg, grad, tgt, loss, None, None, M, V, V, 1.0, IGNORE_INDEX)
+        out = torch.empty(2, dtype=torch.float32, device=lg.device)
+        gpu_ext().xent_finalize(loss, tgt if n_valid is None else None, float(n_valid or 1), out)
+        ctx.save_for_backward(grad, out)
+        return out[0]
 
     @staticmethod
     def backward(ctx, g):
-        grad, cnt = ctx.saved_tensors
-        a = g.to(torch.float32) if cnt is None else (g.to(torch.float32) / cnt).reshape(())
-        return grad * a.to(grad.dtype), None, None
+        grad, out = ctx.saved_tensors
+        dl = torch.empty_like(grad)
+        gpu_ext().scale_dev(grad, dl, g.detach().to(torch.float32).reshape(1).contiguous(), out[1:2])
+        return dl, None, None
 
 
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor, n_valid: int | None = None) -> torch.Tensor:
@@ -123,22 +119,24 @@ class _LMHeadXent(torch.autograd.Function):
                 G.gemm_bf16(x2[r0:r0 + n], ws, chunk, n, Vp, C, C, C, Vp, True, True)
                 gpu_ext().xent(chunk, logits[r0:r0 + n], tgt[r0:r0 + n], loss[r0:r0 + n], None, None, n, vocab,
                                Vp, scale, IGNORE_INDEX)
-        cnt = _valid_count(target) if n_valid is None else None
-        ctx.save_for_backward(x2, ws, logits, cnt)
+        out = torch.empty(2, dtype=torch.float32, device=x.device)
+        # out[0] = mean loss; out[1] = divisor (device count of non-ignored rows, or n_valid -
+        # whose 1/n_valid the kernel already folded into the gradient)
+        gpu_ext().xent_finalize(loss, tgt if n_valid is None else None, float(n_valid or 1), out)
+        ctx.save_for_backward(x2, ws, logits, out[1:2] if n_valid is None else None)
         ctx.in_shape = x.shape
         ctx.w = w
-        if cnt is not None:
-            return (loss.sum() / cnt).reshape(())
-        return loss.sum() / n_valid
+        return out[0]
 
     @staticmethod
     def backward(ctx, g):
         x2, ws, dlogits, cnt = ctx.saved_tensors
         # the upstream loss gradient (and the 1/#valid divisor) is a device-side alpha inside both GEMMs
-        gs = g.detach().to(torch.float32).reshape(1)
+        gs = g.detach().to(torch.float32).reshape(1).contiguous()
         if cnt is not None:
-            gs = gs / cnt
-        gs = gs.contiguous()
+            a = torch.empty(1, dtype=torch.float32, device=gs.device)
+            gpu_ext().xent_alpha(gs, cnt, a)
+            gs = a
         dx = G.linear_dgrad(dlogits, ws, alpha_dev=gs)
         dw = G.linear_wgrad(dlogits, x2, out=grad_target(ctx.w), alpha_dev=gs)
         return dx.view(ctx.in_shape), dw, None, None, None
