@@ -605,12 +605,23 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * t + 4 * g + r;
-        float pv = fexp2(fmaf(sacc[r], c, -lse_s[ql]));
-        if (diag && qb * BQ + ql < mykey) pv = 0.f;
-        p[t][r] = pv;
-        ds[t][r] = pv * (dpacc[r] - del_s[ql]);
+        p[t][r] = fexp2(fmaf(sacc[r], c, -lse_s[ql]));
+        ds[t][r] = dpacc[r] - del_s[ql];
       }
     }
+    // causal mask only on the diagonal block (wave-uniform branch: no per-element selects on
+    // the other steps - the loop is VALU-issue bound)
+    if (diag) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (qb * BQ + 16 * t + 4 * g + r < mykey) p[t][r] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds[t][r] *= p[t][r];
     const bf16x8 p0 = pack_pair(p[0], p[1]), p1 = pack_pair(p[2], p[3]);
     const bf16x8 d0 = pack_pair(ds[0], ds[1]), d1 = pack_pair(ds[2], ds[3]);
 #pragma unroll
@@ -733,11 +744,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
       }
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int key = kb * BKV + 16 * t + 4 * g + rr;
-        float pv = fexp2(fmaf(sacc[rr], c, -lse2));
-        if (diag && key > myq) pv = 0.f;
+        const float pv = fexp2(fmaf(sacc[rr], c, -lse2));
         ds[t][rr] = pv * (dpacc[rr] - del);
       }
+    }
+    if (diag) {  // causal mask on the diagonal block only (wave-uniform)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          if (kb * BKV + 16 * t + 4 * g + rr > myq) ds[t][rr] = 0.f;
     }
     const bf16x8 d0 = pack_pair(ds[0], ds[1]), d1 = pack_pair(ds[2], ds[3]);
 #pragma unroll
