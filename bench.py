@@ -60,6 +60,8 @@ def main():
                     help="gradient all-reduce dtype (fp32 = torch DDP semantics)")
     ap.add_argument("--p2p-kb", type=float, default=0.0,
                     help="buckets <= this many KiB use the one-shot hipIpc all-reduce (0 = all on RCCL)")
+    ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
+                    help="1: ZeRO-1 (reduce-scatter gradients, sharded optimizer step, all-gather parameters)")
     ap.add_argument("--no-ckpt", action="store_true")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-scope", default="full", choices=["full", "model"],
@@ -105,7 +107,8 @@ def main():
     # the last bucket's all-reduce (GPT-2: the tied token table, whose gradient completes at the
     # end of backward) overlaps the fused optimizer's update of every other parameter
     net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, defer_tail_to_optimizer=True,
-                                  grad_comm_dtype=args.grad_comm_dtype, p2p_max_kb=args.p2p_kb) if world > 1 else model
+                                  grad_comm_dtype=args.grad_comm_dtype, p2p_max_kb=args.p2p_kb,
+                                  zero_stage=args.zero) if world > 1 else model
     B, T = wl["batch"], wl["seq_len"]
     fwd_loss = wl["loss"]
 

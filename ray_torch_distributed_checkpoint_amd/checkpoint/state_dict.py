@@ -90,6 +90,8 @@ def get_optimizer_state_dict(model: nn.Module, optimizers, *, options: StateDict
     for opt in _optims(optimizers):
         if any(p not in opt.state for g in opt.param_groups for p in g["params"]):
             _init_optim_state(opt)
+        if hasattr(opt, "consolidate_state"):
+            opt.consolidate_state()  # ZeRO-1 sharded state -> full state on every rank (collective)
         if hasattr(opt, "_materialize_steps"):
             opt._materialize_steps()  # fused optimizers keep step counts as host ints
         for g in opt.param_groups:

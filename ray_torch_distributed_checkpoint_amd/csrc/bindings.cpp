@@ -624,13 +624,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<rtdc_ddp::GradBucketEngine>(m, "GradBucketEngine")
       .def(py::init([](at::Tensor flat, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
                        std::vector<std::pair<int64_t, int64_t>> seg, py::object pg, bool use_avg, double post_scale,
-                       c10::optional<at::Tensor> comm_buf) {
+                       c10::optional<at::Tensor> comm_buf, int64_t zero_world, int64_t zero_rank) {
              auto cpg = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
              return new rtdc_ddp::GradBucketEngine(flat, std::move(bounds), std::move(param_bucket), std::move(seg),
-                                                   cpg, use_avg, post_scale, comm_buf);
+                                                   cpg, use_avg, post_scale, comm_buf, zero_world, zero_rank);
            }),
            py::arg("flat_grad"), py::arg("bounds"), py::arg("param_bucket"), py::arg("segments"),
-           py::arg("process_group"), py::arg("use_avg"), py::arg("post_scale"), py::arg("comm_buf") = py::none())
+           py::arg("process_group"), py::arg("use_avg"), py::arg("post_scale"), py::arg("comm_buf") = py::none(),
+           py::arg("zero_world") = 0, py::arg("zero_rank") = 0)
       .def("comm_bytes_per_step", &rtdc_ddp::GradBucketEngine::comm_bytes_per_step)
       .def("mark_ready", &rtdc_ddp::GradBucketEngine::mark_ready)
       .def("finalize", &rtdc_ddp::GradBucketEngine::finalize, py::arg("defer_last") = false)

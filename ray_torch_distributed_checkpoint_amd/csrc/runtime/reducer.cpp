@@ -43,9 +43,11 @@ class GradBucketEngine {
   // seg: per parameter (offset, numel) inside flat_grad, same order as param_bucket
   GradBucketEngine(at::Tensor flat_grad, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
                    std::vector<std::pair<int64_t, int64_t>> seg, c10::intrusive_ptr<c10d::ProcessGroup> pg,
-                   bool use_avg, double post_scale, c10::optional<at::Tensor> comm_buf)
+                   bool use_avg, double post_scale, c10::optional<at::Tensor> comm_buf, int64_t zero_world = 0,
+                   int64_t zero_rank = 0)
       : flat_(std::move(flat_grad)), bounds_(std::move(bounds)), param_bucket_(std::move(param_bucket)),
-        seg_(std::move(seg)), pg_(std::move(pg)), use_avg_(use_avg), post_scale_(post_scale) {
+        seg_(std::move(seg)), pg_(std::move(pg)), use_avg_(use_avg), post_scale_(post_scale),
+        zero_world_(zero_world > 1 ? zero_world : 0), zero_rank_(zero_rank) {
     TORCH_CHECK(seg_.size() == param_bucket_.size(), "one segment per parameter");
     TORCH_CHECK(bounds_.size() >= 2, "need at least one bucket");
     const size_t nb = bounds_.size() - 1;
@@ -61,6 +63,12 @@ class GradBucketEngine {
         for (auto& e : events_) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
                                             "hipEventCreate");
       }
+    }
+    if (zero_world_) {
+      TORCH_CHECK(zero_rank_ >= 0 && zero_rank_ < zero_world_, "ZeRO rank out of range");
+      for (size_t b = 0; b < nb; ++b)
+        TORCH_CHECK((bounds_[b + 1] - bounds_[b]) % (64 * zero_world_) == 0,
+                    "ZeRO: every bucket must be a multiple of 64 x world elements");
     }
     expected_.assign(nb, 0);
     for (int64_t b : param_bucket_) {
@@ -203,7 +211,15 @@ class GradBucketEngine {
     while (next_ < works_.size() && pending_[next_] <= 0) launch(next_++);
   }
 
-  bool is_p2p(size_t b) const { return p2p_ && b < via_p2p_.size() && via_p2p_[b]; }
+  bool is_p2p(size_t b) const { return !zero_world_ && p2p_ && b < via_p2p_.size() && via_p2p_[b]; }
+
+  // ZeRO-1: the [lo, hi) range of bucket b this rank owns after the reduce-scatter
+  std::pair<int64_t, int64_t> owned(size_t b) const {
+    const int64_t lo = bounds_[b], hi = bounds_[b + 1];
+    if (!zero_world_) return {lo, hi};
+    const int64_t sh = (hi - lo) / zero_world_;
+    return {lo + zero_rank_ * sh, lo + (zero_rank_ + 1) * sh};
+  }
 
   void launch(size_t b) {
     const int64_t lo = bounds_[b], hi = bounds_[b + 1];
@@ -238,9 +254,19 @@ class GradBucketEngine {
       }
       t[0] = dst;
     }
-    c10d::AllreduceOptions opts;
-    opts.reduceOp = use_avg_ ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
-    works_[b] = pg_->allreduce(t, opts);
+    if (zero_world_) {
+      // ZeRO-1: reduce-scatter in place - this rank's shard of the bucket receives the
+      // average, the rest of the slice keeps the local gradient (never read)
+      const auto [olo, ohi] = owned(b);
+      at::Tensor out = t[0].slice(0, olo - lo, ohi - lo);
+      c10d::ReduceScatterOptions ro;
+      ro.reduceOp = use_avg_ ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
+      works_[b] = pg_->_reduce_scatter_base(out, t[0], ro);
+    } else {
+      c10d::AllreduceOptions opts;
+      opts.reduceOp = use_avg_ ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
+      works_[b] = pg_->allreduce(t, opts);
+    }
     launched_[b] = true;
     if (side_) {
       // widen back on the side stream right after the collective (Work::wait on a CUDA-like
@@ -254,7 +280,7 @@ class GradBucketEngine {
 
   // bf16 reduced slice -> fp32 master gradient slice (x post-scale for SUM backends)
   void widen(size_t b) {
-    const int64_t lo = bounds_[b], hi = bounds_[b + 1];
+    const auto [lo, hi] = owned(b);  // (the whole bucket without ZeRO)
     const float scale = use_avg_ ? 1.f : (float)post_scale_;
     if (flat_.is_cuda()) {
       hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
@@ -276,6 +302,7 @@ class GradBucketEngine {
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   bool use_avg_;
   double post_scale_;
+  int64_t zero_world_, zero_rank_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
   c10::intrusive_ptr<c10d::Work> tail_;
   std::vector<bool> launched_, marked_;

@@ -35,8 +35,36 @@ def _is_channels_last(p: torch.Tensor) -> bool:
     return p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(memory_format=torch.channels_last)
 
 
+class ZeroLayout:
+    """ZeRO-1 ownership of a flat space (parallel/ddp.py `zero_stage=1`): every gradient bucket
+    [start, end) - a multiple of 64 x world elements long - is split into `world` equal shards,
+    rank r owns shard r of each.  The data-parallel engine reduce-scatters each bucket onto its
+    owner, the fused optimizer updates owned elements only, and `gather` all-gathers a flat
+    buffer (parameters after every step, optimizer state for a checkpoint) back to every rank."""
+
+    def __init__(self, buckets, rank: int, world: int, group=None):
+        self.buckets = [(int(a), int(b)) for a, b in buckets]
+        self.rank, self.world, self.group = rank, world, group
+        self.owned = []
+        for a, b in self.buckets:
+            n = b - a
+            assert n % (64 * world) == 0, "ZeRO buckets must be multiples of 64 x world elements"
+            sh = n // world
+            self.owned.append((a + rank * sh, a + (rank + 1) * sh))
+
+    def gather(self, buf: torch.Tensor) -> None:
+        """Every bucket of `buf`: each rank's owned shard -> all ranks (in place)."""
+        import torch.distributed as dist
+
+        for (a, b), (oa, ob) in zip(self.buckets, self.owned):
+            dist.all_gather_into_tensor(buf[a:b], buf[oa:ob], group=self.group)
+
+    def owned_elements(self) -> int:
+        return sum(b - a for a, b in self.owned)
+
+
 class FlatParamSpace:
-    def __init__(self, params, device=None, shadow_dtype=torch.bfloat16, grads=True):
+    def __init__(self, params, device=None, shadow_dtype=torch.bfloat16, grads=True, align_after=None):
         params = list(params)
         assert params, "no parameters"
         seen = set()
@@ -55,6 +83,7 @@ class FlatParamSpace:
         self.fresh = False
         self.step_id = 0
         off = 0
+        align_after = align_after or {}
         for i, p in enumerate(uniq):
             assert p.dtype == torch.float32, "FlatParamSpace holds fp32 master parameters"
             # channels-last 4-D parameters (ResNet conv weights) keep that memory order in the
@@ -62,6 +91,9 @@ class FlatParamSpace:
             # the weight-gradient GEMM writes its [O, KH*KW*I] output straight into the slice
             self.segments.append(Segment(i, off, p.numel(), tuple(p.shape), _is_channels_last(p)))
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+            a = align_after.get(i)
+            if a:  # zero padding after this parameter (ZeRO bucket ends: multiples of 64 x world)
+                off = (off + a - 1) // a * a
         self.numel = off
         self._seg_of = {id(p): s for p, s in zip(uniq, self.segments)}
         self.data = torch.zeros(off, dtype=torch.float32, device=self.device)
@@ -80,6 +112,7 @@ class FlatParamSpace:
             self.shadow = torch.empty(off, dtype=shadow_dtype, device=self.device)
             self.refresh_shadows()
         self.grad_scale = 1.0
+        self.zero: ZeroLayout | None = None
         self._offsets = None
         self._chunk_cache: dict = {}
         # (flat offset, wait fn) of a gradient slice whose all-reduce is still in flight
@@ -179,6 +212,27 @@ class FlatParamSpace:
             if p.grad is None:
                 p.grad = self.view(self.grad, s)
 
+    def set_zero(self, layout: ZeroLayout | None) -> None:
+        self.zero = layout
+        self._chunk_cache.clear()
+
+    def _ranges(self, s: Segment):
+        """[start, end) flat ranges of segment s this rank updates (all of it without ZeRO)."""
+        a, b = s.offset, s.offset + s.numel
+        if self.zero is None:
+            return [(a, b)]
+        out = []
+        for oa, ob in self.zero.owned:
+            lo, hi = max(a, oa), min(b, ob)
+            if lo < hi:
+                out.append((lo, hi))
+        return out
+
+    def _chunks(self, s: Segment, d):
+        for a, b in self._ranges(s):
+            for st in range(a, b, CHUNK):
+                yield st, min(CHUNK, b - st) | (int(bool(d)) << 32)
+
     def chunk_table_split(self, params_subset, decay_flags, split: int):
         """Two chunk tables: segments below flat offset `split`, and the rest."""
         key = ("split", tuple(id(p) for p in params_subset), tuple(decay_flags), split)
@@ -188,29 +242,40 @@ class FlatParamSpace:
         lo, hi = [], []
         for p, d in zip(params_subset, decay_flags):
             s = self.segment_of(p)
-            for st in range(0, s.numel, CHUNK):
-                ln = min(CHUNK, s.numel - st)
-                (lo if s.offset < split else hi).append((s.offset + st, ln | (int(bool(d)) << 32)))
+            (lo if s.offset < split else hi).extend(self._chunks(s, d))
         out = tuple((torch.tensor(r if r else [(0, 0)], dtype=torch.int64).to(self.device), len(r)) for r in (lo, hi))
         self._chunk_cache[key] = out
         return out
 
     def chunk_table(self, params_subset, decay_flags) -> tuple[torch.Tensor, int]:
-        """int64 [nchunks, 2] rows of (start, len | decay<<32) for the native optimizer kernels."""
+        """int64 [nchunks, 2] rows of (start, len | decay<<32) for the native optimizer kernels
+        (only this rank's owned elements under ZeRO-1)."""
         key = (tuple(id(p) for p in params_subset), tuple(decay_flags))
         hit = self._chunk_cache.get(key)
         if hit is not None:
             return hit
         rows = []
         for p, d in zip(params_subset, decay_flags):
-            s = self.segment_of(p)
-            for st in range(0, s.numel, CHUNK):
-                ln = min(CHUNK, s.numel - st)
-                rows.append((s.offset + st, ln | (int(bool(d)) << 32)))
+            rows.extend(self._chunks(self.segment_of(p), d))
         t = torch.tensor(rows if rows else [(0, 0)], dtype=torch.int64).to(self.device)
         out = (t, len(rows))
         self._chunk_cache[key] = out
         return out
+
+    def after_step(self) -> None:
+        """End of an optimizer step: under ZeRO-1 every rank updated only its shards; gather
+        the fp32 parameters back and rebuild the bf16 compute shadows."""
+        if self.zero is None:
+            return
+        self.zero.gather(self.data)
+        if self.shadow is not None:
+            from ..ops._ext import gpu_ext
+
+            gpu_ext().f32_to_bf16(self.data, self.shadow)
+            # the in-place collective moved the parameters' version counters: the shadows are
+            # current (converted just now), so re-stamp them instead of re-converting per tensor
+            for p in self.params:
+                p._rtdc_shadow_ver = p._version
 
 
 def space_of(params) -> FlatParamSpace | None:

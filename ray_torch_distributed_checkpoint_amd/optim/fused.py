@@ -110,7 +110,16 @@ class _FlatOptimizer(torch.optim.Optimizer):
             if st is not None:
                 st["step"] = torch.tensor(float(n))
 
+    def consolidate_state(self) -> None:
+        """ZeRO-1: every rank updated only its own shards of the flat state buffers; gather them
+        so every rank holds the full, torch-format state (collective: call on every rank)."""
+        sp = self._space
+        if sp is not None and sp.zero is not None:
+            for buf in self._bufs.values():
+                sp.zero.gather(buf)
+
     def state_dict(self):
+        self.consolidate_state()
         self._materialize_steps()
         return super().state_dict()
 
@@ -230,6 +239,7 @@ class FusedAdamW(_FlatOptimizer):
 
                     launches.append((sub, [wd != 0.0] * len(sub), fn))
             self._launch_split(sp, launches)
+            sp.after_step()  # ZeRO-1: gather the updated shards
             return loss
         sp = space_of(self._all_params())
         if sp is not None:
@@ -303,6 +313,7 @@ class FusedSGD(_FlatOptimizer):
 
                     launches.append((sub, [wd != 0.0] * len(sub), fn))
             self._launch_split(sp, launches)
+            sp.after_step()  # ZeRO-1: gather the updated shards
             return loss
         sp = space_of(self._all_params())
         if sp is not None:

@@ -108,14 +108,19 @@ class TorchConfig:
     # buckets of at most this many KiB use the one-shot hipIpc all-reduce (parallel/p2p.py)
     # instead of RCCL; 0 = off (opt-in: it needs every rank's GPU on one node)
     p2p_max_kb: float = 0.0
+    # 1: ZeRO-1 - reduce-scatter the gradients, each rank runs the optimizer on its 1/world
+    # shard, all-gather the parameters (parallel/ddp.py); 0: every rank updates everything
+    zero_stage: int = 0
 
     def __post_init__(self):
         if self.grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
         if self.p2p_max_kb < 0:
             raise ValueError("p2p_max_kb must be >= 0")
+        if self.zero_stage not in (0, 1):
+            raise ValueError("zero_stage must be 0 or 1")
 
     def ddp_kwargs(self) -> dict:
         return dict(bucket_cap_mb=self.bucket_cap_mb, first_bucket_mb=self.first_bucket_mb,
                     grad_comm_dtype=self.grad_comm_dtype, defer_tail_to_optimizer=self.defer_tail_to_optimizer,
-                    p2p_max_kb=self.p2p_max_kb)
+                    p2p_max_kb=self.p2p_max_kb, zero_stage=self.zero_stage)

@@ -416,7 +416,7 @@ def train_workload(model: str = "gpt2-tiny", steps: int = 20, num_workers: int =
                    ckpt_every_n_steps: int | None = 5, num_checkpoints_to_keep: int | None = 2,
                    checkpoint_storage_path: str | None = None, checkpoint=None, resume_mode: str = "exact",
                    max_failures: int = 0, seed: int = 1234, grad_comm_dtype: str = "fp32",
-                   bucket_cap_mb: float = 32.0, progress_timeout_s: float | None = 300.0,
+                   bucket_cap_mb: float = 32.0, zero_stage: int = 0, progress_timeout_s: float | None = 300.0,
                    dataset_size: int = 1 << 20, name: str | None = None, verbose: int = 1):
     """`train_fashion_mnist`'s counterpart for the bf16 workloads (R/my_ray_module.py:216-251)."""
     cfg = WorkloadConfig(model=model, steps=steps, batch_size_per_worker=batch_size_per_worker, seq_len=seq_len,
@@ -431,7 +431,8 @@ def train_workload(model: str = "gpt2-tiny", steps: int = 20, num_workers: int =
     trainer = train.TorchTrainer(
         train_loop_per_worker, train_loop_config={k: v for k, v in asdict(cfg).items() if v is not None},
         scaling_config=train.ScalingConfig(num_workers=num_workers, use_gpu=use_gpu),
-        torch_config=train.TorchConfig(grad_comm_dtype=grad_comm_dtype, bucket_cap_mb=bucket_cap_mb),
+        torch_config=train.TorchConfig(grad_comm_dtype=grad_comm_dtype, bucket_cap_mb=bucket_cap_mb,
+                                       zero_stage=zero_stage),
         run_config=run_config)
     return trainer.fit()
 
@@ -448,11 +449,13 @@ def main(argv=None):
     ap.add_argument("--storage", default=None)
     ap.add_argument("--max-failures", type=int, default=0)
     ap.add_argument("--grad-comm-dtype", default="fp32")
+    ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1])
     ap.add_argument("--cpu", action="store_true")
     a = ap.parse_args(argv)
     use_gpu = torch.cuda.is_available() and not a.cpu
     res = train_workload(a.model, a.steps, a.num_workers, use_gpu, a.batch, a.seq_len, None, a.ckpt_every, a.keep,
-                         a.storage, max_failures=a.max_failures, grad_comm_dtype=a.grad_comm_dtype)
+                         a.storage, max_failures=a.max_failures, grad_comm_dtype=a.grad_comm_dtype,
+                         zero_stage=a.zero_stage)
     print(res)
 
 

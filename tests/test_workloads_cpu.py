@@ -146,3 +146,16 @@ def test_bf16_grad_comm_workload_runs(tmp_path):
     ref = _losses(_fit(tmp_path, "d", steps=4).path)
     assert la[1] == ref[1]  # identical init and data; the first update differs only by bf16 rounding
     assert all(abs(la[k] - ref[k]) < 0.05 for k in la)
+
+
+def test_zero1_workload_kill_restart_bit_equal(tmp_path, monkeypatch):
+    """ZeRO-1 under the trainer: the consolidated optimizer state goes into the async sharded
+    checkpoint, a restart restores it, and the losses equal both the uninterrupted ZeRO run and
+    the replicated-optimizer run."""
+    a = _fit(tmp_path, "a", steps=6, zero_stage=1)
+    ref = _fit(tmp_path, "r", steps=6)
+    monkeypatch.setenv("RTDC_FAIL_AT_STEP", "5:1")
+    b = _fit(tmp_path, "b", steps=6, zero_stage=1, max_failures=1)
+    la, lb, lr = _losses(a.path), _losses(b.path), _losses(ref.path)
+    assert la == lb
+    assert la == lr

@@ -46,6 +46,7 @@ class RayTorchTrain(FlowSpec):
     steps = Parameter("steps", default=100, help="optimizer steps (bf16 workloads)")
     ckpt_every_n_steps = Parameter("ckpt_every_n_steps", default=25, help="sharded async checkpoint interval")
     grad_comm_dtype = Parameter("grad_comm_dtype", default="fp32", help="fp32 | bf16 gradient all-reduce")
+    zero_stage = Parameter("zero_stage", default=0, help="1: ZeRO-1 sharded optimizer step (bf16 workloads)")
 
     @step
     def start(self):
@@ -99,7 +100,8 @@ class RayTorchTrain(FlowSpec):
                 batch_size_per_worker=max(1, int(self.global_batch_size) // n) if int(self.global_batch_size) != 32
                 else None, lr=None, ckpt_every_n_steps=int(self.ckpt_every_n_steps),
                 checkpoint_storage_path=current.ray_storage_path, checkpoint=args.get("checkpoint"),
-                resume_mode=mode, max_failures=int(self.max_failures), grad_comm_dtype=self.grad_comm_dtype)
+                resume_mode=mode, max_failures=int(self.max_failures), grad_comm_dtype=self.grad_comm_dtype,
+                zero_stage=int(self.zero_stage))
         self.next(self.join)
 
     @step
