@@ -1,0 +1,52 @@
+"""LayerNorm forward at the GPT-2 shape (16384 x 768, bf16): the native row kernel vs ATen's,
+plus the HBM bandwidth it reaches (the backward is timed inside the model profile:
+scripts/gpu_prof_gpt2.sh).  python benchmarks/norm_bench.py"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from ray_torch_distributed_checkpoint_amd.ops import norm  # noqa: E402
+
+
+def timeit(fn, reps=50):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps * 1e3
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    M, D = 16384, 768
+    x = torch.randn(M, D, device=dev).bfloat16()
+    w = torch.nn.Parameter(torch.ones(D, device=dev))
+    b = torch.nn.Parameter(torch.zeros(D, device=dev))
+    nb = M * D * 2
+
+    def ours_fwd():
+        return norm.layer_norm(x, w, b)
+
+    def aten_fwd():
+        return F.layer_norm(x, (D,), w.bfloat16(), b.bfloat16())
+
+    r = {"M": M, "D": D}
+    r["ours_fwd_us"] = round(timeit(ours_fwd), 1)
+    r["ours_fwd_TBps"] = round(2 * nb / r["ours_fwd_us"] / 1e6, 2)
+    r["aten_fwd_us"] = round(timeit(aten_fwd), 1)
+    print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
