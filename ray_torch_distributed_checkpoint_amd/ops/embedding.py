@@ -14,6 +14,17 @@ from .gradbuf import claimed_target, grad_target
 from .shadow import shadow_of
 
 
+_side: dict = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    s = _side.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _side[device] = s
+    return s
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, wte, wpe):
@@ -22,6 +33,18 @@ class _Embedding(torch.autograd.Function):
         idx_c = idx.contiguous()
         out = torch.empty((B, T, D), dtype=torch.bfloat16, device=idx.device)
         gpu_ext().embed_fwd(idx_c, shadow_of(wte), shadow_of(wpe) if wpe is not None else None, out, T)
+        # the backward's stable sort of the token ids depends only on idx: run it now on a side
+        # stream, concurrently with the forward pass, instead of on the backward's critical path
+        cur = torch.cuda.current_stream(idx.device)
+        side = _side_stream(idx.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            sidx, perm = torch.sort(idx_c.reshape(-1), stable=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        sidx.record_stream(cur)
+        perm.record_stream(cur)
+        ctx.sorted = (sidx, perm, done)
         ctx.save_for_backward(idx_c)
         ctx.shapes = (wte.shape, None if wpe is None else wpe.shape)
         ctx.params = (wte, wpe)
@@ -44,8 +67,12 @@ class _Embedding(torch.autograd.Function):
         dwpe = None
         if wpe_shape is not None:
             dwpe = grad_target(wpe)
-            dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device) if dwpe is None else dwpe.zero_()
-        sidx, perm = torch.sort(idx.reshape(-1), stable=True)
+            if dwpe is None:
+                dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device)
+            elif T < wpe_shape[0]:
+                dwpe[T:].zero_()  # the kernel writes (not adds) positions [0, T)
+        sidx, perm, done = ctx.sorted
+        torch.cuda.current_stream(idx.device).wait_event(done)
         gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)
         return None, (None if accumulate else dwte), dwpe
 
