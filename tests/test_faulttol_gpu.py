@@ -123,4 +123,4 @@ def test_eval_device_pipeline_matches_numpy_path_gpu(tmp_path):
     np.testing.assert_array_equal(out["logits"], ref_logits)
     np.testing.assert_array_equal(out["predicted_values"], np.concatenate([r["predicted_values"] for r in ref]))
     print(f"eval pass over {ds.count()} rows: {dt * 1e3:.1f} ms")
-    assert dt < 0.5
+    assert dt < 0.05  # measured 10 ms on one MI355X (<= 50 ms for the 10k-row pass)
