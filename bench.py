@@ -114,11 +114,16 @@ def main():
 
     seed = torch.ones((), dtype=torch.float32, device=dev)  # d(loss)/d(loss): no fill kernel per step
 
+    from ray_torch_distributed_checkpoint_amd.utils.profiling import phase  # roctx ranges (--marker-trace)
+
     def step(i):
-        loss = fwd_loss(net, i)
-        loss.backward(seed)
-        opt.step()
-        opt.zero_grad()
+        with phase("fwd"):
+            loss = fwd_loss(net, i)
+        with phase("bwd"):
+            loss.backward(seed)
+        with phase("opt"):
+            opt.step()
+            opt.zero_grad()
         return loss
 
     for i in range(args.warmup):

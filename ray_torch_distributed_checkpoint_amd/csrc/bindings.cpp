@@ -153,7 +153,8 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
 static void gemm_f32(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c10::optional<Tensor> bias,
                      c10::optional<Tensor> aux_in, c10::optional<Tensor> aux_out, int64_t M, int64_t N,
                      int64_t K, int64_t sam, int64_t sak, int64_t sbk, int64_t sbn, int64_t ldc, double alpha,
-                     double beta, int64_t act) {
+                     double beta, int64_t act, double drop_p, uint64_t drop_seed, uint64_t drop_offset,
+                     c10::optional<Tensor> drop_base) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm_f32 needs GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kFloat && B.scalar_type() == at::kFloat && C.scalar_type() == at::kFloat,
               "gemm_f32: fp32 only");
@@ -169,6 +170,14 @@ static void gemm_f32(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c1
   a.sam = sam; a.sak = sak; a.sbk = sbk; a.sbn = sbn;
   a.ldc = (int)ldc;
   a.alpha = (float)alpha; a.beta = (float)beta; a.act = (int)act;
+  TORCH_CHECK(drop_p == 0.0 || (act == 1 && drop_p > 0.0 && drop_p < 1.0 && ldc == N),
+              "gemm_f32: fused dropout needs act=relu, 0 < p < 1 and a dense output");
+  TORCH_CHECK(!drop_base.has_value() || (drop_base->scalar_type() == at::kLong && drop_base->is_cuda()),
+              "gemm_f32: drop_base must be an int64 GPU tensor");
+  a.drop_p = (float)drop_p;
+  a.drop_seed = drop_seed;
+  a.drop_offset = drop_offset;
+  a.drop_base = drop_base.has_value() ? (const long long*)drop_base->data_ptr<int64_t>() : nullptr;
   check_rc(rtdc_gemm_f32(&a, cur_stream()), "gemm_f32");
 }
 
@@ -308,9 +317,9 @@ static void dropout(Tensor x, Tensor y, double p, uint64_t seed, uint64_t offset
            "dropout");
 }
 static void relu_dropout(Tensor h, c10::optional<Tensor> y, c10::optional<Tensor> dy, c10::optional<Tensor> dx,
-                         double p, uint64_t seed, uint64_t offset, bool backward) {
+                         double p, uint64_t seed, uint64_t offset, int64_t backward) {
   check_rc(rtdc_relu_dropout(h.data_ptr(), ptr_or_null(y), ptr_or_null(dy), ptr_or_null(dx), (long long)h.numel(),
-                             (float)p, seed, offset, backward, h.scalar_type() == at::kBFloat16, cur_stream()),
+                             (float)p, seed, offset, (int)backward, h.scalar_type() == at::kBFloat16, cur_stream()),
            "relu_dropout");
 }
 

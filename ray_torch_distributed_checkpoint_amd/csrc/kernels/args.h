@@ -57,6 +57,12 @@ struct GemmF32Args {
   int ldc;
   float alpha, beta;
   int act;  // 0 none, 1 relu (aux_out gets pre-activation if set), 4 relu-backward via aux_in
+  // fused dropout after the ReLU (act 1, drop_p > 0): element i = m * ldc + n keeps with
+  // Philox4x32(seed, counter = drop_offset (+ *drop_base) + i / 4) lane i % 4 >= drop_p - the
+  // dropout kernel's exact stream, so the fused and unfused forms draw the same mask
+  float drop_p;
+  unsigned long long drop_seed, drop_offset;
+  const long long* drop_base;
 };
 
 }  // namespace rtdc

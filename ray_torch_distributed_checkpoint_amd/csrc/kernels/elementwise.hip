@@ -124,10 +124,12 @@ __global__ __launch_bounds__(256) void relu_dropout_kernel(const T* __restrict__
                                                           const T* __restrict__ dy, T* __restrict__ dx, long long n,
                                                           float p, unsigned long long seed,
                                                           unsigned long long offset, int backward) {
+  // backward == 2: the mask is read off the saved OUTPUT h = relu(x) * keep / (1 - p) (h > 0
+  // iff kept and positive) - no RNG, right under graph replay too (fused GEMM dropout)
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   for (long long q = blockIdx.x * 256LL + threadIdx.x; q * 4 < n; q += gridDim.x * 256LL) {
     uint32_t rr[4] = {0u, 0u, 0u, 0u};
-    if (p > 0.f) {
+    if (p > 0.f && backward != 2) {
       uint4 r = Philox::gen(seed, 0, offset + q);
       rr[0] = r.x; rr[1] = r.y; rr[2] = r.z; rr[3] = r.w;
     }
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256) void relu_dropout_kernel(const T* __restrict__
     for (int e = 0; e < 4; ++e) {
       const long long i = q * 4 + e;
       if (i < n) {
-        const bool keep = p > 0.f ? (u32_to_unit(rr[e]) >= p) : true;
+        const bool keep = (p > 0.f && backward != 2) ? (u32_to_unit(rr[e]) >= p) : true;
         const float hv = ldx<T>(h, i);
         const float m = (keep && hv > 0.f) ? scale : 0.f;
         if (backward) stx<T>(dx, i, ldx<T>(dy, i) * m);

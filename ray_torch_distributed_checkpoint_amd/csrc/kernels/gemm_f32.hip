@@ -54,6 +54,8 @@ __global__ __launch_bounds__(1024) void gemm_f32_kernel(GemmF32Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) part[wave][(4 * (lane >> 4) + r) * BN + 16 * j + (lane & 15)] = acc[j][r];
   __syncthreads();
+  const float dscale = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
+  const unsigned long long doff = a.drop_offset + (a.drop_base ? (unsigned long long)*a.drop_base : 0ull);
   for (int e = tid; e < BM * BN; e += blockDim.x) {
     const int m = m0 + e / BN, n = n0 + e % BN;
     if (m >= a.M || n >= a.N) continue;
@@ -66,6 +68,12 @@ __global__ __launch_bounds__(1024) void gemm_f32_kernel(GemmF32Args a) {
     if (a.act == 1) {
       if (a.aux_out) a.aux_out[off] = v;
       v = fmaxf(v, 0.f);
+      if (a.drop_p > 0.f) {  // fused inverted dropout (ReLU -> Dropout of the toy MLP)
+        const uint4 r = Philox::gen(a.drop_seed, 0, doff + (unsigned long long)(off >> 2));
+        const int l = (int)(off & 3);
+        const uint32_t u = l == 0 ? r.x : (l == 1 ? r.y : (l == 2 ? r.z : r.w));
+        v = u32_to_unit(u) >= a.drop_p ? v * dscale : 0.f;
+      }
     } else if (a.act == 4) {
       v = a.aux_in[off] > 0.f ? v : 0.f;
     }

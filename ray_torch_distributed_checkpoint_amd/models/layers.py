@@ -13,9 +13,11 @@ from .. import ops
 class Linear(nn.Module):
     """y = act(x W^T + b); `relu=True` fuses the ReLU into the GEMM epilogue."""
 
-    def __init__(self, in_features: int, out_features: int, bias: bool = True, relu: bool = False):
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, relu: bool = False,
+                 dropout: float = 0.0):
         super().__init__()
         self.in_features, self.out_features, self.relu = in_features, out_features, relu
+        self.dropout = dropout  # inverted dropout after the ReLU, fused into the GEMM epilogue
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
         self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
         self.reset_parameters()
@@ -28,10 +30,13 @@ class Linear(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x, residual=None):
-        return ops.linear(x, self.weight, self.bias, relu=self.relu, residual=residual)
+        return ops.linear(x, self.weight, self.bias, relu=self.relu, residual=residual,
+                          dropout=self.dropout if self.training else 0.0)
 
     def extra_repr(self):
-        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}, fused_relu={self.relu}"
+        r = f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}, " \
+            f"fused_relu={self.relu}"
+        return r + (f", fused_dropout={self.dropout}" if self.dropout else "")
 
 
 class FusedReLU(nn.Module):
@@ -43,6 +48,21 @@ class FusedReLU(nn.Module):
 
     def extra_repr(self):
         return "fused into previous Linear"
+
+
+class FusedDropout(nn.Module):
+    """Placeholder keeping nn.Sequential indices of a Dropout fused into the preceding Linear's
+    epilogue (`Linear(..., relu=True, dropout=p)`)."""
+
+    def __init__(self, p: float = 0.5):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        return x
+
+    def extra_repr(self):
+        return f"p={self.p}, fused into previous Linear"
 
 
 class Dropout(nn.Module):

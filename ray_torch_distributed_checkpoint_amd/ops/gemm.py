@@ -130,7 +130,10 @@ def colsum(x2d: torch.Tensor, out=None, accumulate=False):
 
 
 def gemm_f32(A, B, C, M, N, K, sam, sak, sbk, sbn, ldc, *, Cin=None, bias=None, aux_in=None, aux_out=None,
-             alpha=1.0, beta=0.0, act=ACT_NONE):
+             alpha=1.0, beta=0.0, act=ACT_NONE, dropout=None):
+    """dropout: (p, seed, offset, device_base or None) - inverted dropout fused after the ReLU
+    epilogue, drawing the Philox stream exactly like the standalone dropout kernel."""
+    p, seed, offset, base = dropout if dropout is not None else (0.0, 0, 0, None)
     gpu_ext().gemm_f32(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, sam, sak, sbk, sbn, ldc, float(alpha),
-                       float(beta), act)
+                       float(beta), act, float(p), int(seed), int(offset), base)
     return C

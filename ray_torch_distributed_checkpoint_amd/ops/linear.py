@@ -21,10 +21,11 @@ from .gradbuf import grad_target
 from .shadow import shadow_of
 
 
-def _relu_mask_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-    """dx = dy * (y > 0) on the native elementwise kernel."""
+def _relu_mask_bwd(dy: torch.Tensor, y: torch.Tensor, p: float = 0.0) -> torch.Tensor:
+    """dx = dy * (y > 0) (/ (1 - p): the output of a fused ReLU + inverted dropout is positive
+    exactly where the unit was kept and active) on the native elementwise kernel."""
     dx = torch.empty_like(dy)
-    gpu_ext().relu_dropout(y, None, dy, dx, 0.0, 0, 0, True)
+    gpu_ext().relu_dropout(y, None, dy, dx, float(p), 0, 0, 2 if p > 0.0 else 1)
     return dx
 
 
@@ -64,14 +65,15 @@ class _LinearBF16(torch.autograd.Function):
 
 class _LinearF32(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, relu: bool):
+    def forward(ctx, x, w, b, relu: bool, drop=None):
         K = x.shape[-1]
         x2 = x.reshape(-1, K).contiguous()
         M, N = x2.shape[0], w.shape[0]
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
-        G.gemm_f32(x2, w, y, M, N, K, K, 1, 1, K, N, bias=b, act=G.ACT_RELU if relu else G.ACT_NONE)
+        G.gemm_f32(x2, w, y, M, N, K, K, 1, 1, K, N, bias=b, act=G.ACT_RELU if relu else G.ACT_NONE, dropout=drop)
         ctx.save_for_backward(x2, w, y if relu else None)
         ctx.relu = relu
+        ctx.p = drop[0] if drop is not None else 0.0
         ctx.has_b = b is not None
         ctx.in_shape = x.shape
         ctx.bias = b
@@ -83,7 +85,7 @@ class _LinearF32(torch.autograd.Function):
         N, K = w.shape
         M = x2.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
-        dpre = _relu_mask_bwd(dy2, y) if ctx.relu else dy2
+        dpre = _relu_mask_bwd(dy2, y, ctx.p) if ctx.relu else dy2
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
@@ -96,23 +98,46 @@ class _LinearF32(torch.autograd.Function):
             G.gemm_f32(dpre, x2, dw, N, K, M, 1, N, K, 1, K)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = G.colsum(dpre, out=grad_target(ctx.bias))
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, relu: bool = False,
-           residual: torch.Tensor | None = None) -> torch.Tensor:
+           residual: torch.Tensor | None = None, dropout: float = 0.0, stream=None) -> torch.Tensor:
+    """y = act(x w^T + b) (+ residual); dropout > 0 (training) applies inverted dropout after
+    the ReLU - fused into the fp32 GEMM's epilogue, the Philox stream `stream` (default:
+    ops.random.default_stream()) consumed exactly like a separate `ops.dropout` call."""
     if not x.is_cuda:
         y = F.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
         if relu:
             y = torch.relu(y)
+        if dropout > 0.0:
+            y = F.dropout(y, dropout, True)
         if residual is not None:
             y = y + residual
         return y
     if x.dtype == torch.float32:
+        drop = None
+        if dropout > 0.0 and relu and residual is None:
+            from .random import default_stream
+
+            st = stream or default_stream()
+            n = x.numel() // x.shape[-1] * w.shape[0]
+            seed, offset = st.reserve(n)
+            drop = (dropout, seed, offset, st.device_base())
+        y = _LinearF32.apply(x, w, b, relu, drop)
+        if dropout > 0.0 and drop is None:
+            from .dropout import dropout as _dropout
+
+            y = _dropout(y, dropout, True, stream)
+        return y + residual if residual is not None else y
+    y = _LinearBF16.apply(x, w, b, residual if dropout == 0.0 else None, relu)
+    if dropout > 0.0:
+        from .dropout import dropout as _dropout
+
+        y = _dropout(y, dropout, True, stream)
         if residual is not None:
-            return _LinearF32.apply(x, w, b, relu) + residual
-        return _LinearF32.apply(x, w, b, relu)
-    return _LinearBF16.apply(x, w, b, residual, relu)
+            y = y + residual
+    return y
 
 
 class _FusedMLP(torch.autograd.Function):

@@ -550,3 +550,33 @@ def test_flash_attention_deterministic():
         causal_attention(qkv, 4).backward(g)
         grads.append(qkv.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("M,K,N,p", [(16, 784, 512, 0.25), (16, 512, 512, 0.25), (37, 100, 130, 0.5)])
+def test_fp32_linear_fused_dropout_equals_separate_kernel(M, K, N, p):
+    """Linear + ReLU + Dropout as one fp32 GEMM (Philox mask in the epilogue) == the GEMM with
+    the ReLU epilogue followed by the standalone dropout kernel on the same Philox stream -
+    bitwise, forward and all three gradients (the fused backward reads the mask off the output)."""
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.ops.random import PhiloxStream
+
+    torch.manual_seed(M + K)
+    x0 = torch.randn(M, K, device="cuda")
+    w0 = torch.randn(N, K, device="cuda") * 0.05
+    b0 = torch.randn(N, device="cuda") * 0.1
+    dy = torch.randn(M, N, device="cuda")
+
+    def run(fused):
+        x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+        st = PhiloxStream(seed=1234, offset=77)
+        if fused:
+            y = ops.linear(x, w, b, relu=True, dropout=p, stream=st)
+        else:
+            y = ops.dropout(ops.linear(x, w, b, relu=True), p, True, st)
+        y.backward(dy)
+        return y.detach(), x.grad, w.grad, b.grad
+
+    a, r = run(True), run(False)
+    for u, v in zip(a, r):
+        assert torch.equal(u, v)
+    assert (a[0] == 0).float().mean().item() > p * 0.5  # really dropped
