@@ -27,7 +27,7 @@ def _side_stream(device) -> torch.cuda.Stream:
 
 class _Embedding(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, idx, wte, wpe):
+    def forward(ctx, idx, wte, wpe, presort=True):
         B, T = idx.shape
         D = wte.shape[1]
         idx_c = idx.contiguous()
@@ -35,16 +35,18 @@ class _Embedding(torch.autograd.Function):
         gpu_ext().embed_fwd(idx_c, shadow_of(wte), shadow_of(wpe) if wpe is not None else None, out, T)
         # the backward's stable sort of the token ids depends only on idx: run it now on a side
         # stream, concurrently with the forward pass, instead of on the backward's critical path
-        cur = torch.cuda.current_stream(idx.device)
-        side = _side_stream(idx.device)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            sidx, perm = torch.sort(idx_c.reshape(-1), stable=True)
-            done = torch.cuda.Event()
-            done.record(side)
-        sidx.record_stream(cur)
-        perm.record_stream(cur)
-        ctx.sorted = (sidx, perm, done)
+        ctx.sorted = None
+        if presort:
+            cur = torch.cuda.current_stream(idx.device)
+            side = _side_stream(idx.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                sidx, perm = torch.sort(idx_c.reshape(-1), stable=True)
+                done = torch.cuda.Event()
+                done.record(side)
+            sidx.record_stream(cur)
+            perm.record_stream(cur)
+            ctx.sorted = (sidx, perm, done)
         ctx.save_for_backward(idx_c)
         ctx.shapes = (wte.shape, None if wpe is None else wpe.shape)
         ctx.params = (wte, wpe)
@@ -71,10 +73,13 @@ class _Embedding(torch.autograd.Function):
                 dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device)
             elif T < wpe_shape[0]:
                 dwpe[T:].zero_()  # the kernel writes (not adds) positions [0, T)
-        sidx, perm, done = ctx.sorted
-        torch.cuda.current_stream(idx.device).wait_event(done)
+        if ctx.sorted is not None:
+            sidx, perm, done = ctx.sorted
+            torch.cuda.current_stream(idx.device).wait_event(done)
+        else:
+            sidx, perm = torch.sort(idx.reshape(-1), stable=True)
         gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)
-        return None, (None if accumulate else dwte), dwpe
+        return None, (None if accumulate else dwte), dwpe, None
 
 
 def embedding(idx: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor | None = None,
@@ -84,4 +89,5 @@ def embedding(idx: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor | None = N
         if wpe is not None:
             x = x + wpe[: idx.shape[1]].unsqueeze(0)
         return x
-    return _Embedding.apply(idx, wte, wpe)
+    # the backward's token sort is prepared during the forward only when a backward can follow
+    return _Embedding.apply(idx, wte, wpe, torch.is_grad_enabled() and wte.requires_grad)
