@@ -14,7 +14,9 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext  # noqa: E402
 from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention  # noqa: E402
 
 SHAPES = [("gpt2", 16, 1024, 12, 12, 64), ("llama8b", 1, 2048, 32, 8, 128), ("llama8b_b4", 4, 2048, 32, 8, 128)]
@@ -38,6 +40,9 @@ def main():
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
     torch.manual_seed(0)
+    from gemm_bench import warm_up_clocks
+
+    warm_up_clocks()
     for name, B, T, H, Hkv, Dh in SHAPES:
         if args.only and name != args.only:
             continue
@@ -53,6 +58,20 @@ def main():
             out.backward(dy)
 
         t_fb = min(timeit(fb, args.reps) for _ in range(3))
+        # the kernels alone (what a training step pays; the autograd round trip above adds host
+        # overhead the GPU can wait on in an isolated loop): flash_fwd, flash_bwd (dQ + dK/dV)
+        ext = gpu_ext()
+        scale = Dh ** -0.5
+        q_ = qkv.detach()
+        o_ = torch.empty((B, T, H * Dh), dtype=torch.bfloat16, device="cuda")
+        lse = torch.empty((B * H, T), dtype=torch.float32, device="cuda")
+        ext.flash_fwd(q_, o_, lse, B, T, H, Hkv, Dh, scale)
+        dqkv = torch.empty_like(q_)
+        delta = torch.empty((B * H, T), dtype=torch.float32, device="cuda")
+        dyc = dy.contiguous()
+        t_kf = min(timeit(lambda: ext.flash_fwd(q_, o_, lse, B, T, H, Hkv, Dh, scale), args.reps) for _ in range(3))
+        t_kb = min(timeit(lambda: ext.flash_bwd(q_, o_, dyc, lse, delta, dqkv, B, T, H, Hkv, Dh, scale), args.reps)
+                   for _ in range(3))
         q = qkv.detach()[..., : H * Dh].view(B, T, H, Dh).transpose(1, 2).contiguous().requires_grad_(True)
         k = qkv.detach()[..., H * Dh:(H + Hkv) * Dh].view(B, T, Hkv, Dh).transpose(1, 2)
         v = qkv.detach()[..., (H + Hkv) * Dh:].view(B, T, Hkv, Dh).transpose(1, 2)
@@ -69,6 +88,9 @@ def main():
                           "fwd_us": round(t_f * 1e6, 1), "fwd_TF": round(flops_f / t_f / 1e12, 1),
                           "bwd_us": round((t_fb - t_f) * 1e6, 1),
                           "bwd_TF": round(2.5 * flops_f / (t_fb - t_f) / 1e12, 1),
+                          "kernel_fwd_us": round(t_kf * 1e6, 1), "kernel_fwd_TF": round(flops_f / t_kf / 1e12, 1),
+                          "kernel_bwd_us": round(t_kb * 1e6, 1),
+                          "kernel_bwd_TF": round(2.5 * flops_f / t_kb / 1e12, 1),
                           "sdpa_fwd_us": round(t_sf * 1e6, 1), "sdpa_fwd_TF": round(flops_f / t_sf / 1e12, 1),
                           "sdpa_bwd_us": round((t_sfb - t_sf) * 1e6, 1)}), flush=True)
 
