@@ -76,8 +76,8 @@ int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rst
                 long long* nbt, hipStream_t st);
 int rtdc_conv_w_flip_t(const void* w, void* out, int Cout, int KH, int KW, int C, hipStream_t st);
 int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
-                void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu, float* ws, int nblk,
-                hipStream_t st);
+                const float* beta, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu,
+                float* ws, int nblk, hipStream_t st);
 int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, int B, int H, int W, int C, int Ho, int Wo,
                  int K, int s, int p, int backward, hipStream_t st);
 int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st);
@@ -477,14 +477,21 @@ static void conv_w_flip_t(Tensor w, Tensor out, int64_t KH, int64_t KW) {
   check_rc(rtdc_conv_w_flip_t(w.data_ptr(), out.data_ptr(), (int)Cout, (int)KH, (int)KW, (int)C, cur_stream()),
            "conv_w_flip_t");
 }
-static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor dx,
-                   c10::optional<Tensor> dres, Tensor dgamma, Tensor dbeta, bool relu, Tensor ws, int64_t nblk) {
+// relu: 0 none, 1 ReLU mask from y (> 0), 2 ReLU mask recomputed from x with gamma / beta (the
+// forward had no residual; y is not read)
+static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, c10::optional<Tensor> beta,
+                   Tensor dx, c10::optional<Tensor> dres, Tensor dgamma, Tensor dbeta, int64_t relu, Tensor ws,
+                   int64_t nblk) {
   const int64_t C = x.size(-1), N = x.numel() / C;
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dx.is_contiguous(), "bn_bwd: contiguous tensors expected");
   TORCH_CHECK(ws.numel() >= 2 * nblk * C, "bn_bwd: workspace too small");
+  TORCH_CHECK(relu >= 0 && relu <= 2, "bn_bwd: relu mode 0/1/2");
+  TORCH_CHECK(relu != 2 || (beta.has_value() && beta->scalar_type() == at::kFloat && beta->numel() == C),
+              "bn_bwd: relu mode 2 needs the fp32 beta");
   check_rc(rtdc_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                       gamma.data_ptr<float>(), dx.data_ptr(), ptr_or_null(dres), dgamma.data_ptr<float>(),
-                       dbeta.data_ptr<float>(), N, (int)C, relu, ws.data_ptr<float>(), (int)nblk, cur_stream()),
+                       gamma.data_ptr<float>(), relu == 2 ? beta->data_ptr<float>() : nullptr, dx.data_ptr(),
+                       ptr_or_null(dres), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), N, (int)C, (int)relu,
+                       ws.data_ptr<float>(), (int)nblk, cur_stream()),
            "bn_bwd");
 }
 // mean cross-entropy from per-row losses: out[0] = loss, out[1] = divisor (device count of

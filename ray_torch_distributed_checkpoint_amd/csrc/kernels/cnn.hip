@@ -209,10 +209,15 @@ __device__ __forceinline__ void ld8f(const bf16_t* p, float* v) {
 
 // mode 0 (forward): a = x            -> out0 = pivot + s1/n (block mean), out1 = M2
 // mode 1 (backward): a = dy, b = y (relu mask, may be null), c = x -> out0 = sum g, out1 = sum g*xhat
+//   with gamma/beta set (ReLU without a residual): the mask is recomputed from x as the forward
+//   computed it, t = fma(x, rstd*gamma, beta - mean*rstd*gamma) > 0 - no pass over y
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ yb,
                                                        const bf16_t* __restrict__ xb, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, long long N, int C, int R,
-                                                       int mode, float* __restrict__ out0, float* __restrict__ out1) {
+                                                       int mode, float* __restrict__ out0, float* __restrict__ out1,
+                                                       const float* __restrict__ gamma = nullptr,
+                                                       const float* __restrict__ beta = nullptr) {
+  const bool mx = gamma != nullptr;  // relu mask from x
   __shared__ float red[2][256][8];
   const long long r0 = (long long)blockIdx.x * R;
   const long long r1 = min(N, r0 + R);
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     const int lane = t / chunk, gi = t % chunk;
     const int c = (gbase + gi) * 8;
     float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float piv[8], m8[8], r8[8];
+    float piv[8], m8[8], r8[8], ka[8], kb[8];
     if (lane < rl && n > 0) {
       if (mode == 0) {
         ld8f(a + r0 * C + c, piv);
@@ -234,6 +239,10 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
         for (int e = 0; e < 8; ++e) {
           m8[e] = mean[c + e];
           r8[e] = rstd[c + e];
+          if (mx) {
+            ka[e] = rstd[c + e] * gamma[c + e];
+            kb[e] = beta[c + e] - mean[c + e] * ka[e];
+          }
         }
       }
       // U rows per iteration with every load issued before any use: 3U 16-B loads in flight
@@ -271,6 +280,9 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
               unpack8(vy[u], yv);
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] = yv[e] > 0.f ? v[e] : 0.f;
+            } else if (mx) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = fmaf(xv[e], ka[e], kb[e]) > 0.f ? v[e] : 0.f;
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -298,6 +310,9 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
             ld8f(yb + r * C + c, yv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = yv[e] > 0.f ? v[e] : 0.f;
+          } else if (mx) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaf(xv[e], ka[e], kb[e]) > 0.f ? v[e] : 0.f;
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -440,7 +455,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     if (res) unpack8(*(const uint4*)(res + off), rr);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float t = (xv[e] - mean[c + e]) * rstd[c + e] * gamma[c + e] + beta[c + e];
+      // the fast path's coefficients exactly (a backward may recompute the ReLU mask from x)
+      const float ka = rstd[c + e] * gamma[c + e], kb = beta[c + e] - mean[c + e] * ka;
+      float t = fmaf(xv[e], ka, kb);
       if (res) t += rr[e];
       if (relu) t = fmaxf(t, 0.f);
       o[e] = t;
@@ -470,18 +487,23 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __rest
 // dx = gamma*rstd*(g - dbeta/N - xhat*dgamma/N) = A*g + B*x + D per channel (g: dy masked by
 // y > 0 when the forward fused a ReLU); dres = g.  Coefficients hoisted per thread as in
 // bn_apply_kernel.
+template <int RELU>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                           const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                           const float* __restrict__ dbeta, const float* __restrict__ dgamma,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long N,
-                                                          int C, int relu) {
+                                                          int C, const float* __restrict__ beta) {
+  // RELU: 0 none, 1 mask y > 0 (y read), 2 mask recomputed from x (ReLU without a residual:
+  // t = fma(x, rstd*gamma, beta - mean*rstd*gamma) as bn_apply_kernel computed it; y not read).
+  // A compile-time mode: with a runtime one hipcc re-loaded the per-channel coefficients inside
+  // the loop (3-6x slower).
   const int cg = C / 8;
   const long long total = N * cg;
   const float invN = 1.f / (float)N;
   const long long i0 = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
   const bool hoist = stride % cg == 0;
-  float kA[8], kB[8], kD[8];
+  float kA[8], kB[8], kD[8], ka[8], kb[8];
   auto coef = [&](int c) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -489,6 +511,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
       kA[e] = gr;
       kB[e] = -gr * r * dgamma[c + e] * invN;
       kD[e] = -gr * dbeta[c + e] * invN - kB[e] * mean[c + e];
+      if constexpr (RELU == 2) {
+        ka[e] = rstd[c + e] * gamma[c + e];
+        kb[e] = beta[c + e] - mean[c + e] * ka[e];
+      }
     }
   };
   if (hoist) coef((int)(i0 % cg) * 8);
@@ -497,15 +523,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     const size_t off = (size_t)i * 8;
     const uint4 g4 = *(const uint4*)(dy + off), x4 = *(const uint4*)(x + off);
     uint4 y4 = g4;
-    if (relu) y4 = *(const uint4*)(y + off);
+    if constexpr (RELU == 1) y4 = *(const uint4*)(y + off);
     float gv[8], xv[8], o[8];
     unpack8(g4, gv);
     unpack8(x4, xv);
-    if (relu) {
+    if constexpr (RELU == 1) {
       float yv[8];
       unpack8(y4, yv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
+    } else if constexpr (RELU == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = fmaf(xv[e], ka[e], kb[e]) > 0.f ? gv[e] : 0.f;
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = fmaf(kA[e], gv[e], fmaf(kB[e], xv[e], kD[e]));
@@ -755,19 +784,26 @@ extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean,
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// relu: 0 none, 1 mask from y, 2 mask recomputed from x (needs beta; y unused)
 extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd,
-                           const float* gamma, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C,
-                           int relu, float* ws, int nblk, hipStream_t st) {
+                           const float* gamma, const float* beta, void* dx, void* dres, float* dgamma, float* dbeta,
+                           long long N, int C, int relu, float* ws, int nblk, hipStream_t st) {
   const int R = (int)((N + nblk - 1) / nblk);
-  if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
+  if (C % 8 != 0 || N * C >= (1LL << 31) || relu < 0 || relu > 2 || (relu == 2 && !beta)) return 1;
   hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)(relu ? y : nullptr), (const bf16_t*)x, mean, rstd, N, C, R, 1, ws,
-                     ws + (long long)nblk * C);
+                     (const bf16_t*)(relu == 1 ? y : nullptr), (const bf16_t*)x, mean, rstd, N, C, R, 1, ws,
+                     ws + (long long)nblk * C, relu == 2 ? gamma : (const float*)nullptr,
+                     relu == 2 ? beta : (const float*)nullptr);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
                      (const float*)(ws + (long long)nblk * C), nblk, C, dbeta, dgamma);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
-                     (const bf16_t*)x, mean, rstd, gamma, (const float*)dbeta, (const float*)dgamma, (bf16_t*)dx,
-                     (bf16_t*)dres, N, C, relu);
+#define BWA(R)                                                                                          \
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<R>, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)dy, \
+                     (const bf16_t*)y, (const bf16_t*)x, mean, rstd, gamma, (const float*)dbeta,           \
+                     (const float*)dgamma, (bf16_t*)dx, (bf16_t*)dres, N, C, beta)
+  if (relu == 2) BWA(2);
+  else if (relu == 1) BWA(1);
+  else BWA(0);
+#undef BWA
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

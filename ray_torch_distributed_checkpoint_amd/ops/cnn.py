@@ -22,6 +22,8 @@ CPU tensors run the PyTorch reference of every op (NHWC in, NHWC out).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -294,6 +296,9 @@ def _bn_blocks(N: int, C: int) -> int:
     return max(1, min(2048, (N * C) // (256 * 8 * 32)))
 
 
+_BN_MASK_FROM_X = os.environ.get("RTDC_BN_MASK_FROM_X", "1") != "0"
+
+
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
@@ -321,9 +326,11 @@ class _BatchNorm(torch.autograd.Function):
         gpu_ext().bn_fwd(x, res, y, mean, rstd, weight, bias, running_mean if training else None,
                          running_var if training else None, eps, momentum, training, relu, ws, nblk, pmean, pm2,
                          p_rows, num_batches_tracked if training else None)
-        ctx.save_for_backward(x, y if relu else None, mean, rstd, weight)
+        # ReLU mask in the backward: recomputed from x (mode 2, no pass over y) unless a
+        # residual was added before the ReLU (mode 1: y > 0)
+        ctx.relu = 0 if not relu else (1 if residual is not None or not _BN_MASK_FROM_X else 2)
+        ctx.save_for_backward(x, y if ctx.relu == 1 else None, mean, rstd, weight)
         ctx.params = (weight, bias)
-        ctx.relu = relu
         ctx.has_res = residual is not None
         return y
 
@@ -343,7 +350,8 @@ class _BatchNorm(torch.autograd.Function):
             dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
-        gpu_ext().bn_bwd(dy, y if ctx.relu else x, x, mean, rstd, weight, dx, dres, dgamma, dbeta, ctx.relu, ws, nblk)
+        gpu_ext().bn_bwd(dy, y if ctx.relu == 1 else x, x, mean, rstd, weight, b if ctx.relu == 2 else None, dx,
+                         dres, dgamma, dbeta, ctx.relu, ws, nblk)
         if dres is not None and ctx.res_stash is not None:
             # the shortcut's gradient: normally added by the block's convolution(s) of the same
             # input inside their dgrad kernels
