@@ -75,6 +75,9 @@ int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rst
                 int relu, float* ws, int nblk, const float* pmean, const float* pm2, int p_nblk, int p_R,
                 long long* nbt, hipStream_t st);
 int rtdc_conv_w_flip_t(const void* w, void* out, int Cout, int KH, int KW, int C, hipStream_t st);
+int rtdc_bn_relu_maxpool(const void* x, void* y, void* arg, const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, int B, int H, int W, int C, int Ho, int Wo, int K, int s, int p,
+                         hipStream_t st);
 int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
                 const float* beta, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu,
                 float* ws, int nblk, hipStream_t st);
@@ -444,7 +447,8 @@ static void col2im(Tensor dcols, Tensor dx, int64_t Ho, int64_t Wo, int64_t KH, 
                        (int)KW, (int)stride, (int)pad, (int)K, (int)Kp, cur_stream()),
            "col2im");
 }
-static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta,
+static void bn_fwd(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> y, Tensor mean, Tensor rstd,
+                   Tensor gamma, Tensor beta,
                    c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var, double eps, double momentum,
                    bool training, bool relu, Tensor ws, int64_t nblk, c10::optional<Tensor> pmean,
                    c10::optional<Tensor> pm2, int64_t p_R, c10::optional<Tensor> num_batches_tracked) {
@@ -453,9 +457,9 @@ static void bn_fwd(Tensor x, c10::optional<Tensor> res, Tensor y, Tensor mean, T
                     num_batches_tracked->numel() == 1,
                 "bn_fwd: num_batches_tracked must be a 1-element int64 GPU tensor");
   const int64_t C = x.size(-1), N = x.numel() / C;
-  TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "bn_fwd: contiguous tensors expected");
+  TORCH_CHECK(x.is_contiguous() && (!y.has_value() || y->is_contiguous()), "bn_fwd: contiguous tensors expected");
   TORCH_CHECK(!training || ws.numel() >= 2 * nblk * C, "bn_fwd: workspace too small");
-  check_rc(rtdc_bn_fwd(x.data_ptr(), ptr_or_null(res), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+  check_rc(rtdc_bn_fwd(x.data_ptr(), ptr_or_null(res), ptr_or_null(y), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), beta.data_ptr<float>(),
                        running_mean.has_value() ? running_mean->data_ptr<float>() : nullptr,
                        running_var.has_value() ? running_var->data_ptr<float>() : nullptr, N, (int)C, (float)eps,
@@ -479,6 +483,22 @@ static void conv_w_flip_t(Tensor w, Tensor out, int64_t KH, int64_t KW) {
 }
 // relu: 0 none, 1 ReLU mask from y (> 0), 2 ReLU mask recomputed from x with gamma / beta (the
 // forward had no residual; y is not read)
+// y [B,Ho,Wo,C] = maxpool(relu(BN(x))) with mean / rstd from bn_fwd (y = None), arg = argmax tap
+static void bn_relu_maxpool(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, Tensor y, Tensor arg,
+                            int64_t K, int64_t s, int64_t p) {
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous() && arg.is_contiguous() &&
+                  x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
+                  arg.scalar_type() == at::kByte && arg.sizes() == y.sizes(),
+              "bn_relu_maxpool: contiguous bf16 NHWC x / y, uint8 arg shaped like y");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && rstd.scalar_type() == at::kFloat && gamma.scalar_type() == at::kFloat &&
+                  beta.scalar_type() == at::kFloat && mean.numel() == x.size(3) && gamma.numel() == x.size(3),
+              "bn_relu_maxpool: fp32 per-channel statistics / affine");
+  check_rc(rtdc_bn_relu_maxpool(x.data_ptr(), y.data_ptr(), arg.data_ptr(), mean.data_ptr<float>(),
+                                rstd.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(), (int)x.size(0),
+                                (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)K,
+                                (int)s, (int)p, cur_stream()),
+           "bn_relu_maxpool");
+}
 static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, c10::optional<Tensor> beta,
                    Tensor dx, c10::optional<Tensor> dres, Tensor dgamma, Tensor dbeta, int64_t relu, Tensor ws,
                    int64_t nblk) {
@@ -702,6 +722,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("col2im", &col2im);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("bn_relu_maxpool", &bn_relu_maxpool);
   m.def("conv_w_flip_t", &conv_w_flip_t);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("xent_finalize", &xent_finalize);

@@ -586,6 +586,65 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
   }
 }
 
+// ResNet stem: y = maxpool_KxK/s(relu(BN(x))) with the per-tap argmax, straight from the
+// convolution output x - the full-resolution BN output (4x the pooled size) is never stored.
+// Each window element is rounded to bf16 exactly as bn_apply_kernel stores it and compared as
+// maxpool_fwd_kernel compares it (first strict maximum in (kh, kw) order), so y and arg are
+// bitwise those of the unfused pair; the backward recomputes the ReLU mask from x.
+// A thread keeps one 8-channel group for the whole grid-stride loop (stride % (C/8) == 0,
+// checked by the launcher), so the BN coefficients are computed once per thread.
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                             uint8_t* __restrict__ arg, const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int B, int H, int W, int C,
+                                                             int Ho, int Wo, int K, int s, int p) {
+  const int cg = C / 8;
+  const int total = B * Ho * Wo * cg;
+  const int i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  const int c = (i0 % cg) * 8;
+  float ka[8], kb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ka[e] = rstd[c + e] * gamma[c + e];
+    kb[e] = beta[c + e] - mean[c + e] * ka[e];
+  }
+  for (int i = i0; i < total; i += stride) {
+    const int pix = i / cg;
+    const int q = pix / Wo, wo = pix - q * Wo;
+    const int b = q / Ho, ho = q - b * Ho;
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      bi[e] = 0;
+    }
+    for (int kh = 0; kh < K; ++kh) {
+      const int h = ho * s - p + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int w = wo * s - p + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float v[8];
+        unpack8(*(const uint4*)(x + ((size_t)(b * H + h) * W + w) * C + c), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = bf2f(f2bf(fmaxf(fmaf(v[e], ka[e], kb[e]), 0.f)));
+          if (t > best[e]) {
+            best[e] = t;
+            bi[e] = kh * K + kw;
+          }
+        }
+      }
+    }
+    const size_t o = (size_t)pix * C + c;
+    *(uint4*)(y + o) = pack8(best);
+    *(uint2*)(arg + o) = make_uint2(bi[0] | bi[1] << 8 | bi[2] << 16 | bi[3] << 24,
+                                    bi[4] | bi[5] << 8 | bi[6] << 16 | bi[7] << 24);
+  }
+}
+
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                          bf16_t* __restrict__ dx, int B, int H, int W, int C, int Ho,
                                                          int Wo, int K, int s, int p) {
@@ -779,8 +838,19 @@ extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean,
                        (const float*)(ws + (long long)nblk * C), nblk, N, R, C, eps, momentum, mean, rstd, running_mean,
                        running_var, nbt);
   }
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)res,
-                     (bf16_t*)y, (const float*)mean, (const float*)rstd, gamma, beta, N, C, relu);
+  if (y)  // (y null: statistics only - the consumer applies the normalisation itself)
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)res, (bf16_t*)y, (const float*)mean, (const float*)rstd, gamma, beta, N, C, relu);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_bn_relu_maxpool(const void* x, void* y, void* arg, const float* mean, const float* rstd,
+                                    const float* gamma, const float* beta, int B, int H, int W, int C, int Ho, int Wo,
+                                    int K, int s, int p, hipStream_t st) {
+  const int cg = C / 8;
+  if (C % 8 != 0 || 256 % cg != 0 || K * K > 255 || (long long)B * H * W * C >= (1LL << 31)) return 1;
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(gsz((long long)B * Ho * Wo * cg)), dim3(256), 0, st,
+                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, mean, rstd, gamma, beta, B, H, W, C, Ho, Wo, K, s, p);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

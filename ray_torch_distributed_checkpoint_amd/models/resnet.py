@@ -43,6 +43,12 @@ class BatchNorm2d(nn.Module):
                               self.momentum, self.eps, residual=residual, relu=relu,
                               num_batches_tracked=self.num_batches_tracked, residual_grad_to=residual_grad_to)
 
+    def relu_max_pool(self, x, k: int = 3, s: int = 2, p: int = 1):
+        """max_pool2d(relu(self(x))) in one pass (the stem; the BN output is never stored)."""
+        return cnn.batch_norm_relu_max_pool(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                            self.training, self.momentum, self.eps,
+                                            num_batches_tracked=self.num_batches_tracked, k=k, s=s, p=p)
+
     def extra_repr(self):
         return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, layout=NHWC"
 
@@ -123,8 +129,7 @@ class ResNet18(nn.Module):
             h = cnn.to_nhwc_bf16(x)
         else:
             h = x.permute(0, 2, 3, 1).float().contiguous()
-        h = self.bn1(self.conv1(h), relu=True)
-        h = cnn.max_pool2d(h, 3, 2, 1)
+        h = self.bn1.relu_max_pool(self.conv1(h), 3, 2, 1)
         h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
         return self.fc(cnn.global_avg_pool(h))
 

@@ -388,6 +388,75 @@ def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, trainin
                             num_batches_tracked, residual_grad_to)
 
 
+class _BNReluMaxPool(torch.autograd.Function):
+    """maxpool(relu(BN(x))) for the ResNet stem without storing the full-resolution BN output:
+    bn_fwd computes the statistics only, one kernel normalises + rectifies + pools; the
+    backward scatters through the argmax and runs the BN backward with the ReLU mask
+    recomputed from x."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, num_batches_tracked, k, s,
+                p):
+        B, H, W, C = x.shape
+        x = x.contiguous()
+        N = x.numel() // C
+        pmean = pm2 = None
+        p_rows = 0
+        if training:
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+            nblk = _bn_blocks(N, C)
+            ws = G.workspace(x.device, 2 * nblk * C, "bn")
+            st = getattr(x, "_rtdc_bn_stats", None)
+            if st is not None and st[0].shape[1] == C and st[0].shape[0] == (N + st[2] - 1) // st[2]:
+                pmean, pm2, p_rows = st
+            gpu_ext().bn_fwd(x, None, None, mean, rstd, weight, bias, running_mean, running_var, eps, momentum, True,
+                             True, ws, nblk, pmean, pm2, p_rows, num_batches_tracked)
+        else:
+            mean = running_mean.float()
+            rstd = torch.rsqrt(running_var.float() + eps)
+        Ho, Wo = _out_hw(H, W, k, k, s, p)
+        y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        gpu_ext().bn_relu_maxpool(x, mean, rstd, weight, bias, y, arg, k, s, p)
+        ctx.save_for_backward(x, mean, rstd, weight, arg)
+        ctx.params = (weight, bias)
+        ctx.pool = (k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, weight, arg = ctx.saved_tensors
+        k, s, p = ctx.pool
+        C = x.shape[-1]
+        N = x.numel() // C
+        dz = torch.empty_like(x)  # gradient at the (never stored) BN output
+        gpu_ext().maxpool_bwd(dy.contiguous(), arg, dz, k, s, p)
+        dx = torch.empty_like(x)
+        w, b = ctx.params
+        dgamma, dbeta = grad_target(w), grad_target(b)
+        if dgamma is None:
+            dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        if dbeta is None:
+            dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        nblk = _bn_blocks(N, C)
+        ws = G.workspace(x.device, 2 * nblk * C, "bn")
+        gpu_ext().bn_bwd(dz, x, x, mean, rstd, weight, b, dx, None, dgamma, dbeta, 2, ws, nblk)
+        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+
+
+def batch_norm_relu_max_pool(x, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
+                             eps: float = 1e-5, num_batches_tracked=None, k: int = 3, s: int = 2, p: int = 1):
+    """max_pool2d(relu(batch_norm(x)), k, s, p) over NHWC; one fused pass on the GPU."""
+    if not x.is_cuda:
+        y = batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=True,
+                       num_batches_tracked=num_batches_tracked)
+        return max_pool2d(y, k, s, p)
+    require_dtype(x, "batch_norm_relu_max_pool")
+    return _BNReluMaxPool.apply(x, weight, bias, running_mean, running_var, training, momentum, eps,
+                                num_batches_tracked if training else None, k, s, p)
+
+
 class _MaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, p):

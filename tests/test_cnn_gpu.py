@@ -116,6 +116,48 @@ def test_batch_norm_eval_and_determinism():
     _close(y, ref, 0.02, "eval")
 
 
+@pytest.mark.parametrize("hw,stats", [(56, True), (28, False), (27, True)])
+def test_stem_bn_relu_maxpool_equals_unfused(hw, stats):
+    """The stem's one-pass BN + ReLU + 3x3/2 max-pool == batch_norm(relu) then max_pool2d,
+    bitwise: output, running statistics and every gradient (x, gamma, beta) - including with
+    the BatchNorm statistics handed over by a convolution epilogue."""
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(hw)
+    C = 64
+    if stats:
+        x0 = (torch.randn(4, hw, hw, C, device=DEV) + 0.3).bfloat16()
+        w = (torch.randn(C, C, 3, 3, device=DEV) * 0.05).requires_grad_(True)
+        y0 = cnn.conv2d(x0, w, 1, 1, bn_stats=True)
+        x = y0.detach()
+        x._rtdc_bn_stats = y0._rtdc_bn_stats
+    else:
+        x = (torch.randn(4, hw, hw, C, device=DEV) * 2 - 0.5).bfloat16()
+    g0 = torch.randn(C, device=DEV)  # negative gammas too: the window max is not a monotone map
+    b0 = torch.randn(C, device=DEV) * 0.5
+    outs = []
+    for fused in (False, True):
+        g, b = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        xi = x.detach().clone().requires_grad_(True)
+        if stats:
+            xi._rtdc_bn_stats = x._rtdc_bn_stats
+        if fused:
+            y = cnn.batch_norm_relu_max_pool(xi, g, b, rm, rv, True, 0.1, 1e-5)
+        else:
+            y = cnn.max_pool2d(cnn.batch_norm(xi, g, b, rm, rv, True, 0.1, 1e-5, relu=True), 3, 2, 1)
+        gy = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1)).bfloat16()
+        y.backward(gy)
+        outs.append((y, rm, rv, xi.grad, g.grad, b.grad))
+    names = ("y", "running_mean", "running_var", "dx", "dgamma", "dbeta")
+    for n, a, b in zip(names, outs[0], outs[1]):
+        assert torch.equal(a, b), f"{n} differs between the fused and the unfused stem"
+    # and against fp32 torch
+    xr = x.float().requires_grad_(True)
+    ref = F.max_pool2d(torch.relu(F.batch_norm(xr.permute(0, 3, 1, 2), None, None, g0, b0, True)), 3, 2, 1)
+    _close(outs[1][0], _nhwc(ref), 0.02, "y vs torch")
+
+
 def test_pools_and_classifier():
     from ray_torch_distributed_checkpoint_amd.ops import cnn
 
