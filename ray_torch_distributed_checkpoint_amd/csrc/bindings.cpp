@@ -75,6 +75,9 @@ int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rst
                 int relu, float* ws, int nblk, const float* pmean, const float* pm2, int p_nblk, int p_R,
                 long long* nbt, hipStream_t st);
 int rtdc_conv_w_flip_t(const void* w, void* out, int Cout, int KH, int KW, int C, hipStream_t st);
+int rtdc_stem_s2d(const float* x, void* y, int B, int H, int W, hipStream_t st);
+int rtdc_stem_w_s2d(const void* w, void* wp, int Cout, hipStream_t st);
+int rtdc_stem_dw_s2d(const float* dwp, float* dw, int Cout, hipStream_t st);
 int rtdc_bn_relu_maxpool(const void* x, void* y, void* arg, const float* mean, const float* rstd, const float* gamma,
                          const float* beta, int B, int H, int W, int C, int Ho, int Wo, int K, int s, int p,
                          hipStream_t st);
@@ -483,6 +486,33 @@ static void conv_w_flip_t(Tensor w, Tensor out, int64_t KH, int64_t KW) {
 }
 // relu: 0 none, 1 ReLU mask from y (> 0), 2 ReLU mask recomputed from x with gamma / beta (the
 // forward had no residual; y is not read)
+// ResNet stem as a space-to-depth convolution (cnn.hip): NCHW fp32 image -> [B, H/2, W/2, 16]
+// bf16; channels-last bf16 7x7x3 weight [Cout, 147] -> [Cout, 256]; gradient [Cout, 256] fp32 ->
+// [Cout, 147] fp32
+static void stem_s2d(Tensor x, Tensor y) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(1) == 3,
+              "stem_s2d: contiguous fp32 NCHW 3-channel images");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 4 && y.size(0) == x.size(0) &&
+                  y.size(1) * 2 == x.size(2) && y.size(2) * 2 == x.size(3) && y.size(3) == 16,
+              "stem_s2d: y must be [B, H/2, W/2, 16] bf16");
+  check_rc(rtdc_stem_s2d(x.data_ptr<float>(), y.data_ptr(), (int)x.size(0), (int)x.size(2), (int)x.size(3),
+                         cur_stream()),
+           "stem_s2d");
+}
+static void stem_w_s2d(Tensor w, Tensor wp) {
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == w.size(0) * 147 &&
+                  wp.scalar_type() == at::kBFloat16 && wp.is_contiguous() && wp.numel() == w.size(0) * 256,
+              "stem_w_s2d: bf16 [Cout, 7*7*3] -> bf16 [Cout, 256]");
+  check_rc(rtdc_stem_w_s2d(w.data_ptr(), wp.data_ptr(), (int)w.size(0), cur_stream()), "stem_w_s2d");
+}
+static void stem_dw_s2d(Tensor dwp, Tensor dw) {
+  TORCH_CHECK(dwp.scalar_type() == at::kFloat && dwp.is_contiguous() && dw.scalar_type() == at::kFloat &&
+                  dw.is_contiguous() && dwp.numel() == dwp.size(0) * 256 && dw.numel() == dwp.size(0) * 147,
+              "stem_dw_s2d: fp32 [Cout, 256] -> fp32 [Cout, 147]");
+  check_rc(rtdc_stem_dw_s2d(dwp.data_ptr<float>(), dw.data_ptr<float>(), (int)dwp.size(0), cur_stream()),
+           "stem_dw_s2d");
+}
 // y [B,Ho,Wo,C] = maxpool(relu(BN(x))) with mean / rstd from bn_fwd (y = None), arg = argmax tap
 static void bn_relu_maxpool(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, Tensor y, Tensor arg,
                             int64_t K, int64_t s, int64_t p) {
@@ -723,6 +753,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_relu_maxpool", &bn_relu_maxpool);
+  m.def("stem_s2d", &stem_s2d);
+  m.def("stem_w_s2d", &stem_w_s2d);
+  m.def("stem_dw_s2d", &stem_dw_s2d);
   m.def("conv_w_flip_t", &conv_w_flip_t);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("xent_finalize", &xent_finalize);

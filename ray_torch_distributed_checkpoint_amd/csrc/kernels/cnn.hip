@@ -758,6 +758,69 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_bf16_kernel(const float* __r
   }
 }
 
+// ---- ResNet stem as a space-to-depth convolution -------------------------------------------
+// The 7x7 / stride-2 / pad-3 convolution of a 3-channel image equals a 4x4 / stride-1 / pad-2
+// convolution (Ho x Wo = H/2 x W/2) of its 2x2 space-to-depth image
+//     X'[b][i][j][q] = X[b][2i+di][2j+dj][c],   q = (2*di + dj)*3 + c  (q < 12; 12..15 zero)
+// with  W'[co][a][bb][q] = W[co][2a+di-1][2bb+dj-1][c]  (zero where 2a+di-1 or 2bb+dj-1 is -1):
+// output pixel (ho, wo) reads input rows 2(ho-2+a)+di = 2ho-3+kh for kh = 2a+di-1.  K becomes
+// 16 taps x 16 channels = 256 = four 64-deep k tiles of 4 taps each - an implicit GEMM on the
+// MFMA kernel (ConvStagerK, C = 16) with no column matrix, instead of a 147(->192)-deep im2col
+// that was written once and read twice per step.
+__global__ __launch_bounds__(256) void nchw_to_s2d_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                              int B, int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long long total = (long long)B * Ho * Wo;
+  const long long HW = (long long)H * W;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long q = i / Wo;
+    const int j = (int)(i - q * Wo);
+    const long long b = q / Ho;
+    const int r = (int)(q - b * Ho);
+    float v[16];
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float2 t = *(const float2*)(x + (b * 3 + c) * HW + (long long)(2 * r + di) * W + 2 * j);
+        v[(2 * di + 0) * 3 + c] = t.x;
+        v[(2 * di + 1) * 3 + c] = t.y;
+      }
+#pragma unroll
+    for (int e = 12; e < 16; ++e) v[e] = 0.f;
+    uint4* dst = (uint4*)(y + i * 16);
+    dst[0] = pack8(v);
+    dst[1] = pack8(v + 8);
+  }
+}
+
+// W' [Cout][256] (k = (a*4 + bb)*16 + q) from the channels-last bf16 weight [Cout][7][7][3]
+__global__ __launch_bounds__(256) void stem_w_to_s2d_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
+                                                           int Cout) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Cout * 256) return;
+  const int co = i >> 8, k = i & 255;
+  const int a = k >> 6, bb = (k >> 4) & 3, q = k & 15;
+  bf16_t v = 0;
+  if (q < 12) {
+    const int di = q / 6, dj = (q / 3) & 1, c = q % 3;
+    const int kh = 2 * a + di - 1, kw = 2 * bb + dj - 1;
+    if (kh >= 0 && kw >= 0) v = w[co * 147 + (kh * 7 + kw) * 3 + c];
+  }
+  wp[i] = v;
+}
+
+// dW [Cout][7][7][3] (fp32, channels-last gradient slot) = the matching entries of dW' [Cout][256]
+__global__ __launch_bounds__(256) void stem_dw_from_s2d_kernel(const float* __restrict__ dwp, float* __restrict__ dw,
+                                                              int Cout) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Cout * 147) return;
+  const int co = i / 147, r = i - co * 147;
+  const int kh = r / 21, kw = (r / 3) % 7, c = r % 3;
+  const int a = (kh + 1) >> 1, di = (kh + 1) & 1, bb = (kw + 1) >> 1, dj = (kw + 1) & 1;
+  dw[i] = dwp[co * 256 + (a * 4 + bb) * 16 + (2 * di + dj) * 3 + c];
+}
+
 // global average pool [B][HW][C] -> [B][C] (fp32 accumulate, bf16 out)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
                                                          int HW, int C) {
@@ -933,5 +996,21 @@ extern "C" int rtdc_nchw_to_nhwc_bf16(const float* x, void* y, int B, int C, lon
   if (HW % 8 != 0 || C != 3) return 1;
   const long long groups = (long long)B * HW / 8;
   hipLaunchKernelGGL(nchw_to_nhwc_bf16_kernel<3>, dim3(gsz(groups)), dim3(256), 0, st, x, (bf16_t*)y, B, HW);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_stem_s2d(const float* x, void* y, int B, int H, int W, hipStream_t st) {
+  if (H % 2 || W % 2 || W % 4) return 1;
+  hipLaunchKernelGGL(nchw_to_s2d_bf16_kernel, dim3(gsz((long long)B * (H / 2) * (W / 2))), dim3(256), 0, st, x,
+                     (bf16_t*)y, B, H, W);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+extern "C" int rtdc_stem_w_s2d(const void* w, void* wp, int Cout, hipStream_t st) {
+  hipLaunchKernelGGL(stem_w_to_s2d_kernel, dim3((Cout * 256 + 255) / 256), dim3(256), 0, st, (const bf16_t*)w,
+                     (bf16_t*)wp, Cout);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+extern "C" int rtdc_stem_dw_s2d(const float* dwp, float* dw, int Cout, hipStream_t st) {
+  hipLaunchKernelGGL(stem_dw_from_s2d_kernel, dim3((Cout * 147 + 255) / 256), dim3(256), 0, st, dwp, dw, Cout);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

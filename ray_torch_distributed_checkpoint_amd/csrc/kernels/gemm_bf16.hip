@@ -69,15 +69,15 @@ __device__ __forceinline__ void conv_tile_stats(const GemmArgs& a, const f32x4 (
         s2[j][r] += v * v;
       }
   }
+  // the 16 lanes of a column group: DPP row reduction (VALU only; the __shfl_xor tree was 128
+  // ds_bpermute LDS round trips per lane per tile)
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1)
+  for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s1[j][r] += __shfl_xor(s1[j][r], off, 64);
-        s2[j][r] += __shfl_xor(s2[j][r], off, 64);
-      }
+    for (int r = 0; r < 4; ++r) {
+      s1[j][r] = row16_sum(s1[j][r]);
+      s2[j][r] = row16_sum(s2[j][r]);
+    }
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -427,7 +427,9 @@ static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, doub
   const double slab_us = (double)a.M * a.N * 8.0 / 4.0e6;  // bytes / (4 TB/s) in us
   int best = 1;
   double best_t = 1e30;
-  for (int s = 1; s <= 128; ++s) {
+  // (up to 1024 slices: a single-tile product - the 64-channel convolutions' weight gradients
+  // over 0.8-3.2 M pixels - needs ~512 of them to fill the chip)
+  for (int s = 1; s <= 1024; ++s) {
     if (ktiles / s < 8 || (long long)s * a.M * a.N > a.ws_elems) break;
     const long long waves = (tiles * s + slots - 1) / slots;
     const double t = (double)waves * (double)((ktiles + s - 1) / s) * t_ktile_us + (s > 1 ? s * slab_us : 0.0);
@@ -516,7 +518,10 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
 //   mode 2: C[M][N]   (fp32) = A[K=npix][M]^T . im2col(X)[npix][N] weight gradient (split-K)
 extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream) {
   GemmArgs a = *args;
-  if (a.cv_C % 64 != 0 || a.cv_npix >= (1 << 24) || a.K % gemm::BK != 0 || a.N % 8 != 0) return 1;
+  // C a multiple of 64 (one tap per k tile) or a divisor of 64 that is a multiple of 8 (16-B
+  // chunks never straddle a tap: the space-to-depth stem, C = 16)
+  const bool c_ok = a.cv_C % 64 == 0 || (a.cv_C % 8 == 0 && 64 % a.cv_C == 0);
+  if (!c_ok || a.cv_npix >= (1 << 24) || a.K % gemm::BK != 0 || a.N % 8 != 0) return 1;
   if (mode == 2 && a.M % 8 != 0) return 1;  // mode 1: rows (pixels) are clamped + masked, any count
   if ((long long)a.cv_H * a.cv_W * a.cv_C * ((long long)a.cv_npix / ((long long)a.cv_Ho * a.cv_Wo)) >= (1LL << 31))
     return 1;

@@ -96,20 +96,24 @@ __device__ __forceinline__ int fdivq(int x, int d, float rd) {
   return q;
 }
 
-// Mode 1: A (K-major) = im2col(X) gathered on the fly.  A 64-deep k tile lies inside one tap
-// (C % 64 == 0), so row m of the tile is 128 contiguous bytes of X at pixel
+// Mode 1: A (K-major) = im2col(X) gathered on the fly.  With C % 64 == 0 a 64-deep k tile lies
+// inside one tap, so row m of the tile is 128 contiguous bytes of X at pixel
 // (b, ho*s - p + kh, wo*s - p + kw), channels c0..c0+63 - exactly the 8 x 16-B pieces the
-// plain K-major stager moves; out-of-image taps read the zero page.
+// plain K-major stager moves; out-of-image taps read the zero page.  With C | 64 (C = 16, 32:
+// the space-to-depth ResNet stem) a k tile spans 64/C taps and each 16-B chunk has its own
+// tap offset to[] and channel offset co[] (k = tap*C + c throughout).
 template <int ROWS, int NW>
 struct ConvStagerK {
   static constexpr int PIECES = ROWS / 8, PPW = PIECES / NW;
   const bf16_t* X;
-  int hb[PPW], wb[PPW], pb[PPW], co[PPW];
+  int hb[PPW], wb[PPW], pb[PPW], co[PPW], to[PPW];
   int H, W, C, KW;
+  float rKW;
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* Xp, int rows, int r0, int wave, int lane) {
     X = Xp;
     H = a.cv_H; W = a.cv_W; C = a.cv_C; KW = a.cv_KW;
+    rKW = 1.f / (float)KW;
     const float rWo = 1.f / (float)a.cv_Wo, rHo = 1.f / (float)a.cv_Ho;
 #pragma unroll
     for (int ii = 0; ii < PPW; ++ii) {
@@ -123,15 +127,24 @@ struct ConvStagerK {
       hb[ii] = ho * a.cv_stride - a.cv_pad;
       wb[ii] = wo * a.cv_stride - a.cv_pad;
       pb[ii] = b * H;
-      co[ii] = lchunk * 8;
+      const int kc = lchunk * 8;  // k offset of this chunk inside the 64-deep tile
+      to[ii] = C >= 64 ? 0 : kc / C;
+      co[ii] = kc - to[ii] * C;
     }
   }
 
   __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
-    const int tap = k0 / C, c0 = k0 - tap * C, kh = tap / KW, kw = tap - kh * KW;
+    const int tap0 = k0 / C, c0 = k0 - tap0 * C;
+    const int kh0 = tap0 / KW, kw0 = tap0 - kh0 * KW;
 #pragma unroll
     for (int ii = 0; ii < PPW; ++ii) {
       const int piece = wave * PPW + ii;
+      int kh = kh0, kw = kw0;
+      if (C < 64) {  // wave-uniform: several taps per k tile
+        const int tap = tap0 + to[ii];
+        kh = fdivq(tap, KW, rKW);
+        kw = tap - kh * KW;
+      }
       const int h = hb[ii] + kh, w = wb[ii] + kw;
       const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
       const bf16_t* src = ok ? X + (size_t)((pb[ii] + h) * W + w) * C + c0 + co[ii] : (const bf16_t*)g_conv_zero;

@@ -125,11 +125,14 @@ class ResNet18(nn.Module):
 
     def forward(self, x):
         """x: NCHW images (any float dtype).  Returns [B, num_classes] logits."""
-        if x.is_cuda:
-            h = cnn.to_nhwc_bf16(x)
+        c1 = self.conv1
+        if cnn.stem_supported(x, c1.weight, c1.stride, c1.pad):
+            # space-to-depth implicit GEMM straight from the NCHW fp32 images (no im2col matrix)
+            h = cnn.stem_conv(x, c1.weight, bn_stats=self.training)
         else:
-            h = x.permute(0, 2, 3, 1).float().contiguous()
-        h = self.bn1.relu_max_pool(self.conv1(h), 3, 2, 1)
+            h = cnn.to_nhwc_bf16(x) if x.is_cuda else x.permute(0, 2, 3, 1).float().contiguous()
+            h = c1(h)
+        h = self.bn1.relu_max_pool(h, 3, 2, 1)
         h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
         return self.fc(cnn.global_avg_pool(h))
 

@@ -291,6 +291,77 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, bn_s
     return y
 
 
+class _StemConvS2D(torch.autograd.Function):
+    """ResNet stem (7x7 / stride 2 / pad 3, 3-channel NCHW fp32 images, no bias) as a 4x4 /
+    stride-1 / pad-2 implicit-GEMM convolution of the 2x2 space-to-depth image (16 channels,
+    K = 256; cnn.hip "ResNet stem as a space-to-depth convolution").  The input needs no
+    gradient (it is the data); the weight gradient is one mode-2 implicit GEMM into [Cout, 256]
+    gathered back into the channels-last [Cout, 7, 7, 3] gradient slot."""
+
+    @staticmethod
+    def forward(ctx, x, w, bn_stats):
+        B, _, H, W = x.shape
+        Ho, Wo = H // 2, W // 2
+        Cout = w.shape[0]
+        xs = torch.empty((B, Ho, Wo, 16), dtype=torch.bfloat16, device=x.device)
+        gpu_ext().stem_s2d(x.contiguous(), xs)
+        wp = _padded_buffer(("stem_s2d", id(w)), (Cout, 256), torch.bfloat16, x.device)
+        gpu_ext().stem_w_s2d(_weight_matrix(w, 147).contiguous(), wp)
+        M = B * Ho * Wo
+        y = torch.empty((M, Cout), dtype=torch.bfloat16, device=x.device)
+        smean = sm2 = None
+        if bn_stats:
+            nt = (M + 127) // 128
+            smean = torch.empty((nt, Cout), dtype=torch.float32, device=x.device)
+            sm2 = torch.empty((nt, Cout), dtype=torch.float32, device=x.device)
+        bm = gpu_ext().conv_gemm(xs, wp, y, 1, M, Cout, 256, 256, Ho, Wo, 4, 1, 2, None, smean, sm2, None)
+        if bn_stats:
+            ntiles = (M + bm - 1) // bm
+            ctx.stats = (smean[:ntiles], sm2[:ntiles], bm)
+        ctx.save_for_backward(xs)
+        ctx.w = w
+        ctx.geom = (M, Ho, Wo, Cout)
+        return y.view(B, Ho, Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xs,) = ctx.saved_tensors
+        M, Ho, Wo, Cout = ctx.geom
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dy2 = _rows_padded(dy.contiguous().view(M, Cout), _ceil(M, 64))
+            dwp = torch.empty((Cout, 256), dtype=torch.float32, device=dy.device)
+            ws = G.workspace(dy.device, G.SPLITK_WS_ELEMS, "splitk")
+            gpu_ext().conv_gemm(xs, dy2, dwp, 2, Cout, 256, dy2.shape[0], Cout, Ho, Wo, 4, 1, 2, ws, None, None,
+                                None)
+            tw, direct = _grad_matrix(ctx.w, 147)
+            if direct is not None:
+                gpu_ext().stem_dw_s2d(dwp, direct)
+                dw = tw
+            else:
+                full = torch.empty((Cout, 147), dtype=torch.float32, device=dy.device)
+                gpu_ext().stem_dw_s2d(dwp, full)
+                dw = full.view(Cout, 7, 7, 3).permute(0, 3, 1, 2)
+                dw = tw.copy_(dw) if tw is not None else dw.contiguous()
+        return None, dw, None
+
+
+def stem_supported(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 3 and x.shape[2] % 2 == 0
+            and x.shape[3] % 4 == 0 and tuple(w.shape[1:]) == (3, 7, 7) and stride == 2 and pad == 3
+            and os.environ.get("RTDC_STEM_S2D", "1") != "0")
+
+
+def stem_conv(x: torch.Tensor, w: torch.Tensor, bn_stats: bool = True) -> torch.Tensor:
+    """conv2d(NCHW fp32 images -> NHWC bf16, 7x7 / 2 / pad 3) through the space-to-depth implicit
+    GEMM; returns [B, H/2, W/2, Cout] with the BatchNorm statistics of the output attached."""
+    y = _StemConvS2D.apply(x, w, bn_stats)
+    st = getattr(y.grad_fn, "stats", None) if y.grad_fn is not None else None
+    if st is not None:
+        y._rtdc_bn_stats = st
+    return y
+
+
 def _bn_blocks(N: int, C: int) -> int:
     # ~32 16-B loads per thread in the statistics pass; bounded so the merge stays cheap
     return max(1, min(2048, (N * C) // (256 * 8 * 32)))

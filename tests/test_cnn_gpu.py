@@ -158,6 +158,38 @@ def test_stem_bn_relu_maxpool_equals_unfused(hw, stats):
     _close(outs[1][0], _nhwc(ref), 0.02, "y vs torch")
 
 
+@pytest.mark.parametrize("B,H", [(2, 224), (3, 64), (2, 36)])
+def test_stem_space_to_depth_conv_matches_torch(B, H):
+    """The 7x7/2 stem as a 4x4/1 implicit GEMM over the space-to-depth image == F.conv2d (fp32
+    reference on the same bf16-rounded operands): output, fused BN statistics, weight gradient
+    (written through the channels-last gradient slot); and == the im2col path."""
+    from ray_torch_distributed_checkpoint_amd.ops import cnn
+
+    torch.manual_seed(B * H)
+    x = torch.randn(B, 3, H, H, device=DEV)
+    w = (torch.randn(64, 3, 7, 7, device=DEV) * 0.1).to(memory_format=torch.channels_last).requires_grad_(True)
+    assert cnn.stem_supported(x, w, 2, 3)
+    y = cnn.stem_conv(x, w, bn_stats=True)
+    xr = x.bfloat16().float()
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    ref = F.conv2d(xr, wr, stride=2, padding=3).permute(0, 2, 3, 1)
+    _close(y, ref, 0.01, "stem y")
+    st = y._rtdc_bn_stats
+    mean_tiles, rows = st[0], st[2]
+    yf = y.float().reshape(-1, 64)
+    n_full = yf.shape[0] // rows
+    if n_full:
+        torch.testing.assert_close(mean_tiles[:n_full], yf[: n_full * rows].view(n_full, rows, 64).mean(1),
+                                   rtol=1e-3, atol=1e-3)
+    gy = torch.randn(y.shape, device=DEV).bfloat16()
+    y.backward(gy)
+    ref.backward(gy.float())
+    _close(w.grad, wr.grad, 0.01, "stem dW")
+    # the generic im2col path on the NHWC bf16 image gives the same output
+    y2 = cnn.conv2d(cnn.to_nhwc_bf16(x), w.detach(), 2, 3)
+    _close(y, y2, 0.01, "stem vs im2col")
+
+
 def test_pools_and_classifier():
     from ray_torch_distributed_checkpoint_amd.ops import cnn
 
