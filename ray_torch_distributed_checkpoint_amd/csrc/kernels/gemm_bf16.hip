@@ -289,28 +289,59 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
   if constexpr (GM == 3) conv_tile_stats<CFG>(a, acc, alpha, m0, n0, wm, wn, lane, smem);
 }
 
-// out[m][n] = sum_s ws[s][m][n] (+ beta * Cin[m][n]); fixed slice order.
+// out[m][n] = sum_s ws[s][m][n] (+ beta * Cin[m][n]).  A block owns 64 float4 column groups
+// and W = min(16, S) waves: wave w sums slices w, w+W, w+2W, ... (four loads in flight), and the
+// W partials are added in wave order - a fixed order for a given S, so the result is bitwise
+// reproducible.  (One thread summing all S slices serially was latency-bound at S = 170-512:
+// the single-tile weight gradients of the 64-channel convolutions.)
 template <typename OutT>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
-                                                           OutT* C, const OutT* Cin, int ldc, float beta) {
+__global__ __launch_bounds__(1024) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                            OutT* C, const OutT* Cin, int ldc, float beta) {
+  __shared__ f32x4 part[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
   const long long total4 = (long long)M * N / 4;
-  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < total4; q += (long long)gridDim.x * 256) {
-    const long long e = q * 4;
-    const int m = (int)(e / N), n = (int)(e % N);
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < S; ++s) {
-      f32x4 x = *(const f32x4*)(ws + (long long)s * M * N + e);
-      v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
+  const long long q = (long long)blockIdx.x * 64 + lane;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (q < total4) {
+    const long long MN = (long long)M * N;
+    const float* p = ws + q * 4;
+    int s = w;
+    for (; s + 3 * W < S; s += 4 * W) {
+      const f32x4 x0 = *(const f32x4*)(p + (long long)s * MN);
+      const f32x4 x1 = *(const f32x4*)(p + (long long)(s + W) * MN);
+      const f32x4 x2 = *(const f32x4*)(p + (long long)(s + 2 * W) * MN);
+      const f32x4 x3 = *(const f32x4*)(p + (long long)(s + 3 * W) * MN);
+      acc += x0;
+      acc += x1;
+      acc += x2;
+      acc += x3;
     }
-    const long long off = (long long)m * ldc + n;
-    if (Cin && beta != 0.f) {
-      float c[4];
-      load4<OutT>(Cin + off, c);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += beta * c[r];
-    }
-    store4<OutT>(C + off, v);
+    for (; s < S; s += W) acc += *(const f32x4*)(p + (long long)s * MN);
   }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w != 0 || q >= total4) return;
+  f32x4 v4 = part[0][lane];
+  for (int i = 1; i < W; ++i) v4 += part[i][lane];
+  const long long e = q * 4;
+  const int m = (int)(e / N), n = (int)(e % N);
+  float v[4] = {v4[0], v4[1], v4[2], v4[3]};
+  const long long off = (long long)m * ldc + n;
+  if (Cin && beta != 0.f) {
+    float c[4];
+    load4<OutT>(Cin + off, c);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += beta * c[r];
+  }
+  store4<OutT>(C + off, v);
+}
+
+template <typename OutT>
+static void launch_splitk_reduce(const GemmArgs& a, hipStream_t st) {
+  const long long total4 = (long long)a.M * a.N / 4;
+  const int W = a.splitk < 16 ? a.splitk : 16;
+  hipLaunchKernelGGL(splitk_reduce_kernel<OutT>, dim3((unsigned)((total4 + 63) / 64)), dim3(64 * W), 0, st, a.ws,
+                     a.splitk, a.M, a.N, (OutT*)a.C, (const OutT*)a.Cin, a.ldc, a.beta);
 }
 
 using Cfg128x128 = TileCfg<128, 128, 2, 2>;
@@ -484,15 +515,8 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     else launch_layout<false, true, bf16_t>(a, cfg, batch, stream);
   }
   if (a.splitk > 1) {
-    long long q = (long long)a.M * a.N / 4;
-    long long blocks = (q + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    if (out_fp32)
-      hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws,
-                         a.splitk, a.M, a.N, (float*)a.C, (const float*)a.Cin, a.ldc, a.beta);
-    else
-      hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws,
-                         a.splitk, a.M, a.N, (bf16_t*)a.C, (const bf16_t*)a.Cin, a.ldc, a.beta);
+    if (out_fp32) launch_splitk_reduce<float>(a, stream);
+    else launch_splitk_reduce<bf16_t>(a, stream);
   }
   if (a.cs_out) {
     // column sums of C: the 8-wave gelu-backward epilogue left one partial row per (row tile,
@@ -542,13 +566,7 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
     a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a));
     if (narrow) launch_cfg<Cfg64x256, false, false, float, 2>(a, 1, stream);
     else launch_cfg<Cfg128x128, false, false, float, 2>(a, 1, stream);
-    if (a.splitk > 1) {
-      long long q = (long long)a.M * a.N / 4;
-      long long blocks = (q + 255) / 256;
-      if (blocks > 4096) blocks = 4096;
-      hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream, a.ws, a.splitk,
-                         a.M, a.N, (float*)a.C, (const float*)a.Cin, a.ldc, a.beta);
-    }
+    if (a.splitk > 1) launch_splitk_reduce<float>(a, stream);
   } else {
     return 1;
   }
