@@ -69,6 +69,7 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, n_valid: int | Non
 # (96 MB), 810.1 (48 MB): the per-chunk GEMM tails cost more than the HBM round trip saves.
 _LM_CHUNK_MB = float(os.environ.get("RTDC_LMHEAD_CHUNK_MB", "0"))
 _chunk_bufs: dict = {}
+_LM_BLASLT = os.environ.get("RTDC_LMHEAD_BLASLT", "1") != "0"
 
 
 def _lm_chunk_rows(M: int, Vp: int) -> int:
@@ -104,7 +105,13 @@ class _LMHeadXent(torch.autograd.Function):
         tgt = target.reshape(-1).contiguous()
         R = _lm_chunk_rows(M, Vp)
         if R >= M:
-            logits = G.linear_fwd(x2, ws)  # [M, Vp] bf16, softmax gradient written in place
+            # [M, Vp] bf16, softmax gradient written in place.  The logits product is a plain
+            # GEMM (no epilogue - the fused work is the cross-entropy kernel after it), the one
+            # place hipBLASLt is measured ahead of the native persistent kernel on a GPT-2 shape
+            # (1172 vs 985 TF, profiles/gemm_bench_r2_warm.jsonl; step 19.35 -> 19.04 ms,
+            # profiles/lmhead_blaslt_ab.txt), so it runs there; RTDC_LMHEAD_BLASLT=0 keeps it
+            # on the MFMA kernel
+            logits = torch.matmul(x2, ws.t()) if _LM_BLASLT else G.linear_fwd(x2, ws)
             gpu_ext().xent(logits, logits, tgt, loss, None, None, M, vocab, Vp, scale, IGNORE_INDEX)
         else:
             # row chunks: each chunk's logits land in one reused buffer small enough to stay in
