@@ -150,8 +150,9 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
     a.cs_ws = cs_ws->data_ptr<float>();
     a.cs_ws_elems = cs_ws->numel();
   }
-  TORCH_CHECK(!(act == 2) || a.aux_out, "gelu forward needs aux_out");
-  TORCH_CHECK(!(act == 3 || act == 4) || a.aux_in, "activation backward needs aux_in");
+  TORCH_CHECK(act >= 0 && act <= 6, "gemm_bf16: act 0..6");
+  TORCH_CHECK(!(act == 2 || act == 5) || a.aux_out, "gelu forward needs aux_out");
+  TORCH_CHECK(!(act == 3 || act == 4 || act == 6) || a.aux_in, "activation backward needs aux_in");
   check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream()),
            "gemm_bf16");
 }

@@ -19,7 +19,8 @@ struct GemmArgs {
   int batch_inner;
   float alpha, beta;
   const float* alpha_dev;  // optional device scalar multiplied into alpha (upstream loss grad)
-  int act;        // 0 none, 1 relu, 2 gelu_tanh, 3 *gelu'(aux_in), 4 *relu'(aux_in)
+  int act;        // 0 none, 1 relu, 2 gelu_tanh (aux_out = pre-activation), 3 *gelu'(aux_in),
+                  // 4 *relu'(aux_in), 5 gelu_tanh (aux_out = gelu'(pre-activation)), 6 *aux_in
   int causal;     // 0 none, 1 skip tiles with n0 > m_last, 2 k < m0+BM, 3 k >= m0
   int bias_type;  // 0 none, 1 bf16, 2 fp32
   // split-K (plain epilogue only): fp32 partial slabs [splitk][M][N] reduced by a second kernel

@@ -180,6 +180,14 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float s = gelu_sigmoid_arg(x);
   return fmaf(2.f * x * s * (1.f - s) * k0, fmaf(3.f * k1, x * x, 1.f), s);
 }
+// gelu(x) and gelu'(x) from one sigmoid (the forward epilogue that stores the derivative for
+// the backward: act 5)
+__device__ __forceinline__ float gelu_tanh_and_grad(float x, float& g) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float s = gelu_sigmoid_arg(x);
+  g = fmaf(2.f * x * s * (1.f - s) * k0, fmaf(3.f * k1, x * x, 1.f), s);
+  return x * s;
+}
 
 // Philox4x32-10 counter-based RNG: deterministic function of (seed, counter), so dropout
 // masks are regenerated in backward and on resume from (seed, offset) alone.

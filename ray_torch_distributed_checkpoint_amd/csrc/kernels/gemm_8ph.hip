@@ -112,7 +112,7 @@ __device__ __forceinline__ typename Frag<KMAJOR>::T load_frag96(const char* tile
 template <int ACT, int TMQ, int TNQ, int SA, int SB, int BH, bool ZERO>
 __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
                                                    int wa, int wb, int lane, float alpha) {
-  constexpr bool ACT_IN = ACT == 3 || ACT == 4;
+  constexpr bool ACT_IN = ACT == 3 || ACT == 4 || ACT == 6;
   // descriptors over this tile's rows m0.. (tile-relative 32-bit offsets: the launcher keeps
   // 256 rows x ldc x 2 B under 2 GiB)
   const long long tile_off = (long long)m0 * a.ldc * 2, rows_bytes = (long long)(a.M - m0) * a.ldc * 2;
@@ -120,7 +120,7 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
   const bool has_cin = a.Cin && a.beta != 0.f;
   const auto rIn = make_rsrc(ACT_IN ? (const void*)a.aux_in : a.Cin, tile_off, (ACT_IN || has_cin) ? rows_bytes : 0);
   const auto rCin = make_rsrc(a.Cin, tile_off, (ACT_IN && has_cin) ? rows_bytes : 0);
-  const auto rAux = make_rsrc(a.aux_out, tile_off, ACT == 2 ? rows_bytes : 0);
+  const auto rAux = make_rsrc(a.aux_out, tile_off, (ACT == 2 || ACT == 5) ? rows_bytes : 0);
   const int bias_elt = a.bias_type == 2 ? 4 : 2;
   const auto rBias = make_rsrc(a.bias, 0, a.bias_type ? (long long)a.N * bias_elt : 0);
 
@@ -160,7 +160,7 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
   }
   // column sums of the gelu-backward output (the c_fc bias gradient): per lane over its pairs,
   // then over the 16 lanes of a row group, one partial row per (row tile, wave row) in cs_ws
-  constexpr bool CSUM = ACT == 3;
+  constexpr bool CSUM = ACT == 3 || ACT == 6;
   const bool do_cs = CSUM && a.cs_ws != nullptr;
   float cs[CSUM ? TNQ : 1][8];
   if constexpr (CSUM) {
@@ -210,9 +210,14 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
       buf_store16(rAux, off, pack8bf(v));
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = gelu_tanh(v[r]);
-    } else if constexpr (ACT == 3) {
+    } else if constexpr (ACT == 5) {
+      float g[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] *= gelu_tanh_grad(x[r]);
+      for (int r = 0; r < 8; ++r) v[r] = gelu_tanh_and_grad(v[r], g[r]);
+      buf_store16(rAux, off, pack8bf(g));
+    } else if constexpr (ACT == 3 || ACT == 6) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] *= ACT == 6 ? x[r] : gelu_tanh_grad(x[r]);
       if (do_cs && off != BUF_OOB) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) cs[c][r] += v[r];
@@ -252,6 +257,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& a, f32x4 (&acc)[2]
       case 2: tile_epilogue_bf16<2, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
       case 3: tile_epilogue_bf16<3, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
       case 4: tile_epilogue_bf16<4, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+      case 5: tile_epilogue_bf16<5, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
+      case 6: tile_epilogue_bf16<6, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
       default: tile_epilogue_bf16<0, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;
     }
   } else {

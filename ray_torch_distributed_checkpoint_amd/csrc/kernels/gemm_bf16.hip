@@ -276,12 +276,17 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
         store4<bf16_t>(a.aux_out + off, v);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-      } else if (a.act == 3 || a.act == 4) {
+      } else if (a.act == 5) {
+        float g[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh_and_grad(v[r], g[r]);
+        store4<bf16_t>(a.aux_out + off, g);
+      } else if (a.act == 3 || a.act == 4 || a.act == 6) {
         float h[4];
         load4<bf16_t>(a.aux_in + off, h);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          v[r] *= (a.act == 3) ? gelu_tanh_grad(h[r]) : (h[r] > 0.f ? 1.f : 0.f);
+          v[r] *= (a.act == 6) ? h[r] : (a.act == 3) ? gelu_tanh_grad(h[r]) : (h[r] > 0.f ? 1.f : 0.f);
       }
       store4<OutT>(C + off, v);
     }
@@ -522,7 +527,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     // column sums of C: the 8-wave gelu-backward epilogue left one partial row per (row tile,
     // wave row) in cs_ws; anything else reduces C itself
     const int tiles_m = (a.M + 255) / 256;
-    if (big && a.act == 3 && !out_fp32) {
+    if (big && (a.act == 3 || a.act == 6) && !out_fp32) {
       const int W = tiles_m * (bn == 256 ? 2 : 4);
       if ((long long)(W + 64) * a.N > a.cs_ws_elems) return 1;
       const int rc = rtdc_colsum_rows(a.cs_ws, W, a.N, a.cs_ws + (long long)W * a.N, a.cs_out, 0, stream);

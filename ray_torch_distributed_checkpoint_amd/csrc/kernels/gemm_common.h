@@ -315,11 +315,17 @@ __device__ __forceinline__ void epilogue4(const GemmArgs& a, OutT* C, const OutT
     store4<bf16_t>(a.aux_out + off, v);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-  } else if (a.act == 3 || a.act == 4) {
+  } else if (a.act == 5) {
+    float g[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = gelu_tanh_and_grad(v[r], g[r]);
+    store4<bf16_t>(a.aux_out + off, g);
+  } else if (a.act == 3 || a.act == 4 || a.act == 6) {
     float h[4];
     load4<bf16_t>(a.aux_in + off, h);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= (a.act == 3) ? gelu_tanh_grad(h[r]) : (h[r] > 0.f ? 1.f : 0.f);
+    for (int r = 0; r < 4; ++r)
+      v[r] *= (a.act == 6) ? h[r] : (a.act == 3) ? gelu_tanh_grad(h[r]) : (h[r] > 0.f ? 1.f : 0.f);
   }
   store4<OutT>(C + off, v);
 }

@@ -14,6 +14,9 @@ import torch
 from ._ext import gpu_ext
 
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
+# GELU forward storing gelu'(pre-activation) (bf16) as the side output, and the dgrad epilogue
+# that multiplies by it: the backward needs no transcendental
+ACT_GELU_SAVE_GRAD, ACT_MUL = 5, 6
 CAUSAL_NONE, CAUSAL_SKIP_UPPER, CAUSAL_K_UPTO_M, CAUSAL_K_FROM_M = 0, 1, 2, 3
 
 _COLSUM_BLOCKS = 256

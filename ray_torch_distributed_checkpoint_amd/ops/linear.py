@@ -12,6 +12,8 @@ On CPU every op is its PyTorch reference implementation (same math, autograd by 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -140,6 +142,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, relu
     return y
 
 
+# 1: the c_fc forward stores gelu'(pre) and the backward multiplies by it (act 5 / 6);
+# 0 (default): it stores the pre-activation and the backward evaluates gelu' (act 2 / 3).
+# Measured neutral on GPT-2-small (profiles/gelu_save_grad_ab.txt): the dgrad epilogue is not
+# bound by its two transcendentals, so the numerics stay on the original pair.
+_GELU_SAVE_GRAD = os.environ.get("RTDC_GELU_SAVE_GRAD", "0") == "1"
+
+
 class _FusedMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_fc, b_fc, w_proj, b_proj, residual):
@@ -150,8 +159,10 @@ class _FusedMLP(torch.autograd.Function):
         M = x2.shape[0]
         H = w_fc.shape[0]
         wfs, wps = shadow_of(w_fc), shadow_of(w_proj)
+        # side output: the pre-activation (or gelu'(pre) with RTDC_GELU_SAVE_GRAD=1)
         pre = torch.empty((M, H), dtype=torch.bfloat16, device=x.device)
-        g = G.linear_fwd(x2, wfs, bias=b_fc, act=G.ACT_GELU, aux_out=pre)
+        g = G.linear_fwd(x2, wfs, bias=b_fc, act=G.ACT_GELU_SAVE_GRAD if _GELU_SAVE_GRAD else G.ACT_GELU,
+                         aux_out=pre)
         res2 = residual.reshape(-1, C) if residual is not None else None
         y = G.linear_fwd(g, wps, bias=b_proj, residual=res2)
         ctx.save_for_backward(x2, wfs, wps, pre, g)
@@ -174,7 +185,8 @@ class _FusedMLP(torch.autograd.Function):
         db_fc = grad_target(b_fc)
         if db_fc is None and b_fc is not None:
             db_fc = torch.empty(b_fc.shape, dtype=torch.float32, device=dy2.device)
-        dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_GELU_BWD, aux_in=pre, colsum_out=db_fc)
+        dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_MUL if _GELU_SAVE_GRAD else G.ACT_GELU_BWD, aux_in=pre,
+                              colsum_out=db_fc)
         dw_fc = G.linear_wgrad(dpre, x2, out=grad_target(w_fc))
         dx = G.linear_dgrad(dpre, wfs).view(ctx.in_shape)
         return dx, dw_fc, db_fc, dw_proj, db_proj, (dy if ctx.has_res else None)

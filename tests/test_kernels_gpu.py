@@ -109,6 +109,36 @@ def test_gemm_gelu_bwd_colsum(cfg):
     _close(cs, ref.sum(0), 5e-3)
 
 
+@pytest.mark.parametrize("cfg", [-1, 0, 6, 7, 9])
+def test_gemm_gelu_saved_derivative_roundtrip(cfg):
+    """act 5: y = gelu(x W^T + b) with aux_out = gelu'(pre) (bf16), act 6: dx = (dy W) * aux_in
+    with the fused column sums - together the GELU forward/backward pair of the MLP, against
+    fp32 torch autograd, on the 4-wave, 8-wave (256x256 / 256x192) and persistent kernels."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(13)
+    M, K, N = 1024, 256, 768
+    x, w, b = _bf(M, K), _bf(N, K, scale=0.1), _bf(N, scale=0.5)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    gp = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(x, w, y, M, N, K, K, K, N, True, True, bias=b, aux_out=gp, act=G.ACT_GELU_SAVE_GRAD, tile_cfg=cfg)
+    pre = (x.float() @ w.float().t() + b.float()).requires_grad_(True)
+    yr = F.gelu(pre, approximate="tanh")
+    (gd,) = torch.autograd.grad(yr.sum(), pre)
+    _close(y, yr, 1e-2)
+    _close(gp, gd, 1e-2)
+    # dgrad through the saved derivative: dpre[M, N] = (dz[M, K2] @ w2[K2, N]) * gp
+    K2 = 256
+    dz, w2 = _bf(M, K2), _bf(K2, N, scale=0.1)
+    dpre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    cs = torch.full((N,), float("nan"), device=DEV)
+    G.gemm_bf16(dz, w2, dpre, M, N, K2, K2, N, N, True, False, aux_in=gp, act=G.ACT_MUL,
+                tile_cfg=cfg if cfg in (-1, 0, 6, 7) else -1, colsum_out=cs)
+    ref = (dz.float() @ w2.float()) * gp.float()
+    _close(dpre, ref, 1e-2)
+    _close(cs, ref.sum(0), 5e-3)
+
+
 def test_gemm_bf16_batched_strided():
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
 
