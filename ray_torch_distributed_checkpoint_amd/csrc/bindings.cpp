@@ -704,6 +704,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("finalize", &rtdc_ddp::GradBucketEngine::finalize, py::arg("defer_last") = false)
       .def("wait_tail", &rtdc_ddp::GradBucketEngine::wait_tail)
       .def("tail_pending", &rtdc_ddp::GradBucketEngine::tail_pending)
+      .def("can_stream_wait", &rtdc_ddp::GradBucketEngine::can_stream_wait)
+      .def("stream_wait_bucket", &rtdc_ddp::GradBucketEngine::stream_wait_bucket)
       .def("tail_start", &rtdc_ddp::GradBucketEngine::tail_start)
       .def("num_buckets", &rtdc_ddp::GradBucketEngine::num_buckets)
       .def("launched", &rtdc_ddp::GradBucketEngine::launched)

@@ -193,6 +193,25 @@ class GradBucketEngine {
   int64_t comm_bytes_per_step() const {
     return (bounds_.back() - bounds_.front()) * (lp_.defined() ? 2 : 4);
   }
+  // Make the CURRENT stream wait until bucket b's reduced gradient is final in the fp32 buffer
+  // (an optimizer update of that slice may then run on it while backward continues): the
+  // widen event (bf16 communication), the P2P done event, or - averaging backends - the
+  // collective itself (Work::wait on a CUDA-like backend orders the current stream after it).
+  // Backends that need the finalize() post-scale (SUM without a widen pass) cannot do this.
+  bool can_stream_wait() const { return flat_.is_cuda() && !zero_world_ && (use_avg_ || side_.has_value()); }
+  void stream_wait_bucket(int64_t b) {
+    TORCH_CHECK(can_stream_wait(), "stream_wait_bucket: needs a device buffer, no ZeRO, and AVG or bf16 comm");
+    TORCH_CHECK(b >= 0 && (size_t)b < works_.size() && launched_[b], "stream_wait_bucket: bucket not launched");
+    hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+    if (is_p2p(b)) {
+      TORCH_CHECK(hipStreamWaitEvent(cur, p2p_done_[b], 0) == hipSuccess, "hipStreamWaitEvent");
+    } else if (side_) {
+      TORCH_CHECK(hipStreamWaitEvent(cur, events_[b], 0) == hipSuccess, "hipStreamWaitEvent");
+    } else {
+      TORCH_CHECK(works_[b], "stream_wait_bucket: no work");
+      works_[b]->wait();
+    }
+  }
   bool tail_pending() const { return (bool)tail_; }
   int64_t tail_start() const { return bounds_[bounds_.size() - 2]; }
 

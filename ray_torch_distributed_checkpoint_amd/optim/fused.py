@@ -34,6 +34,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._steps: dict = {}  # param -> number of optimizer steps taken (host int)
         self._bound: set = set()
         self._have = None  # parameters with a gradient this step (set by the native step)
+        self._overlap = None  # optim.overlap.BackwardOverlap (updates run during backward)
 
     # -- flat setup ------------------------------------------------------------------------
     def _all_params(self):
@@ -198,6 +199,24 @@ class FusedAdamW(_FlatOptimizer):
                                       maximize=False, foreach=None, capturable=False, differentiable=False,
                                       fused=None))
 
+    def _native_launches(self, group, ps) -> list:
+        """[(params, decay_flags, fn(chunks, n))] of one param group's native update of `ps`
+        (advances their step counters)."""
+        sp, ext = self._space, gpu_ext()
+        for p in ps:
+            self._bind_state(p)
+        b1, b2 = group["betas"]
+        wd = group["weight_decay"]
+        out = []
+        for step, sub in self._count(ps).items():
+            def fn(chunks, n, group=group, b1=b1, b2=b2, wd=wd, step=step):
+                ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"],
+                          sp.shadow, group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step,
+                          math.sqrt(1 - b2 ** step), sp.grad_scale)
+
+            out.append((sub, [wd != 0.0] * len(sub), fn))
+        return out
+
     def _count(self, ps) -> dict:
         """Advance the step counter of every parameter in `ps`; {step: [params]}."""
         steps = self._steps
@@ -221,24 +240,16 @@ class FusedAdamW(_FlatOptimizer):
             sp = self._ensure_space()
             have = sp.ensure_grad_views()
             self._have = None if len(have) == len(sp.params) else set(have)
-            ext = gpu_ext()
+            ov = self._overlap
+            done = ov.updated if ov is not None else ()
             launches = []
             for group in self.param_groups:
-                ps = self._with_grad(group)
-                if not ps:
-                    continue
-                for p in ps:
-                    self._bind_state(p)
-                b1, b2 = group["betas"]
-                wd = group["weight_decay"]
-                for step, sub in self._count(ps).items():
-                    def fn(chunks, n, group=group, b1=b1, b2=b2, wd=wd, step=step):
-                        ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"],
-                                  sp.shadow, group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step,
-                                  math.sqrt(1 - b2 ** step), sp.grad_scale)
-
-                    launches.append((sub, [wd != 0.0] * len(sub), fn))
+                ps = [p for p in self._with_grad(group) if p not in done]
+                if ps:
+                    launches += self._native_launches(group, ps)
             self._launch_split(sp, launches)
+            if ov is not None:
+                ov.end_step()  # the compute stream waits for the updates that ran during backward
             sp.after_step()  # ZeRO-1: gather the updated shards
             return loss
         sp = space_of(self._all_params())
@@ -277,6 +288,30 @@ class FusedSGD(_FlatOptimizer):
                                       nesterov=nesterov, maximize=False, foreach=None, differentiable=False,
                                       fused=None))
 
+    def _native_launches(self, group, ps) -> list:
+        sp, ext = self._space, gpu_ext()
+        mom = group["momentum"]
+        wd = group["weight_decay"]
+        # torch's first momentum step is `buf = d` (a clone): parameters without a buffer yet
+        # form their own launch with first=True
+        parts = [(ps, False)]
+        if mom != 0.0:
+            fresh = [p for p in ps if "momentum_buffer" not in self.state[p]]
+            if fresh:
+                old = [p for p in ps if "momentum_buffer" in self.state[p]]
+                parts = [(fresh, True)] + ([(old, False)] if old else [])
+            for p in fresh:
+                self._bind_state(p)
+        out = []
+        for sub, first in parts:
+            def fn(chunks, n, group=group, mom=mom, wd=wd, first=first):
+                ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None,
+                        sp.shadow, group["lr"], mom, group["dampening"], wd, group["nesterov"], first,
+                        sp.grad_scale)
+
+            out.append((sub, [wd != 0.0] * len(sub), fn))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -287,32 +322,16 @@ class FusedSGD(_FlatOptimizer):
             sp = self._ensure_space()
             have = sp.ensure_grad_views()
             self._have = None if len(have) == len(sp.params) else set(have)
-            ext = gpu_ext()
+            ov = self._overlap
+            done = ov.updated if ov is not None else ()
             launches = []
             for group in self.param_groups:
-                ps = self._with_grad(group)
-                if not ps:
-                    continue
-                mom = group["momentum"]
-                wd = group["weight_decay"]
-                # torch's first momentum step is `buf = d` (a clone): parameters without a
-                # buffer yet form their own launch with first=True
-                parts = [(ps, False)]
-                if mom != 0.0:
-                    fresh = [p for p in ps if "momentum_buffer" not in self.state[p]]
-                    if fresh:
-                        old = [p for p in ps if "momentum_buffer" in self.state[p]]
-                        parts = [(fresh, True)] + ([(old, False)] if old else [])
-                    for p in fresh:
-                        self._bind_state(p)
-                for sub, first in parts:
-                    def fn(chunks, n, group=group, mom=mom, wd=wd, first=first):
-                        ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None,
-                                sp.shadow, group["lr"], mom, group["dampening"], wd, group["nesterov"], first,
-                                sp.grad_scale)
-
-                    launches.append((sub, [wd != 0.0] * len(sub), fn))
+                ps = [p for p in self._with_grad(group) if p not in done]
+                if ps:
+                    launches += self._native_launches(group, ps)
             self._launch_split(sp, launches)
+            if ov is not None:
+                ov.end_step()
             sp.after_step()  # ZeRO-1: gather the updated shards
             return loss
         sp = space_of(self._all_params())
