@@ -50,7 +50,9 @@ class BackwardOverlap:
         else:
             from ..parallel.ddp import DistributedDataParallel
 
-            cap = max(1, int(bucket_mb * (1 << 20) / 4))
+            # ~bucket_mb slices, but at most ~24 of them: each group costs one host-side hook
+            # dispatch in the autograd thread (an 8B-parameter model at 32 MB would be ~1000)
+            cap = max(1, int(bucket_mb * (1 << 20) / 4), sp.numel // 24)
             plan = DistributedDataParallel._plan([s.numel for s in sp.segments], cap, cap)
             self.groups = [[sp.params[i] for i in g] for g in plan]
         mine = {id(p) for p in opt._all_params()}
