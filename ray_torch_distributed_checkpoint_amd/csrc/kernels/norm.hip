@@ -220,6 +220,144 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   }
 }
 
+// The same backward with 8-B (4-element) lane chunks, for widths whose 16-B chunk count is not
+// a multiple of 64 (GPT-2: D = 768 -> 96 chunks of 8, so the 16-B form leaves half the lanes
+// idle in its second chunk and carries [2][8] accumulators; here 192 chunks of 4 = 3 per lane,
+// every lane busy, [3][4] accumulators: fewer VGPRs, more waves per SIMD for this latency-bound
+// stream).  Same math, same per-block partial rows.
+__device__ __forceinline__ void ld4b(const bf16_t* p, float* v) {
+  const uint2 q = *(const uint2*)p;
+  v[0] = __uint_as_float(q.x << 16);
+  v[1] = __uint_as_float(q.x & 0xffff0000u);
+  v[2] = __uint_as_float(q.y << 16);
+  v[3] = __uint_as_float(q.y & 0xffff0000u);
+}
+__device__ __forceinline__ void unpack4(uint2 q, float* v) {
+  v[0] = __uint_as_float(q.x << 16);
+  v[1] = __uint_as_float(q.x & 0xffff0000u);
+  v[2] = __uint_as_float(q.y << 16);
+  v[3] = __uint_as_float(q.y & 0xffff0000u);
+}
+
+template <int CPL, bool RMS, bool CS>
+__global__ __launch_bounds__(256) void norm_bwd4_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ ws_dg,
+    float* __restrict__ ws_db, float* __restrict__ ws_cs, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int nch = D >> 2;
+  float adg[CPL][4], adb[CPL][4], acs[CS ? CPL : 1][4];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) adg[i][e] = adb[i][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < (CS ? CPL : 1); ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acs[i][e] = 0.f;
+
+  float gg[CPL][4];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) ld4b(g + c * 4, gg[i]);
+  }
+  uint2 px[CPL], pd[CPL], pr[CPL];
+  float pmean = 0.f, prstd = 0.f;
+  auto fetch = [&](int r) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        px[i] = *(const uint2*)(x + (long long)r * D + c * 4);
+        pd[i] = *(const uint2*)(dy + (long long)r * D + c * 4);
+        if (dres) pr[i] = *(const uint2*)(dres + (long long)r * D + c * 4);
+      }
+    }
+    pmean = RMS ? 0.f : mean_in[r];
+    prstd = rstd_in[r];
+  };
+  if (gw < M) fetch(gw);
+  for (int row = gw; row < M; row += nw) {
+    const float mean = pmean;
+    const float rstd = prstd;
+    uint2 cx[CPL], cd[CPL], rraw[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      cx[i] = px[i];
+      cd[i] = pd[i];
+      rraw[i] = pr[i];
+    }
+    if (row + nw < M) fetch(row + nw);
+    float xh[CPL][4], dxh[CPL][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float xv[4], dv[4];
+        unpack4(cx[i], xv);
+        unpack4(cd[i], dv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[i][e] = (xv[e] - mean) * rstd;
+          dxh[i][e] = dv[e] * gg[i][e];
+          s1 += dxh[i][e];
+          s2 += dxh[i][e] * xh[i][e];
+          adg[i][e] += dv[e] * xh[i][e];
+          adb[i][e] += dv[e];
+        }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / D;
+    const float m2 = wave_sum(s2) / D;
+    bf16_t* dxr = dx + (long long)row * D;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[4], r[4];
+        if (dres) unpack4(rraw[i], r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = rstd * (dxh[i][e] - m1 - xh[i][e] * m2);
+          if (dres) o[e] += r[e];
+          if constexpr (CS) acs[i][e] += o[e];
+        }
+        *(uint2*)(dxr + c * 4) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+      }
+    }
+  }
+  extern __shared__ float red[];
+  constexpr int KCS = RMS ? 1 : 2;
+  const int wv = threadIdx.x >> 6;
+  for (int w = 0; w < 4; ++w) {
+    if (wv == w) {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            red[c * 4 + e] = w ? red[c * 4 + e] + adg[i][e] : adg[i][e];
+            if (!RMS) red[D + c * 4 + e] = w ? red[D + c * 4 + e] + adb[i][e] : adb[i][e];
+            if constexpr (CS) red[KCS * D + c * 4 + e] = w ? red[KCS * D + c * 4 + e] + acs[i][e] : acs[i][e];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int d = threadIdx.x; d < D; d += 256) {
+    ws_dg[(long long)blockIdx.x * D + d] = red[d];
+    if (!RMS) ws_db[(long long)blockIdx.x * D + d] = red[D + d];
+    if constexpr (CS) ws_cs[(long long)blockIdx.x * D + d] = red[KCS * D + d];
+  }
+}
+
 // out[d] (+)= sum_w ws[w][d], fixed summation order.  A block owns 64 columns; its 4 waves
 // stride over the W partial rows (coalesced 256-B rows per wave) and combine through LDS,
 // so a 1024 x 768 workspace is 12 blocks x 256 loads per lane instead of 768 serial chains.
@@ -367,6 +505,31 @@ static int resident_blocks(size_t lds) {
   return cus * occ;
 }
 
+template <bool RMS, bool CS>
+static int resident_blocks4(size_t lds, int cpl4) {
+  static int cus = 0;
+  static int occ[5] = {0, 0, 0, 0, 0};
+  static size_t occ_lds[5] = {~(size_t)0, ~(size_t)0, ~(size_t)0, ~(size_t)0, ~(size_t)0};
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  if (cpl4 < 1 || cpl4 > 4) return cus;
+  if (lds != occ_lds[cpl4]) {
+    hipError_t e = hipErrorInvalidValue;
+    int o = 0;
+    if (cpl4 == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, norm_bwd4_kernel<1, RMS, CS>, 256, lds);
+    if (cpl4 == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, norm_bwd4_kernel<2, RMS, CS>, 256, lds);
+    if (cpl4 == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, norm_bwd4_kernel<3, RMS, CS>, 256, lds);
+    if (cpl4 == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, norm_bwd4_kernel<4, RMS, CS>, 256, lds);
+    occ[cpl4] = (e != hipSuccess || o <= 0) ? 1 : o;
+    occ_lds[cpl4] = lds;
+  }
+  return cus * occ[cpl4];
+}
+
 template <bool RMS>
 static int launch_norm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                            const float* rstd, const void* dres, void* dx, float* ws, float* dg,
@@ -377,10 +540,19 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
   const int nz = (RMS ? 1 : 2) + (cs ? 1 : 0);
   const size_t lds = (size_t)nz * D * sizeof(float);
   if (lds > 160 * 1024) return 1;
+  static int vw4_env = -1;
+  if (vw4_env < 0) {
+    const char* e = getenv("RTDC_NORM_BWD_VW4");
+    vw4_env = (e && e[0] == '0') ? 0 : 1;
+  }
+  // 8-B chunks when they fill every lane (D/4 a multiple of 64) and 16-B ones would not
+  const bool vw4 = vw4_env && (D / 8) % 64 != 0 && (D / 4) % 64 == 0 && D / 4 <= 64 * 4;
   // one wave of blocks: a grid past the resident block slots leaves a partial second wave
   // (GPT-2: 1024 blocks on 768 slots ran 0.94 ms/step of LayerNorm backward, 768 blocks 0.67)
 #define RB(C) (cs ? resident_blocks<C, RMS, true>(lds) : resident_blocks<C, RMS, false>(lds))
-  const int slots = cpl <= 1 ? RB(1) : cpl <= 2 ? RB(2) : cpl <= 4 ? RB(4) : RB(8);
+  const int cpl4 = (D / 4) / 64;
+  const int slots = vw4 ? (cs ? resident_blocks4<RMS, true>(lds, cpl4) : resident_blocks4<RMS, false>(lds, cpl4))
+                        : cpl <= 1 ? RB(1) : cpl <= 2 ? RB(2) : cpl <= 4 ? RB(4) : RB(8);
 #undef RB
   const int nblk = nwaves / 4 < slots ? nwaves / 4 : slots;
   dim3 grid(nblk), block(256);
@@ -395,13 +567,23 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
                      (bf16_t*)dx, ws_dg, ws_db, ws_cs, M, D)
 #define LC(C) \
   if (cs) L(C, true); else L(C, false)
-  if (cpl <= 1) { LC(1); }
+#define L4(C, CS)                                                                             \
+  hipLaunchKernelGGL((norm_bwd4_kernel<C, RMS, CS>), grid, block, lds, st, (const bf16_t*)dy,  \
+                     (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \
+                     (bf16_t*)dx, ws_dg, ws_db, ws_cs, M, D)
+  if (vw4) {
+    if (cpl4 == 1) { if (cs) L4(1, true); else L4(1, false); }
+    else if (cpl4 == 2) { if (cs) L4(2, true); else L4(2, false); }
+    else if (cpl4 == 3) { if (cs) L4(3, true); else L4(3, false); }
+    else { if (cs) L4(4, true); else L4(4, false); }
+  } else if (cpl <= 1) { LC(1); }
   else if (cpl <= 2) { LC(2); }
   else if (cpl <= 4) { LC(4); }
   else if (cpl <= 8) { LC(8); }
   else return 1;
 #undef LC
 #undef L
+#undef L4
   // one reduction launch pair for all of them; the colsum of dx is never accumulated, so it
   // gets its own pair when dgamma/dbeta accumulate
   if (!cs || !accumulate) {

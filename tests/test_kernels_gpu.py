@@ -240,7 +240,7 @@ def test_layernorm_rmsnorm():
     from ray_torch_distributed_checkpoint_amd.ops import layer_norm, rms_norm
 
     torch.manual_seed(6)
-    for D in (768, 4096, 200):
+    for D in (768, 256, 4096, 200):  # 768 / 256: the 8-B-chunk backward (3 / 1 chunks per lane)
         M = 64
         x = _bf(M, D, scale=2.0).requires_grad_(True)
         w = (1 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
