@@ -12,3 +12,4 @@ python3 scripts/kstats.py "$f" 13 40 > gpurun_out/prof_gpt2_summary.txt
 t=$(find gpurun_out/prof_gpt2 -name '*kernel_trace.csv' | head -1)
 python3 scripts/ktimeline.py "$t" --last-ms 100 >> gpurun_out/prof_gpt2_summary.txt
 cat gpurun_out/prof_gpt2_summary.txt | head -80
+python3 scripts/kstep.py "$t" > gpurun_out/prof_gpt2_step.txt
