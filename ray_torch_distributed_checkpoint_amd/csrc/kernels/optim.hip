@@ -76,19 +76,43 @@ __global__ __launch_bounds__(256) void sgd_kernel(const Chunk* __restrict__ chun
   for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const Chunk c = chunks[ci];
     const float w = c.decay ? wd : 0.f;
-    for (int i = threadIdx.x; i < c.len; i += 256) {
-      const long long o = c.start + i;
-      float d = g[o] * grad_scale;
-      float pe = p[o];
+    auto upd = [&](float gv, float& pe, float& b) {
+      float d = gv * grad_scale;
       d += w * pe;
       if (momentum != 0.f) {
-        float b = first ? d : momentum * buf[o] + (1.f - dampening) * d;
-        buf[o] = b;
+        b = first ? d : momentum * b + (1.f - dampening) * d;
         d = nesterov ? d + momentum * b : b;
       }
       pe -= lr * d;
-      p[o] = pe;
-      if (shadow) shadow[o] = f2bf(pe);
+    };
+    const bool vec = (c.start & 3) == 0;
+    // 4 elements per lane and iteration (16-B loads of p, g and the momentum buffer)
+    for (int i = threadIdx.x * 4; i < c.len; i += 256 * 4) {
+      const long long o = c.start + i;
+      if (vec && i + 4 <= c.len) {
+        f32x4 pp = *(f32x4*)(p + o);
+        const f32x4 gg = *(const f32x4*)(g + o);
+        f32x4 bb = (momentum != 0.f && !first) ? *(f32x4*)(buf + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float pe = pp[e], b = bb[e];
+          upd(gg[e], pe, b);
+          pp[e] = pe;
+          bb[e] = b;
+        }
+        *(f32x4*)(p + o) = pp;
+        if (momentum != 0.f) *(f32x4*)(buf + o) = bb;
+        if (shadow) *(uint2*)(shadow + o) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+      } else {
+        for (int e = 0; e < 4 && i + e < c.len; ++e) {
+          const long long oe = o + e;
+          float pe = p[oe], b = (momentum != 0.f && !first) ? buf[oe] : 0.f;
+          upd(g[oe], pe, b);
+          if (momentum != 0.f) buf[oe] = b;
+          p[oe] = pe;
+          if (shadow) shadow[oe] = f2bf(pe);
+        }
+      }
     }
   }
 }
