@@ -7,6 +7,7 @@ MFMA path used by fp32 models (the reference toy MLP, R/my_ray_module.py:94-112)
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -23,6 +24,9 @@ _COLSUM_BLOCKS = 256
 SPLITK_MAX_OUT = 200 * 256 * 256  # outputs that fill < 200 tiles of 256x256 (e.g. Llama-8B at 2k tokens/GPU)
 SPLITK_WS_ELEMS = 64 << 20        # 256 MiB fp32 slab workspace cap
 _ws_cache: dict = {}
+# long-K weight gradients whose last round of output tiles is mostly empty run as two GEMMs
+# (full rounds + a split-K tail); RTDC_WGRAD_ROUND_SPLIT=0 keeps one launch
+_ROUND_SPLIT = os.environ.get("RTDC_WGRAD_ROUND_SPLIT", "1") != "0"
 
 
 def workspace(device, numel: int, tag: str = "ws") -> torch.Tensor:
@@ -78,12 +82,55 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=Non
     return dx
 
 
+_ncu: dict = {}
+
+
+def _num_cus(device) -> int:
+    n = _ncu.get(device)
+    if n is None:
+        n = torch.cuda.get_device_properties(device).multi_processor_count
+        _ncu[device] = n
+    return n
+
+
+def _round_split_rows(rows: int, cols: int, k: int, device) -> int:
+    """Output rows for the full-rounds part of a long-K weight gradient, or 0 (no split).
+
+    The 8-wave kernel runs one 256x256 tile per CU; an output of `tiles` tiles takes
+    ceil(tiles / CUs) rounds, and a last round that is mostly empty idles the chip for a whole
+    tile time (the GPT-2 LM head: 197 x 3 = 591 tiles = 2 full rounds + 79 tiles on 256 CUs).
+    The rows that fill whole rounds run as one GEMM; the rest - too few tiles for a round -
+    runs as a second one that the launcher splits along K (fp32 slabs + a fixed-order reduce),
+    which spreads it over the chip: 2 + 1/3 rounds instead of 3 there."""
+    if rows < 4096 or k < 64 * 64:
+        return 0
+    ncu = _num_cus(device)
+    tn, tm = (cols + 255) // 256, (rows + 255) // 256
+    tiles = tm * tn
+    rem = tiles % ncu
+    if tiles <= ncu or rem == 0 or rem * 2 > ncu:
+        return 0
+    tm_main = (tiles // ncu) * ncu // tn
+    if (tm - tm_main) * tn >= 200:  # the tail must be a split-K candidate (gemm_bf16.hip pick_splitk)
+        return 0
+    return tm_main * 256
+
+
 def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0, alpha_dev=None):
     """dw[N,K] (fp32) = alpha (* alpha_dev[0]) * dy[M,N]^T @ x[M,K]."""
     M, N = dy.shape
     K = x2d.shape[1]
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    split = _round_split_rows(N, K, M, dy.device) if (_ROUND_SPLIT and dy.is_cuda and dy.is_contiguous()
+                                                     and out.is_contiguous()) else 0
+    if split:
+        # rows [0, split) fill whole rounds of the chip; rows [split, N) go split-K (see above)
+        for r0, r1 in ((0, split), (split, N)):
+            o = out[r0:r1]
+            gemm_bf16(dy[:, r0:r1], x2d, o, r1 - r0, K, M, N, K, K, False, False, Cin=o if accumulate else None,
+                      beta=1.0 if accumulate else 0.0, alpha=alpha, alpha_dev=alpha_dev)
+        return out
     gemm_bf16(dy, x2d, out, N, K, M, N, K, K, False, False, Cin=out if accumulate else None,
               beta=1.0 if accumulate else 0.0, alpha=alpha, alpha_dev=alpha_dev)
     return out

@@ -139,6 +139,29 @@ def test_gemm_gelu_saved_derivative_roundtrip(cfg):
     _close(cs, ref.sum(0), 5e-3)
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_round_split(monkeypatch, accumulate):
+    """LM-head-shaped weight gradient (591 tiles on 256 CUs): the full-rounds GEMM + split-K
+    tail decomposition equals the fp32 reference, with and without accumulation."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    M, N, K = 16384, 50304, 768
+    assert G._round_split_rows(N, K, M, torch.device(DEV)) > 0
+    dy, x = _bf(M, N, scale=0.05), _bf(M, K)
+    base = torch.randn(N, K, device=DEV) if accumulate else None
+    ref = dy.float().t() @ x.float() * 0.5 + (base if accumulate else 0.0)
+    out = base.clone() if accumulate else torch.empty(N, K, device=DEV)
+    monkeypatch.setattr(G, "_ROUND_SPLIT", True)
+    G.linear_wgrad(dy, x, out=out, accumulate=accumulate, alpha=0.5)
+    torch.cuda.synchronize()
+    _close(out, ref, 2e-3)
+    out1 = base.clone() if accumulate else torch.empty(N, K, device=DEV)
+    monkeypatch.setattr(G, "_ROUND_SPLIT", False)
+    G.linear_wgrad(dy, x, out=out1, accumulate=accumulate, alpha=0.5)
+    torch.cuda.synchronize()
+    _close(out, out1, 1e-3)
+
+
 def test_gemm_bf16_batched_strided():
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
 
