@@ -25,6 +25,14 @@ __device__ __forceinline__ void st8(bf16_t* p, const float* v) {
   *(uint4*)p = x;
 }
 
+// red4[q] = (add ? red4[q] + v : v) for the 4 floats v (per-block partial-sum combine in LDS)
+__device__ __forceinline__ void red_acc4(float* red, int q, const float* v, int add) {
+  f32x4* p = (f32x4*)red + q;
+  f32x4 a = {v[0], v[1], v[2], v[3]};
+  if (add) a = *p + a;
+  *p = a;
+}
+
 template <int CPL, bool RMS>
 __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ g,
@@ -202,11 +210,12 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
       for (int i = 0; i < CPL; ++i) {
         const int c = lane + 64 * i;
         if (c < nch) {
+          // 16-B LDS accesses (scalar ones at a 32-B lane stride were 8-way bank conflicts)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            red[c * 8 + e] = w ? red[c * 8 + e] + adg[i][e] : adg[i][e];
-            if (!RMS) red[D + c * 8 + e] = w ? red[D + c * 8 + e] + adb[i][e] : adb[i][e];
-            if constexpr (CS) red[KCS * D + c * 8 + e] = w ? red[KCS * D + c * 8 + e] + acs[i][e] : acs[i][e];
+          for (int h = 0; h < 2; ++h) {
+            red_acc4(red, c * 2 + h, adg[i] + 4 * h, w);
+            if (!RMS) red_acc4(red, D / 4 + c * 2 + h, adb[i] + 4 * h, w);
+            if constexpr (CS) red_acc4(red, KCS * D / 4 + c * 2 + h, acs[i] + 4 * h, w);
           }
         }
       }
@@ -340,12 +349,10 @@ __global__ __launch_bounds__(256) void norm_bwd4_kernel(
       for (int i = 0; i < CPL; ++i) {
         const int c = lane + 64 * i;
         if (c < nch) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            red[c * 4 + e] = w ? red[c * 4 + e] + adg[i][e] : adg[i][e];
-            if (!RMS) red[D + c * 4 + e] = w ? red[D + c * 4 + e] + adb[i][e] : adb[i][e];
-            if constexpr (CS) red[KCS * D + c * 4 + e] = w ? red[KCS * D + c * 4 + e] + acs[i][e] : acs[i][e];
-          }
+          // 16-B LDS accesses (scalar ones at a 16-B lane stride were 4-way bank conflicts)
+          red_acc4(red, c, adg[i], w);
+          if (!RMS) red_acc4(red, D / 4 + c, adb[i], w);
+          if constexpr (CS) red_acc4(red, KCS * D / 4 + c, acs[i], w);
         }
       }
     }
