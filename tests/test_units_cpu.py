@@ -170,3 +170,23 @@ def test_cards_render(tmp_path):
     c.append(Table([["a", 1]], headers=["Image", "True label"]))
     html = open(c.save(str(tmp_path), "t")).read()
     assert "<h3>Misclassifications 3 out of 10</h3>" in html and "<th>True label</th>" in html
+
+
+def test_wgrad_round_split_rows():
+    """Weight-gradient decomposition into full rounds of 256x256 tiles + a split-K tail
+    (ops/gemm.py _round_split_rows) on a 256-CU device."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    G._ncu["fake"] = 256
+    # GPT-2 LM head: 197 x 3 = 591 tiles = 2 full rounds + 79 -> rows of 170 row-tiles
+    assert G._round_split_rows(50304, 768, 16384, "fake") == 170 * 256
+    # whole rounds, or fewer tiles than CUs: no split
+    assert G._round_split_rows(256 * 256, 256, 16384, "fake") == 0
+    assert G._round_split_rows(3072, 768, 16384, "fake") == 0
+    # a last round more than half full, or a short K: no split
+    assert G._round_split_rows(256 * 200, 512, 16384, "fake") == 0
+    assert G._round_split_rows(50304, 768, 2048, "fake") == 0
+    # Llama-3 LM head over 16k tokens: 501 x 16 = 8016 tiles = 31 rounds + 80 -> 496 row-tiles
+    assert G._round_split_rows(128256, 4096, 16384, "fake") == 496 * 256
+    # the tail must stay a split-K candidate (< 200 tiles)
+    assert G._round_split_rows(16 * 256, 257 * 256, 16384, "fake") == 0
