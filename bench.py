@@ -162,7 +162,13 @@ def main():
 
     ck = {}
     if not args.no_ckpt:
-        ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp)
+        # the throughput above is measured and must be reported even if the checkpoint phase
+        # fails (e.g. a filesystem that refuses the shard writes): the failure is reported too
+        try:
+            ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp)
+        except Exception as e:  # noqa: BLE001
+            ck = {"ckpt_unmeasured": f"checkpoint phase failed: {type(e).__name__}: {e}"[:300]}
+            print(f"[bench] rank {rank}: {ck['ckpt_unmeasured']}", file=sys.stderr, flush=True)
 
     metric, published = _baseline_metric()
     base = published.get("samples_per_sec") if isinstance(published, dict) else None
