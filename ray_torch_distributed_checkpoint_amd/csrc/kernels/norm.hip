@@ -403,13 +403,61 @@ __global__ __launch_bounds__(256) void colsum_ws_kernel(const float* __restrict_
   }
 }
 
+// One launch for up to kWideMaxRows partial rows: a 1024-thread block owns 64 columns; its 16
+// waves stride the rows (wave w: rows w, w+16, ...) with kWideU loads in flight per lane, and
+// the 16 wave partials are added in wave order in LDS - a fixed order for a given W
+// (bitwise reproducible).  The two-launch form (W -> W/32 -> 1) paid a second launch and a
+// kernel-boundary drain per reduction (~50 per GPT-2 step).
+constexpr int kWideU = 12, kWideMaxRows = 4096;
+__global__ __launch_bounds__(1024) void colsum_wide_kernel(const float* __restrict__ ws, OutPtrs outs, int W, int D,
+                                                          int accumulate, long long ws_z) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  ws += blockIdx.z * ws_z;
+  const int d = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (d < D) {
+    for (int w0 = wv; w0 < W; w0 += 16 * kWideU) {
+      float v[kWideU];
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) {
+        const int w = w0 + 16 * u;
+        v[u] = w < W ? ws[(long long)w * D + d] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) acc += v[u];
+    }
+  }
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && d < D) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += part[i][lane];
+    float* o = outs.p[blockIdx.z] + d;
+    *o = accumulate ? *o + t : t;
+  }
+}
+
+static bool colsum_wide_enabled() {
+  static int v = -1;  // RTDC_COLSUM_WIDE=0: the two-launch form (A/B)
+  if (v < 0) {
+    const char* e = getenv("RTDC_COLSUM_WIDE");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // nz <= 4 independent reductions ws + z*ws_z [W][D] (W partial rows) -> outs.p[z] [D];
 // tmp holds nz x S intermediate rows (nz * 64 * D floats).
 static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, OutPtrs outs, int accumulate,
                              hipStream_t st, int nz = 1, long long ws_z = 0) {
   int S = W / 32;
   S = S < 1 ? 1 : (S > 64 ? 64 : S);
-  if (S > 1 && tmp) {
+  if (S > 1 && W <= kWideMaxRows && colsum_wide_enabled()) {
+    hipLaunchKernelGGL(colsum_wide_kernel, dim3((D + 63) / 64, 1, nz), dim3(1024), 0, st, ws, outs, W, D, accumulate,
+                       ws_z);
+  } else if (S > 1 && tmp) {
     const int R = (W + S - 1) / S;
     hipLaunchKernelGGL(colsum_ws_kernel, dim3((D + 63) / 64, S, nz), dim3(256), 0, st, ws, tmp, outs, W, D, R, 0,
                        ws_z, 64LL * D);
