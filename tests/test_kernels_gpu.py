@@ -293,6 +293,26 @@ def test_layernorm_rmsnorm():
         _close(w.grad, wr2.grad, 1e-3)
 
 
+@pytest.mark.parametrize("M,N", [(100, 72), (4096, 768), (16384, 2304), (65536, 64)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_colsum_two_level_reduce(M, N, accumulate):
+    """Bias-gradient column sums (partial rows + the one-launch wide reduce or the single-stage
+    form for few partial rows) equal the fp32 reference, and repeat bitwise."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    x = _bf(M, N)
+    base = torch.randn(N, device=DEV)
+    out = base.clone() if accumulate else torch.empty(N, device=DEV)
+    G.colsum(x, out=out, accumulate=accumulate)
+    ref = x.float().sum(0) + (base if accumulate else 0.0)
+    torch.cuda.synchronize()
+    _close(out, ref, 1e-4 * math.sqrt(M))
+    out2 = base.clone() if accumulate else torch.empty(N, device=DEV)
+    G.colsum(x, out=out2, accumulate=accumulate)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+
+
 def test_layernorm_bwd_offers_dx_colsum():
     """LayerNorm backward also reduces the column sums of the residual-stream gradient it
     writes (passthrough form, dres added); colsum() of that gradient takes them (no second
