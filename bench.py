@@ -74,6 +74,10 @@ def main():
                     help="if the full train state does not fit on disk, measure model scope (flagged)")
     ap.add_argument("--overlap-steps", type=int, default=5)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (multi-rank rehearsal on 1 GPU)")
+    ap.add_argument("--cpu", action="store_true",
+                    help="run on the CPU (gloo; a plumbing rehearsal of the N-rank path, e.g. in CI - not a benchmark)")
+    ap.add_argument("--sweep", type=int, default=1, choices=[0, 1],
+                    help="N > 1: after the timed run, a short bucket_cap_mb x grad-comm-dtype sweep (comm.sweep)")
     args = ap.parse_args()
     args.batch_set, args.seq_len_set = args.batch is not None, args.seq_len is not None
     if args.batch is None:
@@ -91,9 +95,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local % ndev)
-    dev = torch.device("cuda", local % ndev)
+    if args.cpu:
+        dev = torch.device("cpu")
+        args.backend = "gloo"
+    else:
+        ndev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local % ndev)
+        dev = torch.device("cuda", local % ndev)
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -104,7 +112,10 @@ def main():
     from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
     from ray_torch_distributed_checkpoint_amd.ops import _ext
 
-    _ext.gpu_ext()  # native kernels are mandatory on the GPU path
+    if not args.cpu:
+        _ext.gpu_ext()  # native kernels are mandatory on the GPU path
+    sync = (lambda: None) if args.cpu else torch.cuda.synchronize
+    pre = preflight(world, rank, dev, args) if world > 1 else None
     torch.manual_seed(1234)
     wl = build_workload(args, dev, rank)
     model, opt = wl["model"], wl["opt"]
@@ -128,9 +139,11 @@ def main():
 
     from ray_torch_distributed_checkpoint_amd.utils.profiling import phase  # roctx ranges (--marker-trace)
 
+    cur = {"net": net}
+
     def step(i):
         with phase("fwd"):
-            loss = fwd_loss(net, i)
+            loss = fwd_loss(cur["net"], i)
         with phase("bwd"):
             loss.backward(seed)
         with phase("opt"):
@@ -140,17 +153,17 @@ def main():
 
     for i in range(args.warmup):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([dt], device=dev)
@@ -159,16 +172,26 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     samples_per_s = world * B * args.steps / dt
     final_loss = loss.item()
+    comm_plan = net.comm_plan() if world > 1 else None
+    # every rank must hold bitwise the same parameters (and, without ZeRO, optimizer state)
+    in_sync = ranks_in_sync(model, opt, world, dev) if world > 1 else None
 
     ck = {}
     if not args.no_ckpt:
         # the throughput above is measured and must be reported even if the checkpoint phase
         # fails (e.g. a filesystem that refuses the shard writes): the failure is reported too
         try:
-            ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp)
+            ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync)
         except Exception as e:  # noqa: BLE001
             ck = {"ckpt_unmeasured": f"checkpoint phase failed: {type(e).__name__}: {e}"[:300]}
             print(f"[bench] rank {rank}: {ck['ckpt_unmeasured']}", file=sys.stderr, flush=True)
+
+    sweep = None
+    if world > 1 and args.sweep and args.zero == 0 and not args.overlap_opt:
+        try:
+            sweep = comm_sweep(args, model, opt, net, cur, step, world, sync)
+        except Exception as e:  # noqa: BLE001
+            sweep = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     metric, published = _baseline_metric()
     base = published.get("samples_per_sec") if isinstance(published, dict) else None
@@ -197,11 +220,16 @@ def main():
     # self-description of the communication setup (what ran, on how many ranks)
     comm = {"world_size": world, "backend": (dist.get_backend() if world > 1 else None),
             "optimizer_overlapped_with_backward": overlap is not None,
-            "rccl_version": _rccl_version(), "device": torch.cuda.get_device_name(dev)}
+            "rccl_version": _rccl_version(),
+            "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"}
     if world > 1:
-        comm.update(net.comm_plan())
+        comm.update(comm_plan)
         comm["allreduce_GB_per_s_needed_at_this_step_time"] = round(
             comm["allreduce_bytes_per_step"] * 2 * (world - 1) / world / (ms_per_step / 1e3) / 1e9, 2)
+        comm["preflight"] = pre
+        if sweep is not None:
+            comm["sweep"] = sweep
+        out["ranks_in_sync"] = in_sync
     out["comm"] = comm
     out.update(ck)
     if rank == 0:
@@ -209,6 +237,115 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def preflight(world, rank, dev, args) -> dict:
+    """Before anything is timed: one all-reduce of a known tensor checked on EVERY rank (the
+    first time RCCL runs on a new node, a wrong result must stop the run, not skew it), the
+    peer-access matrix of the visible GPUs, and all-reduce bus bandwidth at three sizes
+    (xGMI evidence for the bucket sizing)."""
+    t = torch.full((1 << 20,), float(rank + 1), device=dev)
+    dist.all_reduce(t)
+    want = world * (world + 1) / 2
+    ok = bool((t == want).all().item())
+    flags = torch.tensor([1 if ok else 0], device=dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    res = {"allreduce_check_ok_all_ranks": bool(flags.item())}
+    if not res["allreduce_check_ok_all_ranks"]:
+        raise RuntimeError(f"preflight: all-reduce returned wrong values on some rank (rank {rank} ok={ok})")
+    if dev.type == "cuda":
+        n = torch.cuda.device_count()
+        res["peer_access"] = [[1 if i == j else int(torch.cuda.can_device_access_peer(i, j)) for j in range(n)]
+                              for i in range(n)]
+    bw = {}
+    sizes = (1 << 20, 32 << 20, 256 << 20) if dev.type == "cuda" else (1 << 20,)
+    for nbytes in sizes:
+        x = torch.ones(nbytes // 4, device=dev)
+        dist.all_reduce(x)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        iters = 5
+        for _ in range(iters):
+            dist.all_reduce(x)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+        tt = torch.tensor([dt], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+        bw[f"{nbytes >> 20}MB"] = {"ms": round(dt * 1e3, 3), "busbw_GBps": round(nbytes * 2 * (world - 1) / world / dt / 1e9, 2)}
+        del x
+    res["allreduce_fp32"] = bw
+    return res
+
+
+def _checksum(buf: torch.Tensor) -> list:
+    """Order-sensitive integer checksum of a float buffer's bits (chunked: bounded memory)."""
+    v = buf.detach().reshape(-1)
+    bits = v.view(torch.int32) if v.element_size() == 4 else v.view(torch.int16)
+    s1 = torch.zeros((), dtype=torch.int64, device=v.device)
+    s2 = torch.zeros((), dtype=torch.int64, device=v.device)
+    step = 1 << 26
+    for a in range(0, bits.numel(), step):
+        x = bits[a:a + step].to(torch.int64)
+        w = (torch.arange(a, a + x.numel(), device=v.device, dtype=torch.int64) % 1000003) + 1
+        s1 += x.sum()
+        s2 += (x * w).sum()
+    return [int(s1.item()), int(s2.item())]
+
+
+def ranks_in_sync(model, opt, world, dev) -> bool:
+    """Post-run cross-rank check: every rank holds bitwise the same parameters and (without
+    ZeRO-1, where each rank keeps only its own shards) the same optimizer state."""
+    sp = getattr(opt, "flat_space", None)
+    bufs = [sp.data] if sp is not None else [p.detach() for p in model.parameters()]
+    if sp is not None and sp.zero is None:
+        bufs += list(getattr(opt, "_bufs", {}).values())
+    mine = []
+    for b in bufs:
+        mine += _checksum(b)
+    t = torch.tensor(mine, dtype=torch.int64, device=dev)
+    lo, hi = t.clone(), t.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(lo, hi))
+
+
+def comm_sweep(args, model, opt, net, cur, step, world, sync) -> list:
+    """bucket_cap_mb x gradient dtype, a few steps each on this node's fabric: the xGMI
+    sizing evidence for the default plan (32 MiB fp32).  Re-wraps the same model (same flat
+    space and optimizer); the timed headline above is untouched."""
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+    out = []
+    net.detach()
+    for dtype in ("fp32", "bf16"):
+        for cap in (16.0, 32.0, 64.0, 128.0):
+            w = DistributedDataParallel(model, bucket_cap_mb=cap, defer_tail_to_optimizer=True, grad_comm_dtype=dtype)
+            cur["net"] = w
+            step(0)
+            sync()
+            dist.barrier()
+            t0 = time.perf_counter()
+            n = 3
+            for i in range(n):
+                step(i)
+            sync()
+            dist.barrier()
+            dt = (time.perf_counter() - t0) / n
+            tt = torch.tensor([dt], device=sp_device(model))
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            out.append({"bucket_cap_mb": cap, "grad_comm_dtype": dtype, "buckets": len(w.buckets),
+                        "ms_per_step": round(tt.item() * 1e3, 3)})
+            w.detach()
+    cur["net"] = net
+    return out
+
+
+def sp_device(model):
+    return next(model.parameters()).device
 
 
 def _rccl_version():
@@ -276,7 +413,7 @@ def build_workload(args, dev, rank):
                 flops_per_sample=model.flops_per_token(T) * T)
 
 
-def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
+def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     base = args.ckpt_dir or os.environ.get("RTDC_BENCH_CKPT_DIR") or tempfile.gettempdir()
     path = os.path.join(base, "rtdc_bench_ckpt")
     if rank == 0:
@@ -316,14 +453,14 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
         return {"ckpt_unmeasured": f"state larger than free disk ({free / 1e9:.0f} GB)"}
 
     # ---- async save overlapped with training steps
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     h = dcp.async_save(state(), path)
     t_resume = time.perf_counter() - t0  # training may continue from here
     t1 = time.perf_counter()
     for i in range(args.overlap_steps):
         step(i)
-    torch.cuda.synchronize()
+    sync()
     overlap_ms = (time.perf_counter() - t1) / max(1, args.overlap_steps) * 1e3
     local_write = h.wait()
     if world > 1:
@@ -343,7 +480,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
         shutil.rmtree(path2, ignore_errors=True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t2 = time.perf_counter()
     dcp.save(state(), path2)
     t_sync = time.perf_counter() - t2
@@ -351,27 +488,28 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     # right after the write), then cold (every shard dropped from the page cache with
     # posix_fadvise(DONTNEED) after its fsync, so the bytes come from the device)
     def restore():
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             dist.barrier()
         t3 = time.perf_counter()
         sd = state()
         dcp.load(sd, path2)
         set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             dist.barrier()
         return time.perf_counter() - t3
 
     t_restore_warm = restore()
-    dropped = drop_page_cache(path2)
+    resident = drop_page_cache(path2)
     if world > 1:
         dist.barrier()
     t_restore = restore()
-    vals = torch.tensor([t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm], device=dev)
+    vals = torch.tensor([t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm, resident],
+                        device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-    t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm = vals.tolist()
+    t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm, resident = vals.tolist()
     if rank == 0:
         shutil.rmtree(path, ignore_errors=True)
         shutil.rmtree(path2, ignore_errors=True)
@@ -382,7 +520,9 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
         "ckpt_save_durable_s": round(t_durable, 4),
         "ckpt_save_sync_s": round(t_sync, 4),
         "ckpt_restore_s": round(t_restore, 4),
-        "ckpt_restore_cold": dropped,
+        "ckpt_restore_collectives": dcp.LAST_LOAD_COLLECTIVES,  # coalesced broadcasts of the last restore
+        "ckpt_restore_cold": resident < 0.01,
+        "ckpt_restore_resident_frac": round(resident, 4),  # measured by mincore before the cold restore
         "ckpt_restore_warm_s": round(t_restore_warm, 4),
         "ckpt_save_plus_restore_s": round(t_sync + t_restore, 4),
         "ckpt_write_GBps": round(total / max(t_sync, 1e-9) / 1e9, 3),
@@ -397,21 +537,15 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp):
     return out
 
 
-def drop_page_cache(path: str) -> bool:
-    """posix_fadvise(DONTNEED) every (fsynced, hence clean) shard so the next read is cold.
-    False when the files live on a RAM-backed filesystem, where there is no cold read."""
-    ok = True
-    for root, _dirs, files in os.walk(path):
-        for name in files:
-            fd = os.open(os.path.join(root, name), os.O_RDONLY)
-            try:
-                os.fsync(fd)
-                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
-            finally:
-                os.close(fd)
-    if _fs_of(path) in ("tmpfs", "ramfs"):
-        ok = False
-    return ok
+def drop_page_cache(path: str) -> float:
+    """fsync + posix_fadvise(DONTNEED) every shard, then MEASURE how much of the checkpoint is
+    still in the page cache (mincore over an mmap of each file): the returned resident
+    fraction is what makes the next restore cold or not (0.0 = every byte comes from the
+    device).  On tmpfs/ramfs the pages cannot be dropped and the fraction stays ~1.0."""
+    from ray_torch_distributed_checkpoint_amd.utils import pagecache
+
+    pagecache.drop(path)
+    return pagecache.resident_fraction(path)
 
 
 def _fs_of(path: str) -> str:

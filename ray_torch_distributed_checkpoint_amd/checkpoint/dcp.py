@@ -28,6 +28,7 @@ import io
 import os
 import pickle
 import struct
+import threading
 import time
 import uuid
 
@@ -104,14 +105,32 @@ class _Item:
     nbytes: int
     tensor: torch.Tensor | None = None
     data: bytes | None = None
+    chunk: tuple | None = None        # (offsets, sizes, global shape) of a shard of a sharded value
+    owner: int | None = None          # writer rank fixed by the value's layout (sharded values)
 
 
-def _collect(state_dict):
+def _collect(state_dict, world: int = 1, rank: int = 0):
+    """Flatten a state dict into write items.  Replicated tensors / bytes get their owner from
+    the balanced plan later; `FlatShardedTensor` values (ZeRO-1 optimizer state) expand into
+    one item per hyper-rectangular piece of every rank's flat ranges, owned by that rank -
+    other ranks' pieces carry meta tensors (shape + dtype are all the file layout needs)."""
+    from .sharded import FlatShardedTensor
+
     sd = _resolve_stateful(state_dict)
     flat, mapping = flatten_state_dict(sd)
     items = []
     for fqn, v in flat.items():
-        if torch.is_tensor(v):
+        if isinstance(v, FlatShardedTensor):
+            if v.world != world:
+                raise ValueError(f"{fqn}: sharded over {v.world} ranks but saving with world size {world}")
+            esz = torch.empty((), dtype=v.dtype).element_size()
+            mine = {tuple(off): t for off, _sz, t in v.local_piece_tensors()}
+            for r in range(world):
+                for off, sz, _fs, n in v.pieces_of(r):
+                    t = mine[tuple(off)].detach() if r == rank else torch.empty(sz, dtype=v.dtype, device="meta")
+                    items.append(_Item(fqn, "tensor", n * esz, tensor=t, chunk=(tuple(off), tuple(sz), tuple(v.shape)),
+                                       owner=r))
+        elif torch.is_tensor(v):
             t = v.detach()
             items.append(_Item(fqn, "tensor", t.numel() * t.element_size(), tensor=t))
         else:
@@ -143,18 +162,30 @@ class AsyncSave:
         self.checkpoint_id, self._h, self._metadata = checkpoint_id, handle, metadata
         self.rank, self.t_start, self.t_return, self.nbytes, self.pg = rank, t_start, t_return, nbytes, pg
         self.write_s = None
+        self._error: BaseException | None = None
+        # waited on by the training loop and by the session's committer thread
+        self._lock = threading.Lock()
 
     def wait(self) -> float:
-        """Local shard durable.  Returns seconds since the save call."""
-        if self._h is not None:
-            self._h.wait()
-            self._h = None
-        if self.write_s is None:
-            self.write_s = time.perf_counter() - self.t_start
-        if getattr(self, "_verify", None):
-            _verify_written(self._verify)
-            self._verify = None
-        return self.write_s
+        """Local shard durable.  Returns seconds since the save call.  The outcome is cached
+        under a lock: concurrent and repeated waiters all get the same result, and a failed
+        write (or verify) raises for every one of them."""
+        with self._lock:
+            if self._error is None and self.write_s is None:
+                try:
+                    if self._h is not None:
+                        self._h.wait()
+                    if getattr(self, "_verify", None):
+                        _verify_written(self._verify)
+                        self._verify = None
+                    self.write_s = time.perf_counter() - self.t_start
+                except BaseException as e:  # noqa: BLE001
+                    self._error = e
+                finally:
+                    self._h = None
+            if self._error is not None:
+                raise IOError(f"sharded save to {self.checkpoint_id} failed: {self._error}") from self._error
+            return self.write_s
 
     def _finish(self):
         """Rank 0: write `.metadata` atomically (call after every rank's wait())."""
@@ -204,17 +235,18 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     t0 = time.perf_counter()
     world, rank = _world(process_group)
     os.makedirs(checkpoint_id, exist_ok=True)
-    items, mapping = _collect(state_dict)
+    items, mapping = _collect(state_dict, world, rank)
+    rep = [it for it in items if it.owner is None]
     if replicated:
-        owner = _balanced_owner([(it.fqn, it.nbytes) for it in items], world)
-        all_items = items
+        owner = _balanced_owner([(it.fqn, it.nbytes) for it in rep], world)
     else:
-        # sharded state (e.g. per-rank shards): every rank writes its own items; fqns must be unique
-        owner = {it.fqn: rank for it in items}
-        all_items = items
+        # per-rank state (e.g. per-rank shards): every rank writes its own items; fqns must be unique
+        owner = {it.fqn: rank for it in rep}
+    for it in rep:
+        it.owner = owner[it.fqn]
     per_rank: dict[int, list[_Item]] = {r: [] for r in range(world)}
-    for it in all_items:
-        per_rank[owner[it.fqn]].append(it)
+    for it in items:
+        per_rank[it.owner].append(it)
     mine = per_rank[rank]
     # HBM / host snapshot of owned tensors: cloned in stream order on the compute stream
     for it in mine:
@@ -235,7 +267,15 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
             arcs = _archives_for(per_rank[r], with_ptrs=False)
             _, lay = ext.plan_layout(arcs)
             for it, (base, size, _recs) in zip(per_rank[r], lay):
-                if it.kind == "tensor":
+                if it.kind == "tensor" and it.chunk is not None:
+                    offs, sizes, gshape = it.chunk
+                    m = sd_md.get(it.fqn)
+                    if m is None:
+                        m = sd_md[it.fqn] = TensorStorageMetadata(
+                            properties=TensorProperties(dtype=it.tensor.dtype), size=torch.Size(gshape), chunks=[])
+                    storage[MetadataIndex(it.fqn, torch.Size(offs), len(m.chunks))] = _StorageInfo(fname, base, size)
+                    m.chunks.append(ChunkStorageMetadata(offsets=torch.Size(offs), sizes=torch.Size(sizes)))
+                elif it.kind == "tensor":
                     t = it.tensor
                     zeros = torch.Size([0] * t.dim())
                     sd_md[it.fqn] = TensorStorageMetadata(
@@ -403,6 +443,12 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
     missing = [k for k in flat if k not in md.state_dict_metadata]
     if missing:
         raise KeyError(f"checkpoint {checkpoint_id} is missing keys: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+    from .sharded import FlatShardedTensor
+
+    sharded_fqns = [k for k, v in flat.items() if isinstance(v, FlatShardedTensor)]
+    if sharded_fqns:
+        # every rank reads exactly the bytes of its own shards (no broadcast, any saved layout)
+        _load_sharded(flat, sharded_fqns, md, chunks_of, checkpoint_id, ext, threads)
     sizes = []
     for k in tensor_fqns:
         m = md.state_dict_metadata[k]
@@ -488,19 +534,12 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
                 region.copy_(src, non_blocking=dest.is_cuda)
         if dest_is_cuda(batch):
             torch.cuda.current_stream().synchronize()  # staging reuse
-    # ---- broadcast from readers
+    # ---- broadcast from readers, coalesced: each reader's tensors packed into <= 256 MB flat
+    # buffers per dtype (GPT-2's train state: ~450 per-tensor broadcasts -> a handful)
     if broadcast and world > 1:
-        for k in tensor_fqns:
-            t = flat[k]
-            if t.is_contiguous():
-                dist.broadcast(t, src=_global_rank(reader[k], process_group), group=process_group)
-            else:
-                tmp = t.contiguous()
-                dist.broadcast(tmp, src=_global_rank(reader[k], process_group), group=process_group)
-                with torch.no_grad():
-                    t.copy_(tmp)
+        _coalesced_broadcast([(flat[k], reader[k]) for k in tensor_fqns], world, process_group)
     # ---- non-tensor values (rank 0 reads, broadcasts as objects)
-    obj_keys = [k for k in flat if not torch.is_tensor(flat[k])]
+    obj_keys = [k for k in flat if not torch.is_tensor(flat[k]) and not isinstance(flat[k], FlatShardedTensor)]
     values = {}
     if obj_keys:
         if rank == 0 or not broadcast:
@@ -524,6 +563,136 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
     if flat and any(torch.is_tensor(v) and v.is_cuda for v in flat.values()):
         torch.cuda.current_stream().synchronize()
     return state_dict
+
+
+def _load_sharded(flat, fqns, md, chunks_of, checkpoint_id, ext, threads) -> None:
+    """Fill each FlatShardedTensor's local slices from the saved chunks that intersect them.
+    Saved chunks must be contiguous in row-major order (a whole tensor, or the pieces a
+    sharded save writes); the intersection is one byte range of the chunk's data record."""
+    from .sharded import chunk_flat_range
+
+    dev_reads: dict[str, tuple[list, list, list]] = {}
+    host_reads: dict[str, tuple[list, list, list]] = {}
+    handles: dict = {}
+    try:
+        for k in fqns:
+            v = flat[k]
+            mdt = md.state_dict_metadata[k]
+            if tuple(mdt.size) != tuple(v.shape):
+                raise ValueError(f"{k}: checkpoint shape {tuple(mdt.size)} != destination {tuple(v.shape)}")
+            if mdt.properties.dtype != v.dtype:
+                raise ValueError(f"{k}: checkpoint dtype {mdt.properties.dtype} != destination {v.dtype}")
+            esz = torch.empty((), dtype=v.dtype).element_size()
+            sizes_of = {tuple(c.offsets): tuple(c.sizes) for c in mdt.chunks}
+            covered = 0
+            for idx, info in chunks_of[k]:
+                fr = chunk_flat_range(idx.offset, sizes_of[tuple(idx.offset)], v.shape)
+                if fr is None:
+                    raise ValueError(f"{k}: chunk at {tuple(idx.offset)} is not contiguous in row-major order; a "
+                                     f"flat-sharded destination cannot read it")
+                cs, cn = fr
+                rec = None
+                for s0, t in v.local:
+                    lo, hi = max(s0, cs), min(s0 + t.numel(), cs + cn)
+                    if lo >= hi:
+                        continue
+                    path = os.path.join(checkpoint_id, info.relative_path)
+                    if rec is None:
+                        fh = handles.get(path)
+                        if fh is None:
+                            fh = handles[path] = open(path, "rb", buffering=0)
+                        rec = _zip_data_record(path, info.offset, info.length, fh)
+                    dst = t[lo - s0:hi - s0]
+                    group = dev_reads if (dst.is_cuda and torch.cuda.is_available()) else host_reads
+                    o, l_, d = group.setdefault(path, ([], [], []))
+                    o.append(rec[0] + (lo - cs) * esz)
+                    l_.append((hi - lo) * esz)
+                    d.append(dst.data_ptr())
+                    covered += hi - lo
+            if covered != v.local_numel():
+                raise ValueError(f"{k}: checkpoint chunks cover {covered} of this rank's {v.local_numel()} elements")
+    finally:
+        for fh in handles.values():
+            fh.close()
+    if dev_reads:
+        from . import torchsave
+
+        eng = torchsave.get_engine()
+        torch.cuda.current_stream().synchronize()
+        for path, (o, l_, d) in dev_reads.items():
+            eng.read_to_device(path, o, l_, d, threads)
+    for path, (o, l_, d) in host_reads.items():
+        ext.read_ranges(path, o, l_, d, threads)
+
+
+BCAST_CAP_BYTES = 256 << 20
+
+
+def _coalesced_broadcast(pairs, world, pg, cap: int = BCAST_CAP_BYTES) -> int:
+    """Broadcast each tensor from its reader rank, packing the tensors of one (reader, dtype,
+    device) into flat buffers of at most `cap` bytes (one collective each; tensors larger than
+    `cap` go alone, in place).  Order is identical on every rank.  Returns the number of
+    collectives issued."""
+    n_coll = 0
+    for src in range(world):
+        groups: dict = {}
+        for t, r in pairs:
+            if r == src:
+                groups.setdefault((t.dtype, t.device), []).append(t)
+        g_src = _global_rank(src, pg)
+        me = dist.get_rank(pg)
+        for (dtype, device), ts in groups.items():
+            esz = torch.empty((), dtype=dtype).element_size()
+            batch, used = [], 0
+
+            def flush(batch):
+                if not batch:
+                    return 0
+                if len(batch) == 1 and batch[0].is_contiguous():
+                    dist.broadcast(batch[0], src=g_src, group=pg)
+                    return 1
+                total = sum(x.numel() for x in batch)
+                buf = torch.empty(total, dtype=dtype, device=device)
+                if me == src:
+                    off = 0
+                    with torch.no_grad():
+                        for x in batch:
+                            buf[off:off + x.numel()].copy_(x.reshape(-1))
+                            off += x.numel()
+                dist.broadcast(buf, src=g_src, group=pg)
+                if me != src:
+                    off = 0
+                    with torch.no_grad():
+                        for x in batch:
+                            x.copy_(buf[off:off + x.numel()].view(x.shape))
+                            off += x.numel()
+                return 1
+
+            for t in ts:
+                nb = t.numel() * esz
+                if nb >= cap:
+                    if t.is_contiguous():
+                        dist.broadcast(t, src=g_src, group=pg)
+                    else:
+                        tmp = t.contiguous()
+                        dist.broadcast(tmp, src=g_src, group=pg)
+                        if me != src:
+                            with torch.no_grad():
+                                t.copy_(tmp)
+                    n_coll += 1
+                    continue
+                if used + nb > cap:
+                    n_coll += flush(batch)
+                    batch, used = [], 0
+                batch.append(t)
+                used += nb
+            n_coll += flush(batch)
+    global LAST_LOAD_COLLECTIVES
+    LAST_LOAD_COLLECTIVES = n_coll
+    return n_coll
+
+
+LAST_LOAD_COLLECTIVES = 0
 
 
 def dest_is_cuda(batch) -> bool:

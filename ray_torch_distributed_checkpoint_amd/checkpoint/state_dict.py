@@ -7,6 +7,9 @@ FQN instead of the process-local integer ids of `Optimizer.state_dict()` - ids a
 stable across model constructions, FQNs are, so a sharded `.metadata` written by one job
 loads into another.  `get_state_dict` materialises lazily-created optimizer state first, so
 the returned dict is a complete load target for `dcp.load` (which fills tensors in place).
+Under ZeRO-1 the fused optimizers' state values are `FlatShardedTensor`s over this rank's
+compact shards (checkpoint/sharded.py): `dcp.save` writes them as chunks and `dcp.load` reads
+only the intersecting bytes, so a sharded checkpoint never all-gathers the optimizer state.
 
     model_sd, optim_sd = get_state_dict(model, opt)
     dcp.save({"model": model_sd, "optim": optim_sd}, path)
@@ -90,8 +93,6 @@ def get_optimizer_state_dict(model: nn.Module, optimizers, *, options: StateDict
     for opt in _optims(optimizers):
         if any(p not in opt.state for g in opt.param_groups for p in g["params"]):
             _init_optim_state(opt)
-        if hasattr(opt, "consolidate_state"):
-            opt.consolidate_state()  # ZeRO-1 sharded state -> full state on every rank (collective)
         if hasattr(opt, "_materialize_steps"):
             opt._materialize_steps()  # fused optimizers keep step counts as host ints
         for g in opt.param_groups:
@@ -101,7 +102,11 @@ def get_optimizer_state_dict(model: nn.Module, optimizers, *, options: StateDict
             for p in g["params"]:
                 st = opt.state.get(p)
                 if st:
-                    state[names[p]] = dict(st)
+                    d = dict(st)
+                    if hasattr(opt, "checkpoint_value"):
+                        # ZeRO-1: FlatShardedTensor shards, written as DCP chunks (no all-gather)
+                        d = {k: opt.checkpoint_value(p, k, v) for k, v in d.items()}
+                    state[names[p]] = d
     return _maybe_cpu({"state": state, "param_groups": groups}, opts)
 
 

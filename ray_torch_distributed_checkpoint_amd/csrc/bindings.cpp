@@ -48,6 +48,10 @@ int rtdc_softmax_bwd(const void* P, const void* dP, void* dS, long long rows, in
                      hipStream_t st);
 int rtdc_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int ntok, int T, int D,
                    hipStream_t st);
+int rtdc_sort_ids(const int64_t* ids, int n, int nbits, uint32_t* ws, int64_t* sorted, int64_t* perm,
+                  hipStream_t st);
+int rtdc_synth_tokens(const int64_t* ids, int B, int T, long long vocab, unsigned long long seed_add, int64_t* inp,
+                      int64_t* tgt, hipStream_t st);
 int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe, int B, int T,
                    int D, int accumulate_wpe, int accumulate_wte, hipStream_t st);
 int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
@@ -265,9 +269,16 @@ static void xent(Tensor logits, c10::optional<Tensor> dlogits, c10::optional<Ten
 }
 
 // ---------------------------------------------------------------------------------- optim
+// chunk tables: int64 [n, 3] rows (start, len | decay << 32, state start) - kernels/optim.hip Chunk
+static void check_chunks(const Tensor& chunks, int64_t nchunks, const char* op) {
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong && chunks.is_contiguous() && chunks.dim() == 2 &&
+                  chunks.size(1) == 3 && chunks.size(0) >= nchunks,
+              op, ": chunk table must be a contiguous int64 [n, 3] GPU tensor");
+}
 static void adamw(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, Tensor m, Tensor v,
                   c10::optional<Tensor> shadow, double lr, double b1, double b2, double eps, double wd, double bc1,
                   double bc2_sqrt, double grad_scale) {
+  check_chunks(chunks, nchunks, "adamw");
   check_rc(rtdc_adamw(chunks.data_ptr(), (int)nchunks, p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                       v.data_ptr<float>(), ptr_or_null(shadow), (float)lr, (float)b1, (float)b2, (float)eps,
                       (float)wd, (float)bc1, (float)bc2_sqrt, (float)grad_scale, cur_stream()),
@@ -276,6 +287,7 @@ static void adamw(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, Tensor m, 
 static void sgd(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, c10::optional<Tensor> buf,
                 c10::optional<Tensor> shadow, double lr, double momentum, double dampening, double wd,
                 bool nesterov, bool first, double grad_scale) {
+  check_chunks(chunks, nchunks, "sgd");
   check_rc(rtdc_sgd(chunks.data_ptr(), (int)nchunks, p.data_ptr<float>(), g.data_ptr<float>(),
                     (float*)ptr_or_null(buf), ptr_or_null(shadow), (float)lr, (float)momentum, (float)dampening,
                     (float)wd, nesterov, first, (float)grad_scale, cur_stream()),
@@ -285,6 +297,7 @@ static void f32_to_bf16(Tensor x, Tensor y) {
   check_rc(rtdc_f32_to_bf16(x.data_ptr<float>(), y.data_ptr(), (long long)x.numel(), cur_stream()), "f32_to_bf16");
 }
 static void sumsq(Tensor chunks, int64_t nchunks, Tensor g, Tensor partial) {
+  check_chunks(chunks, nchunks, "sumsq");
   check_rc(rtdc_sumsq(chunks.data_ptr(), (int)nchunks, g.data_ptr<float>(), partial.data_ptr<float>(), cur_stream()),
            "sumsq");
 }
@@ -305,6 +318,32 @@ static void embed_fwd(Tensor idx, Tensor wte, c10::optional<Tensor> wpe, Tensor 
   check_rc(rtdc_embed_fwd(idx.data_ptr<int64_t>(), wte.data_ptr(), ptr_or_null(wpe), out.data_ptr(),
                           (int)idx.numel(), (int)T, D, cur_stream()),
            "embed_fwd");
+}
+// stable sort of token ids (< 2^nbits): sorted ids + original positions, one workgroup
+static void sort_ids(Tensor ids, Tensor sorted, Tensor perm, Tensor ws, int64_t nbits) {
+  const int64_t n = ids.numel();
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous(), "sort_ids: ids must be contiguous int64 on the GPU");
+  TORCH_CHECK(sorted.numel() == n && perm.numel() == n && sorted.scalar_type() == at::kLong &&
+                  perm.scalar_type() == at::kLong && sorted.is_contiguous() && perm.is_contiguous(),
+              "sort_ids: outputs must be contiguous int64 of ids.numel()");
+  TORCH_CHECK(ws.numel() * ws.element_size() >= 16 * n && ws.is_contiguous(), "sort_ids: workspace needs 16 B per id");
+  TORCH_CHECK(n < (1LL << 31), "sort_ids: too many ids");
+  check_rc(rtdc_sort_ids(ids.data_ptr<int64_t>(), (int)n, (int)nbits, (uint32_t*)ws.data_ptr(),
+                         sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), cur_stream()),
+           "sort_ids");
+}
+// inputs/targets [B, T] int64 of the synthetic sequences ids[B] (workloads.SyntheticTokens)
+static void synth_tokens(Tensor ids, Tensor inp, Tensor tgt, int64_t vocab, int64_t seed_add) {
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.dim() == 1,
+              "synth_tokens: ids must be a contiguous 1-D int64 GPU tensor");
+  const int64_t B = ids.numel();
+  TORCH_CHECK(inp.dim() == 2 && inp.size(0) == B && tgt.sizes() == inp.sizes() && inp.is_contiguous() &&
+                  tgt.is_contiguous() && inp.scalar_type() == at::kLong && tgt.scalar_type() == at::kLong,
+              "synth_tokens: inp/tgt must be contiguous int64 [B, T]");
+  check_rc(rtdc_synth_tokens(ids.data_ptr<int64_t>(), (int)B, (int)inp.size(1), (long long)vocab,
+                             (unsigned long long)seed_add, inp.data_ptr<int64_t>(), tgt.data_ptr<int64_t>(),
+                             cur_stream()),
+           "synth_tokens");
 }
 // sidx / perm: stably sorted token ids and their original positions (deterministic backward)
 static void embed_bwd(Tensor sidx, Tensor perm, Tensor dout, Tensor dwte, c10::optional<Tensor> dwpe, int64_t B,
@@ -741,6 +780,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
   m.def("embed_fwd", &embed_fwd);
+  m.def("sort_ids", &sort_ids);
+  m.def("synth_tokens", &synth_tokens);
   m.def("embed_bwd", &embed_bwd, py::arg("sidx"), py::arg("perm"), py::arg("dout"), py::arg("dwte"), py::arg("dwpe"),
         py::arg("B"), py::arg("T"), py::arg("accumulate_wpe"), py::arg("accumulate_wte") = false);
   m.def("dropout", &dropout);

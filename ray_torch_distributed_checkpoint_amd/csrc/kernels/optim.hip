@@ -9,16 +9,22 @@
 //
 // AdamW: fp32 master + m + v, optional bf16 shadow written in the same pass (the copy the
 // bf16 MFMA kernels read).  grad_scale folds the DDP 1/world pre-divide into the step.
+// A chunk carries two offsets: `start` into the flat parameter / gradient / shadow buffers and
+// `sstart` into the optimizer-state buffers.  Without ZeRO they are equal; under ZeRO-1 the
+// state buffers hold only this rank's owned shards back to back (1/world of the bytes), so
+// `sstart` is the chunk's position in that compact buffer.
 // Semantics follow torch.optim.AdamW / SGD (decoupled weight decay; SGD first-step clone).
 #include "common.h"
 
 namespace rtdc {
 
 struct Chunk {
-  long long start;
+  long long start;   // offset into p / g / shadow
   int len;
   int decay;
+  long long sstart;  // offset into the optimizer state (m, v / momentum buffer)
 };
+static_assert(sizeof(Chunk) == 24, "chunk table rows are 3 x int64");
 
 __global__ __launch_bounds__(256) void adamw_kernel(const Chunk* __restrict__ chunks, int nchunks,
                                                    float* __restrict__ p, const float* __restrict__ g,
@@ -31,10 +37,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(const Chunk* __restrict__ ch
     const Chunk c = chunks[ci];
     const float decay = c.decay ? (1.f - lr * wd) : 1.f;
     for (int i = threadIdx.x * 4; i < c.len; i += 256 * 4) {
-      const long long o = c.start + i;
+      const long long o = c.start + i, so = c.sstart + i;
       if (i + 4 <= c.len) {
         f32x4 pp = *(f32x4*)(p + o), gg = *(const f32x4*)(g + o);
-        f32x4 mm = *(f32x4*)(m + o), vv = *(f32x4*)(v + o);
+        f32x4 mm = *(f32x4*)(m + so), vv = *(f32x4*)(v + so);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float gr = gg[e] * grad_scale;
@@ -46,18 +52,18 @@ __global__ __launch_bounds__(256) void adamw_kernel(const Chunk* __restrict__ ch
           pp[e] = pe;
         }
         *(f32x4*)(p + o) = pp;
-        *(f32x4*)(m + o) = mm;
-        *(f32x4*)(v + o) = vv;
+        *(f32x4*)(m + so) = mm;
+        *(f32x4*)(v + so) = vv;
         if (shadow) *(uint2*)(shadow + o) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
       } else {
         for (int e = 0; e < 4 && i + e < c.len; ++e) {
-          const long long oe = o + e;
+          const long long oe = o + e, se = so + e;
           const float gr = g[oe] * grad_scale;
           float pe = p[oe] * decay;
-          m[oe] = b1 * m[oe] + (1.f - b1) * gr;
-          v[oe] = b2 * v[oe] + (1.f - b2) * gr * gr;
-          const float denom = sqrtf(v[oe]) / bc2_sqrt + eps;
-          pe -= step_size * m[oe] / denom;
+          m[se] = b1 * m[se] + (1.f - b1) * gr;
+          v[se] = b2 * v[se] + (1.f - b2) * gr * gr;
+          const float denom = sqrtf(v[se]) / bc2_sqrt + eps;
+          pe -= step_size * m[se] / denom;
           p[oe] = pe;
           if (shadow) shadow[oe] = f2bf(pe);
         }
@@ -85,14 +91,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(const Chunk* __restrict__ chun
       }
       pe -= lr * d;
     };
-    const bool vec = (c.start & 3) == 0;
+    const bool vec = (c.start & 3) == 0 && (c.sstart & 3) == 0;
     // 4 elements per lane and iteration (16-B loads of p, g and the momentum buffer)
     for (int i = threadIdx.x * 4; i < c.len; i += 256 * 4) {
-      const long long o = c.start + i;
+      const long long o = c.start + i, so = c.sstart + i;
       if (vec && i + 4 <= c.len) {
         f32x4 pp = *(f32x4*)(p + o);
         const f32x4 gg = *(const f32x4*)(g + o);
-        f32x4 bb = (momentum != 0.f && !first) ? *(f32x4*)(buf + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 bb = (momentum != 0.f && !first) ? *(f32x4*)(buf + so) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float pe = pp[e], b = bb[e];
@@ -101,14 +107,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(const Chunk* __restrict__ chun
           bb[e] = b;
         }
         *(f32x4*)(p + o) = pp;
-        if (momentum != 0.f) *(f32x4*)(buf + o) = bb;
+        if (momentum != 0.f) *(f32x4*)(buf + so) = bb;
         if (shadow) *(uint2*)(shadow + o) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
       } else {
         for (int e = 0; e < 4 && i + e < c.len; ++e) {
-          const long long oe = o + e;
-          float pe = p[oe], b = (momentum != 0.f && !first) ? buf[oe] : 0.f;
+          const long long oe = o + e, se = so + e;
+          float pe = p[oe], b = (momentum != 0.f && !first) ? buf[se] : 0.f;
           upd(g[oe], pe, b);
-          if (momentum != 0.f) buf[oe] = b;
+          if (momentum != 0.f) buf[se] = b;
           p[oe] = pe;
           if (shadow) shadow[oe] = f2bf(pe);
         }

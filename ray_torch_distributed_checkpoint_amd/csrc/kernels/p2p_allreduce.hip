@@ -16,7 +16,8 @@
 // call e + 1, which every peer can only publish after finishing call e's reads.
 // Uncached staging means no L2 on any XCD ever holds a stale or dirty copy of it.
 // The wait is BOUNDED (wall_clock64, 100 MHz): on timeout the kernel records an error in a
-// host-visible word and exits, so a missing peer can never leave waves spinning on the GPU.
+// host-visible word, fills the bucket with NaN (never a silently un-reduced gradient) and
+// exits, so a missing peer can never leave waves spinning on the GPU.
 #include "common.h"
 
 namespace rtdc {
@@ -59,10 +60,18 @@ __global__ __launch_bounds__(256) void oneshot_kernel(Peers peers, int world, in
     bad = timed_out;
   }
   __syncthreads();
-  if (bad) return;
-  const long long off = FLAG_BYTES + (long long)(epoch & 1u) * cap;
   constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
   const long long nv = n / V;
+  if (bad) {
+    // a peer never arrived: poison this rank's bucket with NaN instead of leaving the local,
+    // un-reduced gradient in place (which would let the optimizer silently apply a
+    // rank-dependent update); the host raises on the error word at the next finalize
+    const uint4 qnan = sizeof(T) == 4 ? make_uint4(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u)
+                                      : make_uint4(0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u);
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) ((uint4*)out)[i] = qnan;
+    return;
+  }
+  const long long off = FLAG_BYTES + (long long)(epoch & 1u) * cap;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
     float acc[8];
 #pragma unroll

@@ -441,22 +441,36 @@ class Engine {
   bool poll(int id) {
     std::lock_guard<std::mutex> lk(jmu_);
     auto it = jobs_.find(id);
-    if (it == jobs_.end()) return true;
+    if (it == jobs_.end()) {
+      if (results_.count(id)) return true;
+      throw std::runtime_error("poll: unknown checkpoint job id " + std::to_string(id));
+    }
     return it->second->done;
   }
 
-  // returns (error, seconds from submit to durable)
+  // returns (error, seconds from submit to durable).  A finished job's outcome is kept (the
+  // job itself - its staged buffers - is released), so a second waiter on the same id gets the
+  // same answer - in particular the same error - instead of "unknown id == success".
   std::pair<std::string, double> wait(int id) {
-    std::shared_ptr<SaveJob> job;
-    {
-      std::unique_lock<std::mutex> lk(jmu_);
-      auto it = jobs_.find(id);
-      if (it == jobs_.end()) return {"", 0.0};
-      job = it->second;
-      jcv_.wait(lk, [&] { return job->done; });
-      jobs_.erase(id);
+    std::unique_lock<std::mutex> lk(jmu_);
+    auto it = jobs_.find(id);
+    if (it == jobs_.end()) {
+      auto r = results_.find(id);
+      if (r != results_.end()) return r->second;
+      throw std::runtime_error("wait: unknown checkpoint job id " + std::to_string(id));
     }
-    return {job->error, job->t_done - job->t_submit};
+    std::shared_ptr<SaveJob> job = it->second;
+    jcv_.wait(lk, [&] { return job->done; });
+    std::pair<std::string, double> res{job->error, job->t_done - job->t_submit};
+    if (jobs_.erase(id)) {
+      results_[id] = res;
+      result_order_.push_back(id);
+      while (result_order_.size() > 4096) {  // bounded history of finished jobs
+        results_.erase(result_order_.front());
+        result_order_.pop_front();
+      }
+    }
+    return res;
   }
 
   size_t slot_bytes() const { return ring_.slot_bytes(); }
@@ -786,6 +800,8 @@ class Engine {
   std::deque<std::shared_ptr<SaveJob>> save_q_;
   std::deque<WJob> wq_;
   std::map<int, std::shared_ptr<SaveJob>> jobs_;
+  std::map<int, std::pair<std::string, double>> results_;  // outcomes of waited (finished) jobs
+  std::deque<int> result_order_;
   int next_id_ = 1;
   std::atomic<bool> stop_{false};
   bool wstop_ = false;

@@ -3,7 +3,9 @@
 The token-table gradient is a scatter-add where rows repeat; instead of float atomics (whose
 summation order changes run to run) the token ids are stably sorted once and the native
 kernel sums each run of equal ids in original token order: bitwise-reproducible gradients,
-required for bit-exact resume (BASELINE config 5)."""
+required for bit-exact resume (BASELINE config 5).  The sort is the native
+one-workgroup radix sort (`data_ops.hip` sort_ids) on a side stream under the forward pass -
+no rocprim / ATen sort kernels in the step."""
 from __future__ import annotations
 
 import torch
@@ -15,6 +17,17 @@ from .shadow import shadow_of
 
 
 _side: dict = {}
+
+
+def sort_ids(ids: torch.Tensor, num_rows: int):
+    """(sorted ids, original positions) of a 1-D int64 GPU tensor of ids in [0, num_rows):
+    stable, deterministic, one native kernel launch."""
+    n = ids.numel()
+    sidx = torch.empty(n, dtype=torch.int64, device=ids.device)
+    perm = torch.empty(n, dtype=torch.int64, device=ids.device)
+    ws = torch.empty(4 * max(n, 1), dtype=torch.int32, device=ids.device)
+    gpu_ext().sort_ids(ids, sidx, perm, ws, max(1, int(num_rows - 1).bit_length()))
+    return sidx, perm
 
 
 def _side_stream(device) -> torch.cuda.Stream:
@@ -41,7 +54,7 @@ class _Embedding(torch.autograd.Function):
             side = _side_stream(idx.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
-                sidx, perm = torch.sort(idx_c.reshape(-1), stable=True)
+                sidx, perm = sort_ids(idx_c.reshape(-1), wte.shape[0])
                 done = torch.cuda.Event()
                 done.record(side)
             sidx.record_stream(cur)
@@ -77,7 +90,7 @@ class _Embedding(torch.autograd.Function):
             sidx, perm, done = ctx.sorted
             torch.cuda.current_stream(idx.device).wait_event(done)
         else:
-            sidx, perm = torch.sort(idx.reshape(-1), stable=True)
+            sidx, perm = sort_ids(idx.reshape(-1), wte_shape[0])
         gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)
         return None, (None if accumulate else dwte), dwpe, None
 

@@ -39,18 +39,44 @@ class ZeroLayout:
     """ZeRO-1 ownership of a flat space (parallel/ddp.py `zero_stage=1`): every gradient bucket
     [start, end) - a multiple of 64 x world elements long - is split into `world` equal shards,
     rank r owns shard r of each.  The data-parallel engine reduce-scatters each bucket onto its
-    owner, the fused optimizer updates owned elements only, and `gather` all-gathers a flat
-    buffer (parameters after every step, optimizer state for a checkpoint) back to every rank."""
+    owner, the fused optimizer updates owned elements only and keeps its state for them alone
+    in COMPACT buffers (owned shards back to back: 1/world of the bytes), and `gather`
+    all-gathers a flat buffer (parameters after every step) back to every rank.
+
+    The layout is a pure function of (bucket plan, world), so every rank knows every other
+    rank's shards: sharded checkpoints are planned without collectives (checkpoint/sharded.py).
+    """
 
     def __init__(self, buckets, rank: int, world: int, group=None):
         self.buckets = [(int(a), int(b)) for a, b in buckets]
         self.rank, self.world, self.group = rank, world, group
-        self.owned = []
+        self.owned = self.owned_by(rank)
+        # compact position of each owned range (the optimizer-state offset of its first element)
+        self.compact_starts = []
+        c = 0
+        for oa, ob in self.owned:
+            self.compact_starts.append(c)
+            c += ob - oa
+        self.compact_numel = c
+
+    def owned_by(self, rank: int) -> list:
+        out = []
         for a, b in self.buckets:
             n = b - a
-            assert n % (64 * world) == 0, "ZeRO buckets must be multiples of 64 x world elements"
-            sh = n // world
-            self.owned.append((a + rank * sh, a + (rank + 1) * sh))
+            assert n % (64 * self.world) == 0, "ZeRO buckets must be multiples of 64 x world elements"
+            sh = n // self.world
+            out.append((a + rank * sh, a + (rank + 1) * sh))
+        return out
+
+    def compact_of(self, flat: int) -> int:
+        """Compact (optimizer-state) offset of an owned flat offset."""
+        import bisect
+
+        i = bisect.bisect_right([oa for oa, _ in self.owned], flat) - 1
+        oa, ob = self.owned[i]
+        if not (oa <= flat < ob):
+            raise ValueError(f"flat offset {flat} is not owned by rank {self.rank}")
+        return self.compact_starts[i] + flat - oa
 
     def gather(self, buf: torch.Tensor) -> None:
         """Every bucket of `buf`: each rank's owned shard -> all ranks (in place)."""
@@ -59,8 +85,15 @@ class ZeroLayout:
         for (a, b), (oa, ob) in zip(self.buckets, self.owned):
             dist.all_gather_into_tensor(buf[a:b], buf[oa:ob], group=self.group)
 
+    def gather_compact(self, compact: torch.Tensor, full: torch.Tensor) -> None:
+        """All-gather a compact owned-shard buffer into a full flat buffer on every rank."""
+        import torch.distributed as dist
+
+        for (a, b), (oa, ob), c in zip(self.buckets, self.owned, self.compact_starts):
+            dist.all_gather_into_tensor(full[a:b], compact[c:c + (ob - oa)], group=self.group)
+
     def owned_elements(self) -> int:
-        return sum(b - a for a, b in self.owned)
+        return self.compact_numel
 
 
 class FlatParamSpace:
@@ -228,10 +261,25 @@ class FlatParamSpace:
                 out.append((lo, hi))
         return out
 
+    def state_offset(self, flat: int) -> int:
+        """Optimizer-state offset of flat offset `flat` (compact under ZeRO-1)."""
+        return flat if self.zero is None else self.zero.compact_of(flat)
+
+    @property
+    def state_numel(self) -> int:
+        """Elements of one optimizer-state buffer: the whole space, or the owned shards."""
+        return self.numel if self.zero is None else self.zero.compact_numel
+
     def _chunks(self, s: Segment, d):
         for a, b in self._ranges(s):
+            so = self.state_offset(a)
             for st in range(a, b, CHUNK):
-                yield st, min(CHUNK, b - st) | (int(bool(d)) << 32)
+                yield st, min(CHUNK, b - st) | (int(bool(d)) << 32), so + (st - a)
+
+    def owned_ranges(self, s: Segment) -> list:
+        """[(flat start, flat end, state start)] of segment s this rank owns (all of it without
+        ZeRO).  The fused optimizers' per-parameter state is these slices of the state buffers."""
+        return [(a, b, self.state_offset(a)) for a, b in self._ranges(s)]
 
     def chunk_table_split(self, params_subset, decay_flags, split: int):
         """Two chunk tables: segments below flat offset `split`, and the rest."""
@@ -243,13 +291,15 @@ class FlatParamSpace:
         for p, d in zip(params_subset, decay_flags):
             s = self.segment_of(p)
             (lo if s.offset < split else hi).extend(self._chunks(s, d))
-        out = tuple((torch.tensor(r if r else [(0, 0)], dtype=torch.int64).to(self.device), len(r)) for r in (lo, hi))
+        out = tuple((torch.tensor(r if r else [(0, 0, 0)], dtype=torch.int64).to(self.device), len(r))
+                    for r in (lo, hi))
         self._chunk_cache[key] = out
         return out
 
     def chunk_table(self, params_subset, decay_flags) -> tuple[torch.Tensor, int]:
-        """int64 [nchunks, 2] rows of (start, len | decay<<32) for the native optimizer kernels
-        (only this rank's owned elements under ZeRO-1)."""
+        """int64 [nchunks, 3] rows of (start, len | decay<<32, state start) for the native
+        optimizer kernels (only this rank's owned elements under ZeRO-1, whose state lives in
+        compact buffers)."""
         key = (tuple(id(p) for p in params_subset), tuple(decay_flags))
         hit = self._chunk_cache.get(key)
         if hit is not None:
@@ -257,7 +307,7 @@ class FlatParamSpace:
         rows = []
         for p, d in zip(params_subset, decay_flags):
             rows.extend(self._chunks(self.segment_of(p), d))
-        t = torch.tensor(rows if rows else [(0, 0)], dtype=torch.int64).to(self.device)
+        t = torch.tensor(rows if rows else [(0, 0, 0)], dtype=torch.int64).to(self.device)
         out = (t, len(rows))
         self._chunk_cache[key] = out
         return out

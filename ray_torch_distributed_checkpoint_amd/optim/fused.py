@@ -35,6 +35,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._bound: set = set()
         self._have = None  # parameters with a gradient this step (set by the native step)
         self._overlap = None  # optim.overlap.BackwardOverlap (updates run during backward)
+        # DistributedDataParallel(zero_stage=1) leaves p.grad reduced only on this rank's shards:
+        # only these optimizers (which update exactly the owned shards) may step such a model
+        for p in self._all_params():
+            p._rtdc_zero_capable = True
 
     # -- flat setup ------------------------------------------------------------------------
     def _all_params(self):
@@ -54,31 +58,105 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 else:
                     p.grad = None
         self._space = sp
+        # optimizer state: the whole flat space, or (ZeRO-1) only this rank's owned shards,
+        # back to back - 1/world of the bytes (FlatParamSpace.state_numel)
         for k in self._state_keys:
-            self._bufs[k] = torch.zeros(sp.numel, dtype=torch.float32, device=sp.device)
+            self._bufs[k] = torch.zeros(sp.state_numel, dtype=torch.float32, device=sp.device)
         # adopt any state that already exists (e.g. loaded before the first step)
         for p in params:
             st = self.state.get(p)
-            seg = sp.segment_of(p)
             if st is None:
                 continue
             for k in self._state_keys:
-                if k in st and torch.is_tensor(st[k]):
-                    v = FlatParamSpace.view(self._bufs[k], seg)
-                    v.copy_(st[k].to(v.device, v.dtype))
-                    st[k] = v
+                if k in st and st[k] is not None:
+                    self._adopt(p, k, st[k])
+                    st[k] = self._state_value(p, k)
         return sp
+
+    # -- per-parameter state views -------------------------------------------------------------
+    def _zero(self):
+        sp = self._space
+        return None if sp is None else sp.zero
+
+    def _state_value(self, p, k):
+        """What `self.state[p][k]` holds: a view of the flat state buffer, or under ZeRO-1 a
+        `FlatShardedTensor` over this rank's compact slices (checkpoint/sharded.py) - the value
+        a sharded checkpoint writes and reads without any all-gather."""
+        sp = self._space
+        seg = sp.segment_of(p)
+        z = sp.zero
+        if z is None:
+            return FlatParamSpace.view(self._bufs[k], seg)
+        from ..checkpoint.sharded import FlatShardedTensor
+
+        buf = self._bufs[k]
+        local = [(a - seg.offset, buf[so:so + (b - a)]) for a, b, so in sp.owned_ranges(seg)]
+        lo, hi = seg.offset, seg.offset + seg.numel
+        ranges = []
+        for r in range(z.world):
+            rr = []
+            for oa, ob in z.owned_by(r):
+                a, b = max(lo, oa), min(hi, ob)
+                if a < b:
+                    rr.append((a - lo, b - lo))
+            ranges.append(rr)
+        return FlatShardedTensor(seg.shape, torch.float32, local, ranges, z.rank)
+
+    def _adopt(self, p, k, v) -> None:
+        """Copy a loaded/pre-existing state value into this optimizer's buffers (no-op when it
+        already views them).  `v`: a full tensor of the parameter's shape, or a
+        FlatShardedTensor whose local pieces cover this rank's owned ranges."""
+        from ..checkpoint.sharded import FlatShardedTensor
+
+        sp = self._space
+        seg = sp.segment_of(p)
+        buf = self._bufs[k]
+        if isinstance(v, FlatShardedTensor):
+            have = {s: t for s, t in v.local}
+            for a, b, so in sp.owned_ranges(seg):
+                t = have.get(a - seg.offset)
+                if t is None or t.numel() != b - a:
+                    raise ValueError(f"optimizer state {k!r}: sharded value does not cover owned range {a}-{b}")
+                dst = buf[so:so + (b - a)]
+                if t.data_ptr() != dst.data_ptr():
+                    with torch.no_grad():
+                        dst.copy_(t.reshape(-1).to(dst.device, dst.dtype))
+            return
+        if not torch.is_tensor(v):
+            return
+        if sp.zero is None:
+            dst = FlatParamSpace.view(buf, seg)
+            if v.data_ptr() != dst.data_ptr():
+                with torch.no_grad():
+                    dst.copy_(v.to(dst.device, dst.dtype))
+            return
+        # a full (replicated-layout) tensor: keep the owned ranges of its storage-order elements
+        full = v.detach().to(buf.device, buf.dtype)
+        if seg.channels_last:
+            o, i, kh, kw = seg.shape
+            full = full.permute(0, 2, 3, 1).contiguous()
+        flat = full.reshape(-1)
+        with torch.no_grad():
+            for a, b, so in sp.owned_ranges(seg):
+                buf[so:so + (b - a)].copy_(flat[a - seg.offset:b - seg.offset])
 
     def _bind_state(self, p):
         if p in self._bound:
             return self.state[p]
         st = self.state[p]
-        seg = self._space.segment_of(p)
         for k in self._state_keys:
             if k not in st:
-                st[k] = FlatParamSpace.view(self._bufs[k], seg)
+                st[k] = self._state_value(p, k)
         self._bound.add(p)
         return st
+
+    def _flat_mode(self) -> bool:
+        """Updates run over the flat buffers' chunk tables: always on the GPU (native kernels),
+        and on the CPU under ZeRO-1 (owned shards only, compact state - reference path)."""
+        if self._use_native():
+            return True
+        sp = space_of(self._all_params())
+        return sp is not None and sp.zero is not None
 
     @torch.no_grad()
     def init_state(self) -> None:
@@ -88,9 +166,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
         with a zero-grad step, T/distributed/checkpoint/state_dict.py `_init_optim_state`).
         Numerically a no-op for AdamW; for SGD a zero momentum buffer equals torch's
         first-step `buf = g` whenever dampening == 0."""
+        flat = self._flat_mode()
         for p in self._all_params():
             st = self.state[p]
-            if self._use_native():
+            if flat:
                 self._ensure_space()
                 self._bind_state(p)
             else:
@@ -111,18 +190,65 @@ class _FlatOptimizer(torch.optim.Optimizer):
             if st is not None:
                 st["step"] = torch.tensor(float(n))
 
-    def consolidate_state(self) -> None:
-        """ZeRO-1: every rank updated only its own shards of the flat state buffers; gather them
-        so every rank holds the full, torch-format state (collective: call on every rank)."""
+    def checkpoint_value(self, p, k, v):
+        """The value a sharded checkpoint stores for state `k` of `p`: `v` itself, except a
+        ZeRO-1 shard of a channels-last (ResNet conv) weight - its flat order is the storage
+        order [O, KH, KW, I], not the torch shape's row-major order - which is consolidated
+        into a full tensor (a sum of zero-filled shards: exact; collective over the group)."""
+        from ..checkpoint.sharded import FlatShardedTensor
+
+        if not isinstance(v, FlatShardedTensor):
+            return v
+        seg = self._space.segment_of(p)
+        if not seg.channels_last:
+            return v
+        import torch.distributed as dist
+
+        full = torch.zeros(seg.numel, dtype=v.dtype, device=self._space.device)
+        for s0, t in v.local:
+            full[s0:s0 + t.numel()].copy_(t)
+        dist.all_reduce(full, group=self._space.zero.group)
+        o, i, kh, kw = seg.shape
+        return full.view(o, kh, kw, i).permute(0, 3, 1, 2)
+
+    def consolidate_state(self) -> dict | None:
+        """ZeRO-1: {state key: full flat buffer} all-gathered from every rank's compact shards
+        (collective: call on every rank); None without ZeRO.  Only the torch-format
+        `state_dict()` needs this - sharded checkpoints write the shards as they are."""
         sp = self._space
-        if sp is not None and sp.zero is not None:
-            for buf in self._bufs.values():
-                sp.zero.gather(buf)
+        if sp is None or sp.zero is None:
+            return None
+        full = {}
+        for k, buf in self._bufs.items():
+            f = torch.zeros(sp.numel, dtype=buf.dtype, device=buf.device)
+            sp.zero.gather_compact(buf, f)
+            full[k] = f
+        return full
 
     def state_dict(self):
-        self.consolidate_state()
+        """torch.optim format.  Under ZeRO-1 this is a collective that returns FULL state
+        tensors (gathered copies); `checkpoint.state_dict.get_optimizer_state_dict` returns
+        the sharded form instead."""
+        full = self.consolidate_state()
         self._materialize_steps()
-        return super().state_dict()
+        sd = super().state_dict()
+        if full is None:
+            return sd
+        # torch packs the live per-parameter dicts: replace the sharded values in copies
+        ids = [i for g in sd["param_groups"] for i in g["params"]]
+        state = {}
+        for i, p in zip(ids, self._all_params()):
+            st = sd["state"].get(i)
+            if st is None:
+                continue
+            st = dict(st)
+            seg = self._space.segment_of(p)
+            for k in self._state_keys:
+                if k in st:
+                    st[k] = FlatParamSpace.view(full[k], seg)
+            state[i] = st
+        sd["state"] = state
+        return sd
 
     def zero_grad(self, set_to_none: bool = True):
         if self._space is not None and self._space.grad is not None:
@@ -143,13 +269,38 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 st = self.state.get(p)
                 if not st:
                     continue
-                seg = self._space.segment_of(p)
                 for k in self._state_keys:
-                    if k in st and torch.is_tensor(st[k]):
-                        v = FlatParamSpace.view(self._bufs[k], seg)
-                        if st[k].data_ptr() != v.data_ptr():
-                            v.copy_(st[k].to(v.device, v.dtype))
-                            st[k] = v
+                    if k in st and st[k] is not None:
+                        self._adopt(p, k, st[k])
+                        st[k] = self._state_value(p, k)
+
+    def _flat_step(self) -> None:
+        """One step over the flat buffers: native chunk-table kernels on the GPU, the same
+        chunk walk with torch ops on the CPU (ZeRO-1 reference path); then, under ZeRO-1, the
+        parameter all-gather."""
+        sp = self._ensure_space()
+        have = sp.ensure_grad_views()
+        self._have = None if len(have) == len(sp.params) else set(have)
+        ov = self._overlap
+        done = ov.updated if ov is not None else ()
+        native = self._use_native()
+        launches = []
+        for group in self.param_groups:
+            ps = [p for p in self._with_grad(group) if p not in done]
+            if ps:
+                launches += self._native_launches(group, ps) if native else self._cpu_launches(group, ps)
+        self._launch_split(sp, launches)
+        if ov is not None:
+            ov.end_step()  # the compute stream waits for the updates that ran during backward
+        sp.after_step()  # ZeRO-1: gather the updated shards
+
+    @staticmethod
+    def _rows(chunks, n):
+        for start, lend, so in chunks[:n].tolist():
+            yield start, lend & 0xFFFFFFFF, bool(lend >> 32), so
+
+    def _cpu_launches(self, group, ps) -> list:
+        raise NotImplementedError
 
     def _launch_split(self, sp, launches) -> None:
         """launches: [(params, decay_flags, fn(chunks, n))].  With a pending last-bucket
@@ -217,6 +368,34 @@ class FusedAdamW(_FlatOptimizer):
             out.append((sub, [wd != 0.0] * len(sub), fn))
         return out
 
+    def _cpu_launches(self, group, ps) -> list:
+        """CPU twin of `_native_launches` (ZeRO-1 on gloo): the per-tensor reference math of
+        `step`, applied chunk by chunk to the owned flat slices and the compact state."""
+        sp = self._space
+        for p in ps:
+            self._bind_state(p)
+        b1, b2 = group["betas"]
+        wd, lr, eps = group["weight_decay"], group["lr"], group["eps"]
+        m_all, v_all = self._bufs["exp_avg"], self._bufs["exp_avg_sq"]
+        out = []
+        for step, sub in self._count(ps).items():
+            def fn(chunks, n, step=step):
+                for start, ln, decay, so in self._rows(chunks, n):
+                    p = sp.data[start:start + ln]
+                    g = sp.grad[start:start + ln]
+                    if sp.grad_scale != 1.0:
+                        g = g * sp.grad_scale
+                    m, v = m_all[so:so + ln], v_all[so:so + ln]
+                    if decay:
+                        p.mul_(1 - lr * wd)
+                    m.lerp_(g, 1 - b1)
+                    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+                    denom = (v.sqrt() / math.sqrt(1 - b2 ** step)).add_(eps)
+                    p.addcdiv_(m, denom, value=-lr / (1 - b1 ** step))
+
+            out.append((sub, [wd != 0.0] * len(sub), fn))
+        return out
+
     def _count(self, ps) -> dict:
         """Advance the step counter of every parameter in `ps`; {step: [params]}."""
         steps = self._steps
@@ -233,24 +412,11 @@ class FusedAdamW(_FlatOptimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if self._use_native():
-            if torch.cuda.is_current_stream_capturing():
+        if self._flat_mode():
+            if self._use_native() and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("FusedAdamW computes bias corrections on the host per step: not graph-capturable "
                                    "(use eager steps, or FusedSGD inside utils.graphs.CapturedStep)")
-            sp = self._ensure_space()
-            have = sp.ensure_grad_views()
-            self._have = None if len(have) == len(sp.params) else set(have)
-            ov = self._overlap
-            done = ov.updated if ov is not None else ()
-            launches = []
-            for group in self.param_groups:
-                ps = [p for p in self._with_grad(group) if p not in done]
-                if ps:
-                    launches += self._native_launches(group, ps)
-            self._launch_split(sp, launches)
-            if ov is not None:
-                ov.end_step()  # the compute stream waits for the updates that ran during backward
-            sp.after_step()  # ZeRO-1: gather the updated shards
+            self._flat_step()
             return loss
         sp = space_of(self._all_params())
         if sp is not None:
@@ -312,27 +478,50 @@ class FusedSGD(_FlatOptimizer):
             out.append((sub, [wd != 0.0] * len(sub), fn))
         return out
 
+    def _cpu_launches(self, group, ps) -> list:
+        """CPU twin of `_native_launches` (ZeRO-1 on gloo), torch.optim.SGD's math per chunk."""
+        sp = self._space
+        mom, wd, lr, damp, nest = (group["momentum"], group["weight_decay"], group["lr"], group["dampening"],
+                                   group["nesterov"])
+        parts = [(ps, False)]
+        if mom != 0.0:
+            fresh = [p for p in ps if "momentum_buffer" not in self.state[p]]
+            if fresh:
+                old = [p for p in ps if "momentum_buffer" in self.state[p]]
+                parts = [(fresh, True)] + ([(old, False)] if old else [])
+            for p in fresh:
+                self._bind_state(p)
+        buf_all = self._bufs.get("momentum_buffer")
+        out = []
+        for sub, first in parts:
+            def fn(chunks, n, first=first):
+                for start, ln, decay, so in self._rows(chunks, n):
+                    p = sp.data[start:start + ln]
+                    d = sp.grad[start:start + ln]
+                    if sp.grad_scale != 1.0:
+                        d = d * sp.grad_scale
+                    if wd != 0 and decay:
+                        d = d.add(p, alpha=wd)
+                    if mom != 0:
+                        b = buf_all[so:so + ln]
+                        if first:
+                            b.copy_(d)
+                        else:
+                            b.mul_(mom).add_(d, alpha=1 - damp)
+                        d = d.add(b, alpha=mom) if nest else b
+                    p.add_(d, alpha=-lr)
+
+            out.append((sub, [wd != 0.0] * len(sub), fn))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if self._use_native():
-            sp = self._ensure_space()
-            have = sp.ensure_grad_views()
-            self._have = None if len(have) == len(sp.params) else set(have)
-            ov = self._overlap
-            done = ov.updated if ov is not None else ()
-            launches = []
-            for group in self.param_groups:
-                ps = [p for p in self._with_grad(group) if p not in done]
-                if ps:
-                    launches += self._native_launches(group, ps)
-            self._launch_split(sp, launches)
-            if ov is not None:
-                ov.end_step()
-            sp.after_step()  # ZeRO-1: gather the updated shards
+        if self._flat_mode():
+            self._flat_step()
             return loss
         sp = space_of(self._all_params())
         if sp is not None:

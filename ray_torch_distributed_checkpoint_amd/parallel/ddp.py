@@ -30,9 +30,12 @@ MI355X:
 * `zero_stage=1` (ZeRO-1) shards the optimizer work: every bucket is padded to a multiple of
   64 x world elements and REDUCE-SCATTERED in place (rank r receives the averaged shard r), the
   fused optimizer updates only this rank's shards (1/world of the AdamW traffic - 40 of 150 ms
-  per Llama-3-8B step on one GPU), and the updated fp32 shards are all-gathered back after the
-  step (same bytes on xGMI as the all-reduce).  Optimizer state is consolidated for a
-  checkpoint, so the DCP/torch formats are unchanged.
+  per Llama-3-8B step on one GPU) and keeps optimizer state for them alone (compact buffers:
+  1/world of the exp_avg/exp_avg_sq bytes), and the updated fp32 shards are all-gathered back
+  after the step (same bytes on xGMI as the all-reduce).  Sharded checkpoints write each
+  rank's state shards as DCP chunks of the torch-shaped state tensors - no consolidation
+  (checkpoint/sharded.py).  `p.grad` is reduced only on the owned shards, so only
+  FusedAdamW / FusedSGD may step a ZeRO-1 model (checked at the first backward).
 * Parameters and buffers are broadcast from rank 0 once at construction as ONE flat tensor;
   module buffers (BatchNorm running stats) are broadcast before each forward when
   `broadcast_buffers` (distributed.py:1557-1558 semantics) as one coalesced flat tensor.
@@ -64,7 +67,7 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: float = 2.0, broadcast_buffers: bool = True, device_ids=None,
                  output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  defer_tail_to_optimizer: bool = False, grad_comm_dtype: str = "fp32", p2p_max_kb: float = 0.0,
-                 zero_stage: int = 0):
+                 zero_stage: int = 0, p2p_timeout_s: float = 30.0):
         super().__init__()
         if grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
@@ -159,6 +162,8 @@ class DistributedDataParallel(nn.Module):
         self._engine = None
         self._check = os.environ.get("RTDC_COLLECTIVE_CHECK", "0") == "1"
         self._steps = 0
+        self._zero_checked = False
+        self._p2p_timeout_s = float(p2p_timeout_s)
         self._comm = None
         self.p2p = None
         self.p2p_max_bytes = 0
@@ -177,15 +182,22 @@ class DistributedDataParallel(nn.Module):
         most first_cap elements (so its collective starts early in backward), the others cap
         (a parameter's extent counts its 64-element alignment padding from the next one on)."""
         groups, cur, cur_size = [], [], 0
+        sizes = []
         for i, n in enumerate(numels):
             limit = first_cap if not groups else cap
             if cur and cur_size + n > limit:
                 groups.append(cur)
+                sizes.append(cur_size)
                 cur, cur_size = [], 0
             cur.append(i)
             cur_size += (n + 63) // 64 * 64
         if cur:
             groups.append(cur)
+            sizes.append(cur_size)
+        # a degenerate first bucket (GPT-2: only ln_f, 6 KB, because the next parameter alone
+        # exceeds first_cap) is a latency-only collective: fold it into the second bucket
+        if len(groups) > 1 and sizes[0] < min(first_cap, cap) // 4:
+            groups = [groups[0] + groups[1]] + groups[2:]
         return groups
 
     def _agree(self, value: int, what: str) -> None:
@@ -246,7 +258,8 @@ class DistributedDataParallel(nn.Module):
         if not small:
             return
         cap_mb = max(small) / (1 << 20) + 0.01
-        self.p2p = P2PAllReduce(process_group, capacity_mb=cap_mb, device=self.space.device)
+        self.p2p = P2PAllReduce(process_group, capacity_mb=cap_mb, device=self.space.device,
+                                timeout_s=self._p2p_timeout_s)
         self.p2p_max_bytes = int(max_kb * 1024)
         self._engine.set_p2p(self.p2p.comm, self.p2p_max_bytes)
 
@@ -342,14 +355,18 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._steps += 1
         if self._engine is not None:
+            if self.p2p is not None and self.p2p.error():
+                # an earlier one-shot all-reduce timed out waiting for a peer (its bucket was
+                # poisoned with NaN): fail the step on the host as soon as the flag is visible
+                raise RuntimeError("P2P all-reduce timed out waiting for a peer rank (gradients poisoned with NaN); "
+                                   f"p2p_timeout_s={self._p2p_timeout_s}")
             self._engine.finalize(self.defer_tail)
             if self._engine.tail_pending():
                 self.space.pending_tail = (self._engine.tail_start(), self._engine.wait_tail)
             if self._check:  # RTDC_COLLECTIVE_CHECK=1: desync detector (one tiny all-reduce per step)
                 self._agree(self._steps * 1000003 + self._engine.launched() + len(self.buckets), "step sequence")
-            if self.zero and self.space.device.type != "cuda":
-                # the CPU optimizers update whole tensors: give every rank every reduced shard
-                self.space.zero.gather(self.space.grad)
+            if self.zero and not self._zero_checked:
+                self._check_zero_optimizer()
             self.space.attach_grad_views()
             return
         # params that produced no gradient this step: zero-filled grads, still reduced
@@ -372,6 +389,31 @@ class DistributedDataParallel(nn.Module):
         self.space.attach_grad_views()
         self._next = 0
         self._callback_queued = False
+
+    def _check_zero_optimizer(self) -> None:
+        """ZeRO-1 leaves `p.grad` reduced only on this rank's owned shards (the rest is this
+        rank's local, un-averaged gradient).  Only FusedAdamW / FusedSGD, which update exactly
+        the owned shards and then all-gather the parameters, may step such a model: a stock
+        torch optimizer - or grad clipping / grad-norm logging on p.grad - would silently apply
+        rank-dependent updates.  Fail loudly at the end of the first backward instead."""
+        self._zero_checked = True
+        bad = [i for i, p in enumerate(self.space.params) if not getattr(p, "_rtdc_zero_capable", False)]
+        if bad:
+            raise RuntimeError(
+                f"DistributedDataParallel(zero_stage=1): {len(bad)} parameter(s) are not owned by a FusedAdamW / "
+                "FusedSGD optimizer.  Under ZeRO-1 p.grad holds the averaged gradient only on this rank's shards, "
+                "so stock torch optimizers (and grad clipping on p.grad) would diverge across ranks; construct "
+                "ray_torch_distributed_checkpoint_amd.optim.FusedAdamW/FusedSGD over model.parameters() "
+                "or use zero_stage=0.")
+
+    def detach(self) -> None:
+        """Remove this wrapper's gradient hooks (e.g. before re-wrapping the same model with
+        another bucket plan, as bench.py's bucket sweep does).  The model keeps its flat space."""
+        self.space.wait_pending_tail()
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self._engine = None
 
     # ------------------------------------------------------------------ passthrough
     def state_dict(self, *args, **kwargs):

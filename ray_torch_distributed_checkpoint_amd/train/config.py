@@ -39,7 +39,9 @@ class CheckpointConfig:
     async_checkpoint: bool = True             # HBM snapshot + background write + background commit
     pinned_ring_mb: int = 512                 # bounded pinned-host ring per rank (D2H staging)
     ring_slot_mb: int = 64                    # ring slot = unit of one D2H copy / pwrite
-    writer_threads: int = 0                   # 0 = min(8, max(2, ncpu // 2))
+    # 0 = a per-NODE budget split over the node's ranks: max(2, min(8, ncpu // (2 * local_world)))
+    # (8 ranks x 8 writers x CRC32 on a shared host starved the training threads during async saves)
+    writer_threads: int = 0
 
     def __post_init__(self):
         if self.num_to_keep is not None and self.num_to_keep <= 0:
@@ -77,9 +79,10 @@ class RunConfig:
     log_to_file: bool = False
     # MI355X-native knobs (failure detection)
     heartbeat_timeout_s: float = 600.0       # a worker process stopped heart-beating (host hang)
-    # a worker that published a step counter (train.report_progress / report) and then did not
-    # advance it for this long is stalled - e.g. stuck in a collective whose peer died or hung,
-    # which the heartbeat thread cannot see.  None disables the check.
+    # a worker that publishes a step counter (it called train.report_progress at least once) and
+    # then advances neither that counter nor its report count for this long is stalled - e.g.
+    # stuck in a collective whose peer died or hung, which the heartbeat thread cannot see.
+    # Loops that only call report() are not watched.  None disables the check.
     progress_timeout_s: Optional[float] = 300.0
 
     def resolved_storage_path(self) -> str:
@@ -111,6 +114,8 @@ class TorchConfig:
     # 1: ZeRO-1 - reduce-scatter the gradients, each rank runs the optimizer on its 1/world
     # shard, all-gather the parameters (parallel/ddp.py); 0: every rank updates everything
     zero_stage: int = 0
+    # bounded wait of the one-shot P2P all-reduce for a late peer; a timeout fails the step
+    p2p_timeout_s: float = 30.0
 
     def __post_init__(self):
         if self.grad_comm_dtype not in ("fp32", "bf16"):
@@ -123,4 +128,4 @@ class TorchConfig:
     def ddp_kwargs(self) -> dict:
         return dict(bucket_cap_mb=self.bucket_cap_mb, first_bucket_mb=self.first_bucket_mb,
                     grad_comm_dtype=self.grad_comm_dtype, defer_tail_to_optimizer=self.defer_tail_to_optimizer,
-                    p2p_max_kb=self.p2p_max_kb, zero_stage=self.zero_stage)
+                    p2p_max_kb=self.p2p_max_kb, zero_stage=self.zero_stage, p2p_timeout_s=self.p2p_timeout_s)

@@ -8,8 +8,8 @@ torch.distributed rendezvous (RCCL unique-id exchange / gloo) and the control pl
 * a worker exiting non-zero, publishing an error, or missing heartbeats for
   `heartbeat_timeout_s` fails the attempt; every surviving worker of the gang is killed
   (SIGKILL to its process group - a partially failed RCCL communicator cannot recover);
-* a worker whose training-thread step counter (`train.report_progress`, `report`) stops
-  advancing for `progress_timeout_s` fails the attempt the same way: this catches a rank
+* a worker whose training-thread step counter (`train.report_progress`; every `report` also
+  counts as progress) stops advancing for `progress_timeout_s` fails the attempt the same way: this catches a rank
   stuck inside a collective (a dead or hung peer), which the heartbeat thread keeps hiding
   until the 30-minute process-group timeout;
 * up to `FailureConfig.max_failures` restarts, each resuming from the latest committed
@@ -170,10 +170,12 @@ class WorkerGroup:
             if v == "done":
                 self._progress.pop(r, None)
                 continue
-            step = int(v.split()[0])
+            parts = v.split()
+            step = int(parts[0])
+            token = (step, parts[2] if len(parts) > 2 else "")  # step or report sequence advanced
             prev = self._progress.get(r)
-            if prev is None or prev[0] != step:
-                self._progress[r] = (step, now)
+            if prev is None or prev[0] != token:
+                self._progress[r] = (token, now)
             elif now - prev[1] > timeout:
                 return r, step
         return None

@@ -147,6 +147,8 @@ class _Session:
         self._prog_key = f"a{ctx.attempt}/prog/{ctx.world_rank}"
         self._prog_last = 0.0
         self._prog_step = -1
+        self._prog_explicit = False  # set by the first report_progress(): only those ranks are watched
+        self._prog_seq = 0           # advanced by every report(), so report-only loops never look stalled
         self._fail_at = self._parse_injector("RTDC_FAIL_AT_STEP")
         self._hang_at = self._parse_injector("RTDC_HANG_AT_STEP")
 
@@ -167,15 +169,23 @@ class _Session:
             self._publish_progress(step)
             threading.Event().wait()  # never returns: the gang is killed by the supervisor
         self._prog_step = max(self._prog_step, int(step))
+        first = not self._prog_explicit
+        self._prog_explicit = True
         now = time.time()
-        if force or now - self._prog_last >= 1.0:
+        if force or first or now - self._prog_last >= 1.0:
             self._publish_progress(self._prog_step, now)
 
     def _publish_progress(self, step, now=None):
+        """Publish `<step> <time> <report seq>`; the supervisor treats a change of either the
+        step or the report sequence as progress.  Nothing is published for a loop that never
+        called `report_progress` (a Ray-style loop that only reports once per epoch must not
+        be judged by a per-step timeout)."""
+        if not self._prog_explicit:
+            return
         now = now or time.time()
         self._prog_last = now
         try:
-            self.store.set(self._prog_key, f"{step} {now}")
+            self.store.set(self._prog_key, f"{step} {now} {self._prog_seq}")
         except Exception:
             pass
 
@@ -194,6 +204,7 @@ class _Session:
             # report commits; anything else would commit an empty staging dir
             raise ValueError(f"async checkpoint written to {checkpoint.path}, but this report commits {stage}: "
                              f"save into train.get_context().next_checkpoint_dir()")
+        self._prog_seq += 1
         self._publish_progress(self._prog_step)
         with self._timing_lock:
             if self._ckpt_timing:

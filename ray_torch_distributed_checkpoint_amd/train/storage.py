@@ -75,13 +75,61 @@ def merge_into(src: str, dst: str, overwrite: bool) -> None:
             os.replace(tmp, d)
 
 
+_RENAME_EXCHANGE = 2
+
+
+def _exchange(a: str, b: str) -> bool:
+    """renameat2(RENAME_EXCHANGE): atomically swap two existing paths (Linux >= 3.15)."""
+    try:
+        import ctypes
+
+        libc = ctypes.CDLL(None, use_errno=True)
+        f = libc.renameat2
+    except (OSError, AttributeError):
+        return False
+    AT_FDCWD = -100
+    return f(AT_FDCWD, a.encode(), AT_FDCWD, b.encode(), _RENAME_EXCHANGE) == 0
+
+
 def commit(trial_dir: str, index: int) -> str:
+    """Publish `checkpoint_NNNNNN.tmp/` as `checkpoint_NNNNNN/` atomically.  A final directory
+    of the same index (only possible after a crash between a commit and the registry update)
+    is never deleted first: the new one is swapped in with RENAME_EXCHANGE and only then is
+    the old one removed, so `checkpoint_NNNNNN/` always names a complete checkpoint."""
     src, dst = staging_dir(trial_dir, index), final_dir(trial_dir, index)
     if os.path.exists(dst):
-        shutil.rmtree(dst)
-    os.replace(src, dst)
+        if _exchange(src, dst):
+            shutil.rmtree(src, ignore_errors=True)  # src now holds the replaced checkpoint
+            fsync_dir(trial_dir)
+            return dst
+        # no renameat2: move the old one aside (a rename), then publish - still never a
+        # moment where dst names a partial directory
+        aside = dst + f".replaced.{os.getpid()}"
+        os.replace(dst, aside)
+        os.replace(src, dst)
+        shutil.rmtree(aside, ignore_errors=True)
+    else:
+        os.replace(src, dst)
     fsync_dir(trial_dir)
     return dst
+
+
+def sweep_stale_staging(trial_dir: str) -> list[str]:
+    """Remove what a crashed attempt left behind: `checkpoint_*.tmp/` staging directories
+    (partial shards of a checkpoint that was never committed) and `*.replaced.*` leftovers.
+    Called by the driver before every attempt, while no worker runs, so a restarted attempt
+    never commits a staging dir that still holds a dead attempt's partial files."""
+    removed = []
+    if not os.path.isdir(trial_dir):
+        return removed
+    for name in os.listdir(trial_dir):
+        if name.startswith("checkpoint_") and (name.endswith(".tmp") or ".replaced." in name):
+            p = os.path.join(trial_dir, name)
+            shutil.rmtree(p, ignore_errors=True)
+            removed.append(p)
+    if removed:
+        fsync_dir(trial_dir)
+    return removed
 
 
 def list_committed(trial_dir: str) -> list[tuple[int, str]]:

@@ -91,6 +91,9 @@ class TorchTrainer:
                 "checkpoint_config": ck_cfg, "resume_checkpoint": resume, "torch_config": self.torch_config,
             }
             ppath = write_payload(payload)
+            stale = storage.sweep_stale_staging(trial_dir)  # a failed attempt's partial shards
+            if stale and self.run.verbose:
+                print(f"[rtdc] removed {len(stale)} uncommitted staging dir(s) of a failed attempt", flush=True)
             try:
                 group.start(ppath, attempt)
                 outcome = group.supervise(attempt, self.run.heartbeat_timeout_s, on_report,

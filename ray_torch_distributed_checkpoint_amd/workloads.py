@@ -108,9 +108,20 @@ class SyntheticTokens:
         return self.n
 
     def batch(self, idx: torch.Tensor):
+        """(inputs, targets), contiguous [B, seq_len] int64.  On the GPU one native kernel
+        (`data_ops.hip` synth_tokens) writes both; the CPU path is the same hash in ATen."""
+        if idx.is_cuda:
+            from .ops._ext import gpu_ext
+
+            ids = idx.to(torch.int64).contiguous()
+            B = ids.numel()
+            inp = torch.empty((B, self.seq_len), dtype=torch.int64, device=idx.device)
+            tgt = torch.empty_like(inp)
+            gpu_ext().synth_tokens(ids, inp, tgt, self.vocab, self.seed * 7919 + 1)
+            return inp, tgt
         pos = torch.arange(self.seq_len + 1, device=idx.device, dtype=torch.int64)
         tok = _mix(idx.to(torch.int64)[:, None] * (self.seq_len + 1) + pos, self.seed) % self.vocab
-        return tok[:, :-1], tok[:, 1:]
+        return tok[:, :-1].contiguous(), tok[:, 1:].contiguous()
 
 
 class SyntheticImages:

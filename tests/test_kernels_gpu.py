@@ -653,3 +653,31 @@ def test_fp32_linear_fused_dropout_equals_separate_kernel(M, K, N, p):
     for u, v in zip(a, r):
         assert torch.equal(u, v)
     assert (a[0] == 0).float().mean().item() > p * 0.5  # really dropped
+
+
+@pytest.mark.parametrize("n,V", [(1, 10), (63, 50257), (1000, 7), (16384, 50257), (2048, 128256), (5000, 1 << 24)])
+def test_sort_ids_matches_stable_sort(n, V):
+    """Native one-workgroup radix sort == torch's stable sort (ids and original positions)."""
+    from ray_torch_distributed_checkpoint_amd.ops.embedding import sort_ids
+
+    g = torch.Generator(device=DEV).manual_seed(n)
+    ids = torch.randint(0, V, (n,), device=DEV, generator=g)
+    if n >= 1000:
+        ids[: n // 3] = ids[0]  # long runs of one id: the stability order matters
+    s, p = sort_ids(ids, V)
+    rs, rp = torch.sort(ids, stable=True)
+    assert torch.equal(s, rs)
+    assert torch.equal(p, rp)
+
+
+def test_synth_tokens_matches_cpu_hash():
+    """The native synthetic-token kernel reproduces workloads.SyntheticTokens' CPU hash."""
+    from ray_torch_distributed_checkpoint_amd.workloads import SyntheticTokens
+
+    ds = SyntheticTokens(1 << 20, 1024, 50257, seed=1234)
+    ids = torch.tensor([0, 5, 1 << 19, (1 << 20) - 1, 77], dtype=torch.int64)
+    ci, ct = ds.batch(ids)
+    gi, gt = ds.batch(ids.to(DEV))
+    assert gi.is_contiguous() and gt.is_contiguous()
+    assert torch.equal(gi.cpu(), ci) and torch.equal(gt.cpu(), ct)
+    assert torch.equal(gi[:, 1:], gt[:, :-1])

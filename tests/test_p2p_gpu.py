@@ -146,3 +146,44 @@ def test_ddp_buckets_over_p2p_equal_the_process_group_path(comm_dtype):
     for n, v in base[0][0].items():
         for r in range(world):
             assert np.array_equal(p2p[r][0][n], v), f"{n} differs on rank {r}"
+
+
+def _timeout_worker(rank, world, port, q):
+    try:
+        import time
+
+        import torch.distributed as dist
+
+        dev = _init(rank, world, port)
+        from ray_torch_distributed_checkpoint_amd.parallel.p2p import P2PAllReduce
+
+        comm = P2PAllReduce(capacity_mb=1.0, device=dev, timeout_s=1.0, blocks=4)
+        x = torch.randn(4096, device=dev)
+        raised = None
+        if rank == 0:
+            comm.all_reduce_(x)  # rank 1 arrives ~3 s late: the bounded wait gives up after 1 s
+            torch.cuda.synchronize()
+            try:
+                comm.all_reduce_(torch.randn(4096, device=dev))
+            except RuntimeError as e:
+                raised = str(e)
+        dist.barrier()  # gloo: rank 1 starts only after rank 0's call is over
+        if rank == 1:
+            time.sleep(0.5)
+            comm.all_reduce_(x)  # sees rank 0's flag and staged data: completes
+            torch.cuda.synchronize()
+        q.put((rank, "ok", (bool(torch.isnan(x).all().item()), comm.error(), raised)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def test_p2p_timeout_poisons_bucket_and_raises():
+    """A peer that misses the bounded wait: the late rank's bucket is NaN-filled (never a
+    silently un-reduced gradient), its error word is set, and its next call raises."""
+    out = _spawn(_timeout_worker, 2)
+    nan0, err0, raised0 = out[0]
+    assert nan0 and err0 == 1 and raised0 and "timed out" in raised0
+    nan1, err1, _ = out[1]
+    assert not nan1 and err1 == 0
