@@ -76,6 +76,11 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (multi-rank rehearsal on 1 GPU)")
     ap.add_argument("--cpu", action="store_true",
                     help="run on the CPU (gloo; a plumbing rehearsal of the N-rank path, e.g. in CI - not a benchmark)")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="checkpoint phase only (1 process): plan the sharded save/restore as rank "
+                         "--simulate-rank of a W-rank data-parallel job and write/read just that rank's "
+                         "shard (e.g. Llama-3-8B's full train-state 1/8 shard on one GPU)")
+    ap.add_argument("--simulate-rank", type=int, default=0)
     ap.add_argument("--sweep", type=int, default=1, choices=[0, 1],
                     help="N > 1: after the timed run, a short bucket_cap_mb x grad-comm-dtype sweep (comm.sweep)")
     args = ap.parse_args()
@@ -425,6 +430,12 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     from ray_torch_distributed_checkpoint_amd.checkpoint.state_dict import get_state_dict, set_state_dict
 
     scope = args.ckpt_scope
+    sim = None
+    if args.simulate_world and args.simulate_world > 1:
+        if world != 1:
+            raise ValueError("--simulate-world runs in a single process")
+        sim = (args.simulate_world, args.simulate_rank)
+    share = sim[0] if sim else max(world, 1)  # this rank writes ~1/share of the state
 
     def state():
         msd, osd = get_state_dict(model, opt)
@@ -443,19 +454,19 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     # model scope and flagged as downgraded).
     free = shutil.disk_usage(base).free
     downgraded = False
-    if scope == "full" and nbytes_of(state()) / max(world, 1) * 1.15 > free:
+    if scope == "full" and nbytes_of(state()) / share * 1.15 > free:
         if not args.ckpt_scope_fallback:
             return {"ckpt_unmeasured": f"full train state ({nbytes_of(state()) / 1e9:.1f} GB) larger than free "
                                        f"disk ({free / 1e9:.0f} GB) at {base}; pass --ckpt-scope-fallback for a "
                                        f"model-only measurement"}
         scope, downgraded = "model", True
-    if nbytes_of(state()) / max(world, 1) * 1.15 > free:
+    if nbytes_of(state()) / share * 1.15 > free:
         return {"ckpt_unmeasured": f"state larger than free disk ({free / 1e9:.0f} GB)"}
 
     # ---- async save overlapped with training steps
     sync()
     t0 = time.perf_counter()
-    h = dcp.async_save(state(), path)
+    h = dcp.async_save(state(), path, simulate=sim)
     t_resume = time.perf_counter() - t0  # training may continue from here
     t1 = time.perf_counter()
     for i in range(args.overlap_steps):
@@ -482,7 +493,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
         dist.barrier()
     sync()
     t2 = time.perf_counter()
-    dcp.save(state(), path2)
+    dcp.save(state(), path2, simulate=sim)
     t_sync = time.perf_counter() - t2
     # ---- restore into the live model + optimizer: first warm (shards still in the page cache
     # right after the write), then cold (every shard dropped from the page cache with
@@ -493,7 +504,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
             dist.barrier()
         t3 = time.perf_counter()
         sd = state()
-        dcp.load(sd, path2)
+        dcp.load(sd, path2, simulate=sim)
         set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
         sync()
         if world > 1:
@@ -534,6 +545,11 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     }
     if downgraded:
         out["ckpt_scope_downgraded"] = True
+    if sim:
+        # one rank's share of a W-rank job: bytes/GBps above are this rank's shard
+        out["ckpt_simulated"] = {"world": sim[0], "rank": sim[1], "note": "per-rank shard of a W-rank plan, "
+                                 "written and restored by one process; other ranks' shards not written"}
+        out["ckpt_format"] = f"torch.distributed.checkpoint (.metadata + __{sim[1]}_0.distcp of {sim[0]}), native engine"
     return out
 
 

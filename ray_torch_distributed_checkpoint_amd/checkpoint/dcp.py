@@ -188,8 +188,9 @@ class AsyncSave:
             return self.write_s
 
     def _finish(self):
-        """Rank 0: write `.metadata` atomically (call after every rank's wait())."""
-        if self.rank == 0 and self._metadata is not None:
+        """Rank 0 (or a simulated rank): write `.metadata` atomically (call after every rank's
+        wait())."""
+        if self._metadata is not None:
             write_metadata(self.checkpoint_id, self._metadata)
 
     def result(self):
@@ -229,11 +230,34 @@ def write_metadata(checkpoint_id: str, md: Metadata):
     fsync_dir(checkpoint_id)
 
 
+def _simulated(simulate):
+    """(world, rank) this process plays in a SIMULATED multi-rank save/load, or None.
+    `simulate=(W, r)` or env RTDC_DCP_SIMULATE="W:r": plan exactly as rank r of a W-rank
+    data-parallel job (owner plan, file layout, `.metadata` for all W ranks) but write / read
+    only rank r's share, with no collectives - how one GPU measures a per-rank shard of an
+    8-GPU job (e.g. Llama-3-8B's ~12 GB train-state shard).  The result on disk is one rank's
+    file plus the full metadata: a measurement artifact, not a restorable checkpoint."""
+    if simulate is None:
+        env = os.environ.get("RTDC_DCP_SIMULATE")
+        if not env:
+            return None
+        w, _, r = env.partition(":")
+        simulate = (int(w), int(r or 0))
+    w, r = int(simulate[0]), int(simulate[1])
+    if not (0 <= r < w):
+        raise ValueError(f"simulate=({w}, {r}): rank out of range")
+    if _world(None)[0] != 1:
+        raise ValueError("a simulated multi-rank save/load runs in a single process (no process group)")
+    return w, r
+
+
 def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsync: bool = True,
-               crc: bool = True, replicated: bool = True) -> AsyncSave:
-    """Start a sharded save; returns once the HBM snapshot is enqueued (non-blocking)."""
+               crc: bool = True, replicated: bool = True, simulate=None) -> AsyncSave:
+    """Start a sharded save; returns once the HBM snapshot is enqueued (non-blocking).
+    `simulate=(W, r)`: see `_simulated`."""
     t0 = time.perf_counter()
-    world, rank = _world(process_group)
+    sim = _simulated(simulate)
+    world, rank = sim if sim else _world(process_group)
     os.makedirs(checkpoint_id, exist_ok=True)
     items, mapping = _collect(state_dict, world, rank)
     rep = [it for it in items if it.owner is None]
@@ -258,7 +282,7 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
         ready.record()
     ext = _ext.ext()
     metadata = None
-    if rank == 0 or not replicated:
+    if rank == 0 or not replicated or sim:
         sd_md = {}
         storage = {}
         ranks = range(world) if replicated else [rank]
@@ -288,7 +312,7 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
         metadata = Metadata(state_dict_metadata=sd_md, planner_data=mapping, storage_data=storage,
                             storage_meta=StorageMeta(checkpoint_id=checkpoint_id, save_id=str(uuid.uuid4())),
                             version=DCP_VERSION)
-        if not replicated and world > 1:
+        if not replicated and world > 1 and not sim:
             # gather per-rank metadata on rank 0 (CPU object collective)
             parts = [None] * world
             dist.all_gather_object(parts, metadata, group=process_group)
@@ -427,10 +451,15 @@ def _pinned(n: int) -> torch.Tensor:
 
 
 def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast: bool = True,
-         pinned_mb: int = 1024, threads: int = 8) -> dict:
+         pinned_mb: int = 1024, threads: int = 8, simulate=None) -> dict:
     """Load a DCP-format checkpoint IN PLACE into `state_dict` (tensors copied into, Stateful
-    objects get load_state_dict).  Collective when a process group is initialised."""
-    world, rank = _world(process_group)
+    objects get load_state_dict).  Collective when a process group is initialised.
+    Reader plan: a checkpoint saved by the same number of ranks is read back by its writers
+    (each rank reads the file it wrote - no cross-rank file access, page-cache local);
+    otherwise readers are balanced by bytes.  Every tensor is then broadcast from its reader
+    (coalesced).  `simulate=(W, r)`: read only rank r's share of a W-rank plan, no collectives."""
+    sim = _simulated(simulate)
+    world, rank = sim if sim else _world(process_group)
     md = read_metadata(checkpoint_id)
     resolved = _resolve_stateful(state_dict)
     flat, mapping = flatten_state_dict(resolved)
@@ -456,7 +485,7 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
         for s in m.size:
             n *= s
         sizes.append((k, n * flat[k].element_size()))
-    reader = _balanced_owner(sizes, world) if broadcast else {k: rank for k in tensor_fqns}
+    reader = _reader_plan(md, chunks_of, sizes, world) if broadcast else {k: rank for k in tensor_fqns}
     my = [k for k in tensor_fqns if reader[k] == rank]
     # ---- read my items: (dest tensor, chunk offsets, chunk sizes, file, data offset, nbytes)
     reqs = []
@@ -536,19 +565,21 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
             torch.cuda.current_stream().synchronize()  # staging reuse
     # ---- broadcast from readers, coalesced: each reader's tensors packed into <= 256 MB flat
     # buffers per dtype (GPT-2's train state: ~450 per-tensor broadcasts -> a handful)
-    if broadcast and world > 1:
+    if broadcast and world > 1 and not sim:
         _coalesced_broadcast([(flat[k], reader[k]) for k in tensor_fqns], world, process_group)
     # ---- non-tensor values (rank 0 reads, broadcasts as objects)
     obj_keys = [k for k in flat if not torch.is_tensor(flat[k]) and not isinstance(flat[k], FlatShardedTensor)]
     values = {}
     if obj_keys:
-        if rank == 0 or not broadcast:
+        if rank == 0 or not broadcast or sim:
             for k in obj_keys:
                 (idx, info), = chunks_of[k]
+                if sim and not os.path.exists(os.path.join(checkpoint_id, info.relative_path)):
+                    continue  # another simulated rank's file
                 with open(os.path.join(checkpoint_id, info.relative_path), "rb") as f:
                     f.seek(info.offset)
                     values[k] = torch.load(io.BytesIO(f.read(info.length)), weights_only=True)
-        if broadcast and world > 1:
+        if broadcast and world > 1 and not sim:
             box = [values]
             dist.broadcast_object_list(box, src=_global_rank(0, process_group), group=process_group)
             values = box[0]
@@ -623,6 +654,27 @@ def _load_sharded(flat, fqns, md, chunks_of, checkpoint_id, ext, threads) -> Non
             eng.read_to_device(path, o, l_, d, threads)
     for path, (o, l_, d) in host_reads.items():
         ext.read_ranges(path, o, l_, d, threads)
+
+
+def _reader_plan(md, chunks_of, sizes, world) -> dict:
+    """fqn -> reader rank.  Same world as the save: the rank whose file holds the tensor (its
+    writer); otherwise (or for multi-file tensors) byte-balanced."""
+    import re
+
+    files = {info.relative_path for info in md.storage_data.values()}
+    ranks = {int(m.group(1)) for f in files for m in [re.match(r"__(\d+)_\d+\.distcp$", f)] if m}
+    if ranks and max(ranks) + 1 == world:
+        out, rest = {}, []
+        for k, n in sizes:
+            fs = {info.relative_path for _idx, info in chunks_of[k]}
+            m = re.match(r"__(\d+)_\d+\.distcp$", next(iter(fs))) if len(fs) == 1 else None
+            if m:
+                out[k] = int(m.group(1))
+            else:
+                rest.append((k, n))
+        out.update(_balanced_owner(rest, world) if rest else {})
+        return out
+    return _balanced_owner(sizes, world)
 
 
 BCAST_CAP_BYTES = 256 << 20

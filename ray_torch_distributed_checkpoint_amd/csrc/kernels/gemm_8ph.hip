@@ -651,6 +651,246 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
   }
 }
 
+// ---- 4-wave 256x256 kernel: a 128x128 output per wave (accumulators in AGPRs) ----------
+//
+// Why: the 8-wave kernel's per-wave 128x64 tile reads (128 + 64) x 64 x 2 B of LDS fragments per
+// 2 x 128 x 64 x 64 FLOP: 384 B per 16x16x32 MFMA, ~96 B/clk per CU at the MFMA peak against an
+// LDS port that delivers ~64 B/clk for swizzled ds_read_b128 - the fragment reads, not MFMA issue,
+// bound its main loop (profiles/gemm_mfma_shape_diag.txt).  A 128x128 per-wave tile reads
+// 256 B per MFMA (-33 %).  Its 256 fp32 accumulators live in AGPRs (one wave per SIMD: 512
+// registers per lane), the fragments in VGPRs.
+//
+// With one wave per SIMD nothing else hides a wave's own LDS latency, so fragments are
+// PREFETCHED one phase ahead - the ds_reads of phase p+1 are issued at the top of phase p and
+// run under phase p's 32 MFMAs:
+//     phase   MFMA quadrant (A half, B half)   reads issued (for later phases)
+//       p1      (lo, lo)  fa0 fbl              B-hi(t)   -> fbh
+//       p2      (lo, hi)  fa0 fbh              A-hi(t)   -> fa1
+//       p3      (hi, lo)  fa1 fbl              -
+//       p4      (hi, hi)  fa1 fbh              A-lo(t+1) -> fa0, B-lo(t+1) -> fbl
+// Half-tile DMA (event e = 4 * K-tile + kind, kind 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi; 4 glds
+// per thread each) is issued as soon as the region's previous occupant (same half, K-tile
+// t - 2, same LDS buffer) has been read: p1 issues A-lo(t+2), B-lo(t+2); p2 B-hi(t+2); p3
+// A-hi(t+2).  Every load then has ~6 phases (~190 MFMAs per SIMD) to land, with up to 6
+// half-tiles (24 glds) in flight per wave across each raw s_barrier (counted vmcnt, never 0
+// in the steady state).
+// RAW: a half is read in the phase after the barrier that follows its retiring wait;
+// WAR: a half is restaged only after the barrier that follows the lgkmcnt(0) retiring its
+// last read.
+__device__ __forceinline__ void wait_vm4(int allowed_events) {
+  // allowed outstanding glds = 4 per event
+  switch (allowed_events < 0 ? 0 : (allowed_events > 6 ? 6 : allowed_events)) {
+    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <bool AK, bool BKM, typename OutT>
+__global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
+  constexpr int BN = 256, BH = 128, SA = 64, SB = 64, TMQ = 4, TNQ = 4;
+  constexpr int BUF = 4 * HALF;  // [A-lo, A-hi, B-lo, B-hi]
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wave & 1, wb = wave >> 1;
+
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  int tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  int kb = 0, ke = a.K;
+  if (a.splitk > 1) {
+    const int ktiles = a.K / gemm::BK;
+    const int per = (ktiles + a.splitk - 1) / a.splitk;
+    kb = blockIdx.y * per * gemm::BK;
+    ke = min(a.K, kb + per * gemm::BK);
+  }
+  const int nt = ke > kb ? (ke - kb) / gemm::BK : 0;
+  const int tev = 4 * nt;
+
+  Stager<AK, 128, 4> sa0, sa1;
+  Stager<BKM, 128, 4> sb0, sb1;
+  sa0.init(a.A, a.lda, a.M, m0, wave, lane);
+  sa1.init(a.A, a.lda, a.M, m0 + 128, wave, lane);
+  sb0.init(a.B, a.ldb, a.N, n0, wave, lane);
+  sb1.init(a.B, a.ldb, a.N, n0 + BH, wave, lane);
+
+  auto issue = [&](int e) {
+    if (e >= tev) return;
+    const int j = e >> 2, kind = e & 3;
+    const int k0 = kb + j * gemm::BK;
+    char* base = smem + (j & 1) * BUF;
+    if (kind == 0) sa0.issue(k0, base, wave);
+    else if (kind == 1) sb0.issue(k0, base + 2 * HALF, wave);
+    else if (kind == 2) sb1.issue(k0, base + 3 * HALF, wave);
+    else sa1.issue(k0, base + HALF, wave);
+  };
+  // wait until event `need` has landed, given that events up to `last` were issued
+  auto retire = [&](int need, int last) { wait_vm4(min(last, tev - 1) - need); };
+
+  f32x4 acc[2][2][TMQ][TNQ];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa0[TMQ][2], fa1[TMQ][2], fbl[TNQ][2], fbh[TNQ][2];
+  if (nt > 0) {
+    // prologue: K-tiles 0 and 1 in flight; A-lo(0), B-lo(0) into registers (B-hi(0) landed too)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) issue(e);
+    retire(2, 7);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    typename Frag<AK>::T ra[TMQ][2];
+    typename Frag<BKM>::T rb[TNQ][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(smem, SA * wa + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(smem + 2 * HALF, SB * wb + 16 * j, ks, lane);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // WAR: nobody restages A-lo/B-lo(0)'s buffer before all read it
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i) fa0[i][ks] = fval(ra[i][ks]);
+#pragma unroll
+      for (int j = 0; j < TNQ; ++j) fbl[j][ks] = fval(rb[j][ks]);
+    }
+  }
+
+  auto mfma_quadrant = [&](int qa, int qb, bf16x8 (&fa)[TMQ][2], bf16x8 (&fb)[TNQ][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j)
+          acc[qa][qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qa][qb][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  for (int t = 0; t < nt; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const char* nbuf = smem + ((t + 1) & 1) * BUF;
+    const bool more = t + 1 < nt;
+    // ---- p1: (lo, lo); prefetch B-hi(t)
+    {
+      typename Frag<BKM>::T rb[TNQ][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(buf + 3 * HALF, SB * wb + 16 * j, ks, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant(0, 0, fa0, fbl);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(4 * (t + 2));
+      issue(4 * (t + 2) + 1);
+      retire(4 * t + 3, 4 * t + 9);  // A-hi(t) for p2's reads
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j) fbh[j][ks] = fval(rb[j][ks]);
+    }
+    // ---- p2: (lo, hi); prefetch A-hi(t)
+    {
+      typename Frag<AK>::T ra[TMQ][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(buf + HALF, SA * wa + 16 * i, ks, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant(0, 1, fa0, fbh);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(4 * (t + 2) + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i) fa1[i][ks] = fval(ra[i][ks]);
+    }
+    // ---- p3: (hi, lo); no reads
+    mfma_quadrant(1, 0, fa1, fbl);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(4 * (t + 2) + 3);
+    if (more) retire(4 * t + 5, 4 * t + 11);  // A-lo(t+1), B-lo(t+1) for p4's reads
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // ---- p4: (hi, hi); prefetch A-lo(t+1), B-lo(t+1)
+    {
+      typename Frag<AK>::T ra[TMQ][2];
+      typename Frag<BKM>::T rb[TNQ][2];
+      if (more) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(nbuf, SA * wa + 16 * i, ks, lane);
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(nbuf + 2 * HALF, SB * wb + 16 * j, ks, lane);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_quadrant(1, 1, fa1, fbh);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+        retire(4 * t + 6, 4 * t + 11);  // B-hi(t+1) for the next p1's reads
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int i = 0; i < TMQ; ++i) fa0[i][ks] = fval(ra[i][ks]);
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) fbl[j][ks] = fval(rb[j][ks]);
+        }
+      }
+    }
+  }
+
+  const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
+  if (a.splitk > 1) {
+    float* Wp = a.ws + (long long)blockIdx.y * a.M * a.N;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i) {
+          const int m = m0 + 128 * qa + SA * wa + 16 * i + (lane & 15);
+          if (m >= a.M) continue;
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            const int n = n0 + BH * qb + SB * wb + 16 * j + 4 * (lane >> 4);
+            if (n >= a.N) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[qa][qb][i][j][r] * alpha;
+            store4<float>(Wp + (long long)m * a.N + n, v);
+          }
+        }
+    return;
+  }
+  tile_epilogue<OutT, TMQ, TNQ, SA, SB, BH, false>(a, acc, m0, n0, wa, wb, lane, alpha);
+}
+
 }  // namespace g8
 }  // namespace rtdc
 
@@ -720,5 +960,26 @@ extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmaj
     else G8P(false, true, bf16_t);
   }
 #undef G8P
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// 4-wave 256x256 kernel (gemm4_kernel): same contract as rtdc_gemm8_launch with bn = 256.
+extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st) {
+  const GemmArgs& a = *args;
+  const unsigned tiles = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
+  dim3 grid(tiles, a.splitk > 1 ? a.splitk : 1, 1), block(256);
+#define G4(AK, BKM, T) hipLaunchKernelGGL((g8::gemm4_kernel<AK, BKM, T>), grid, block, 0, st, a)
+  if (out_fp32) {
+    if (a_kmajor && b_kmajor) G4(true, true, float);
+    else if (a_kmajor) G4(true, false, float);
+    else if (!b_kmajor) G4(false, false, float);
+    else G4(false, true, float);
+  } else {
+    if (a_kmajor && b_kmajor) G4(true, true, bf16_t);
+    else if (a_kmajor) G4(true, false, bf16_t);
+    else if (!b_kmajor) G4(false, false, bf16_t);
+    else G4(false, true, bf16_t);
+  }
+#undef G4
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

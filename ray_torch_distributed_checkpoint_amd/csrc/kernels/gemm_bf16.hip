@@ -435,6 +435,18 @@ extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajo
                                  hipStream_t st);
 extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
                                   hipStream_t st);
+extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
+
+// cfg 10: the 4-wave 256x256 kernel (gemm_8ph.hip gemm4_kernel, 128x128 per wave).
+// RTDC_GEMM4W=1 routes the 8-wave 256x256 choices (cfg 6 / 8) to it.
+static bool gemm4w_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_GEMM4W");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
 
 // Persistent 8-wave kernel (gemm_8ph.hip gemm8p_kernel) for plain-K (no split-K) products with
 // more tiles than CUs: the next tile's loads and this tile's epilogue overlap MFMA work instead
@@ -482,26 +494,31 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   GemmArgs a = *args;
   if (a.K % gemm::BK != 0 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
   int cfg = pick_cfg(a, batch, a_kmajor, b_kmajor);
+  if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4w_enabled()) cfg = 10;
   // the 8-wave kernels write bf16 outputs 16 B at a time through tile-relative 32-bit buffer
   // offsets (gemm_8ph.hip tile_epilogue)
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
                        (uintptr_t)a.bias;
-  if (cfg >= 6 && cfg <= 9 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
+  if (cfg >= 6 && cfg <= 10 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
   long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
                   : cfg == 2 ? ntiles<Cfg128x256>(a) : cfg == 4 ? ntiles<Cfg256x64>(a)
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
-  const bool big = cfg >= 6 && cfg <= 9;  // 8-wave counted-vmcnt pipeline (gemm_8ph.hip)
+  const bool big = cfg >= 6 && cfg <= 10;  // counted-vmcnt pipelines (gemm_8ph.hip)
   const int bn = (cfg == 7 || cfg == 9) ? 192 : 256;
   if (big) {
     if (batch != 1 || a.causal != 0) return 1;
     tiles = (long long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
   }
   // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
-  if (plain && cfg <= 7) a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : 1.8) : pick_splitk(a, tiles);
-  if (big) {
+  if (plain && (cfg <= 7 || cfg == 10))
+    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : 1.8) : pick_splitk(a, tiles);
+  if (cfg == 10) {
+    const int rc = rtdc_gemm4_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
+    if (rc) return rc;
+  } else if (big) {
     // cfg 8 / 9 force the persistent form; 6 / 7 take it automatically where it applies
     const bool persist = cfg >= 8 || (persist_enabled() && a.splitk == 1 && a_kmajor && b_kmajor &&
                                       tiles > 256 && a.K >= 2 * gemm::BK);

@@ -87,7 +87,7 @@ def test_gemm_bf16_epilogues():
     _close(Cb, base * gd, 1e-4)
 
 
-@pytest.mark.parametrize("cfg", [-1, 6, 7])
+@pytest.mark.parametrize("cfg", [-1, 6, 7, 10])
 def test_gemm_gelu_bwd_colsum(cfg):
     """dpre = (dy @ W) * gelu'(pre) with the column sums of dpre (the c_fc bias gradient)
     reduced by the 8-wave epilogue (cfg 6 / 7: 256x256 / 256x192 tiles; rows past M and a
@@ -109,7 +109,7 @@ def test_gemm_gelu_bwd_colsum(cfg):
     _close(cs, ref.sum(0), 5e-3)
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 6, 7, 9])
+@pytest.mark.parametrize("cfg", [-1, 0, 6, 7, 9, 10])
 def test_gemm_gelu_saved_derivative_roundtrip(cfg):
     """act 5: y = gelu(x W^T + b) with aux_out = gelu'(pre) (bf16), act 6: dx = (dy W) * aux_in
     with the fused column sums - together the GELU forward/backward pair of the MLP, against
@@ -133,7 +133,7 @@ def test_gemm_gelu_saved_derivative_roundtrip(cfg):
     dpre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     cs = torch.full((N,), float("nan"), device=DEV)
     G.gemm_bf16(dz, w2, dpre, M, N, K2, K2, N, N, True, False, aux_in=gp, act=G.ACT_MUL,
-                tile_cfg=cfg if cfg in (-1, 0, 6, 7) else -1, colsum_out=cs)
+                tile_cfg=cfg if cfg in (-1, 0, 6, 7, 10) else -1, colsum_out=cs)
     ref = (dz.float() @ w2.float()) * gp.float()
     _close(dpre, ref, 1e-2)
     _close(cs, ref.sum(0), 5e-3)
@@ -494,7 +494,7 @@ def test_ckpt_engine_writes_torch_loadable(tmp_path):
         assert torch.equal(got[k], sd[k].cpu())
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 10])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)])
 def test_gemm_tile_configs(cfg, a_k, b_k):
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
@@ -510,7 +510,7 @@ def test_gemm_tile_configs(cfg, a_k, b_k):
     _close(C, Af @ Bf, 1e-5)
 
 
-@pytest.mark.parametrize("cfg", [8, 9])
+@pytest.mark.parametrize("cfg", [8, 9, 10])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("K", [128, 320])
 def test_gemm_persistent_multi_tile(cfg, a_k, b_k, K):
@@ -545,7 +545,7 @@ def test_gemm_persistent_epilogues():
     bias = torch.randn(N, device=DEV)
     res = _bf(M, N)
     pre_ref = x.float() @ w.float().t() + bias
-    for cfg in (8, 9):
+    for cfg in (8, 9, 10):
         y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         G.gemm_bf16(x, w, y, M, N, K, K, K, N, True, True, bias=bias, aux_out=pre, act=G.ACT_GELU, tile_cfg=cfg)
@@ -681,3 +681,17 @@ def test_synth_tokens_matches_cpu_hash():
     assert gi.is_contiguous() and gt.is_contiguous()
     assert torch.equal(gi.cpu(), ci) and torch.equal(gt.cpu(), ct)
     assert torch.equal(gi[:, 1:], gt[:, :-1])
+
+
+@pytest.mark.parametrize("a_k,b_k", [(False, False), (True, False)])
+def test_gemm4w_splitk_weight_gradient(a_k, b_k):
+    """4-wave kernel (cfg 10) on a long-K weight-gradient product: split-K slabs + reduce."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(31)
+    Mt, N, K = 16384, 768, 512  # dW[N, K] = dY^T X over Mt tokens
+    dy, x = _bf(Mt, N), _bf(Mt, K)
+    A = dy if not a_k else dy.t().contiguous()
+    dw = torch.empty(N, K, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, x, dw, N, K, Mt, A.shape[1], K, K, a_k, b_k, tile_cfg=10)
+    _close(dw, dy.float().t() @ x.float(), 1e-5)
