@@ -140,7 +140,7 @@ def test_p2p_allreduce_matches_reference_on_every_rank():
 def test_ddp_buckets_over_p2p_equal_the_process_group_path(comm_dtype):
     world = 2
     base = _spawn(_ddp_worker, world, 0.0, comm_dtype)
-    p2p = _spawn(_ddp_worker, world, 64.0, comm_dtype)
+    p2p = _spawn(_ddp_worker, world, 200.0, comm_dtype)
     assert p2p[0][1]["p2p_buckets"], "no bucket was routed through P2P"
     assert not base[0][1]["p2p_buckets"]
     for n, v in base[0][0].items():
