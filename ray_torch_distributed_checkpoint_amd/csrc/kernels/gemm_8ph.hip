@@ -690,6 +690,47 @@ __device__ __forceinline__ void wait_vm4(int allowed_events) {
   }
 }
 
+// 16 MFMAs of one k-slice, c[i][j] += b[j] (x) a[i], with the accumulators pinned to AGPRs
+// ("+a"): hipcc's own allocation of 256 accumulators beside 128+ fragment VGPRs rotated them
+// through a[4:7] with 4 v_accvgpr_mov per MFMA (and spilled VGPRs into AGPRs).  Hazards
+// (cdna_hip_programming.md §5.7 item 2): the leading s_nop 1 covers a VALU write of an operand
+// right before the statement; consecutive statements chain accumulators whole (0 states); the
+// reader after the last statement is fenced by mfma_drain().
+__device__ __forceinline__ void mfma16_agpr(f32x4 (&c)[4][4], const bf16x8 (&a)[4], const bf16x8 (&b)[4]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %20, %16, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %21, %16, %1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %2, %22, %16, %2\n\t"
+      "v_mfma_f32_16x16x32_bf16 %3, %23, %16, %3\n\t"
+      "v_mfma_f32_16x16x32_bf16 %4, %20, %17, %4\n\t"
+      "v_mfma_f32_16x16x32_bf16 %5, %21, %17, %5\n\t"
+      "v_mfma_f32_16x16x32_bf16 %6, %22, %17, %6\n\t"
+      "v_mfma_f32_16x16x32_bf16 %7, %23, %17, %7\n\t"
+      "v_mfma_f32_16x16x32_bf16 %8, %20, %18, %8\n\t"
+      "v_mfma_f32_16x16x32_bf16 %9, %21, %18, %9\n\t"
+      "v_mfma_f32_16x16x32_bf16 %10, %22, %18, %10\n\t"
+      "v_mfma_f32_16x16x32_bf16 %11, %23, %18, %11\n\t"
+      "v_mfma_f32_16x16x32_bf16 %12, %20, %19, %12\n\t"
+      "v_mfma_f32_16x16x32_bf16 %13, %21, %19, %13\n\t"
+      "v_mfma_f32_16x16x32_bf16 %14, %22, %19, %14\n\t"
+      "v_mfma_f32_16x16x32_bf16 %15, %23, %19, %15\n\t"
+      : "+a"(c[0][0]), "+a"(c[0][1]), "+a"(c[0][2]), "+a"(c[0][3]), "+a"(c[1][0]), "+a"(c[1][1]), "+a"(c[1][2]), "+a"(c[1][3]), "+a"(c[2][0]), "+a"(c[2][1]), "+a"(c[2][2]), "+a"(c[2][3]), "+a"(c[3][0]), "+a"(c[3][1]), "+a"(c[3][2]), "+a"(c[3][3])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]));
+}
+
+// MFMA D -> any other reader needs 12 wait states (8-pass XDL): naming every accumulator keeps
+// the compiler's reads below the nops
+__device__ __forceinline__ void mfma_drain(f32x4 (&c)[4][4]) {
+  asm volatile("s_nop 15" : "+a"(c[0][0]), "+a"(c[0][1]), "+a"(c[0][2]), "+a"(c[0][3]), "+a"(c[1][0]), "+a"(c[1][1]), "+a"(c[1][2]), "+a"(c[1][3]), "+a"(c[2][0]), "+a"(c[2][1]), "+a"(c[2][2]), "+a"(c[2][3]), "+a"(c[3][0]), "+a"(c[3][1]), "+a"(c[3][2]), "+a"(c[3][3]));
+}
+
+// all LDS reads retired, stated through the builtin so hipcc's wait bookkeeping knows it (an
+// asm wait is invisible to it: it then re-waits lgkmcnt(0) before the first use of data it
+// still thinks is in flight - after the next phase's prefetch reads were issued, which
+// serialised them with the MFMAs).  vmcnt / expcnt fields at their maxima (no wait).
+__device__ __forceinline__ void lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
 template <bool AK, bool BKM, typename OutT>
 __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
   constexpr int BN = 256, BH = 128, SA = 64, SB = 64, TMQ = 4, TNQ = 4;
@@ -745,7 +786,37 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < TNQ; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa0[TMQ][2], fa1[TMQ][2], fbl[TNQ][2], fbh[TNQ][2];
+  // fragments [k-slice][row / column block]
+  bf16x8 fa0[2][TMQ], fa1[2][TMQ], fbl[2][TNQ], fbh[2][TNQ];
+  auto load_a = [&](typename Frag<AK>::T (&r)[2][TMQ], const char* half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i) r[ks][i] = load_fragx<AK, 128>(half, SA * wa + 16 * i, ks, lane);
+  };
+  auto load_b = [&](typename Frag<BKM>::T (&r)[2][TNQ], const char* half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < TNQ; ++j) r[ks][j] = load_fragx<BKM, 128>(half, SB * wb + 16 * j, ks, lane);
+  };
+  auto take_a = [&](bf16x8 (&f)[2][TMQ], typename Frag<AK>::T (&r)[2][TMQ]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i) f[ks][i] = fval(r[ks][i]);
+  };
+  auto take_b = [&](bf16x8 (&f)[2][TNQ], typename Frag<BKM>::T (&r)[2][TNQ]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < TNQ; ++j) f[ks][j] = fval(r[ks][j]);
+  };
+  auto quadrant = [&](int qa, int qb, bf16x8 (&fa)[2][TMQ], bf16x8 (&fb)[2][TNQ]) {
+    mfma16_agpr(acc[qa][qb], fa[0], fb[0]);
+    mfma16_agpr(acc[qa][qb], fa[1], fb[1]);
+  };
+
   if (nt > 0) {
     // prologue: K-tiles 0 and 1 in flight; A-lo(0), B-lo(0) into registers (B-hi(0) landed too)
 #pragma unroll
@@ -753,37 +824,15 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
     retire(2, 7);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    typename Frag<AK>::T ra[TMQ][2];
-    typename Frag<BKM>::T rb[TNQ][2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(smem, SA * wa + 16 * i, ks, lane);
-#pragma unroll
-      for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(smem + 2 * HALF, SB * wb + 16 * j, ks, lane);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    typename Frag<AK>::T ra[2][TMQ];
+    typename Frag<BKM>::T rb[2][TNQ];
+    load_a(ra, smem);
+    load_b(rb, smem + 2 * HALF);
+    lgkm0();
     __builtin_amdgcn_s_barrier();  // WAR: nobody restages A-lo/B-lo(0)'s buffer before all read it
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int i = 0; i < TMQ; ++i) fa0[i][ks] = fval(ra[i][ks]);
-#pragma unroll
-      for (int j = 0; j < TNQ; ++j) fbl[j][ks] = fval(rb[j][ks]);
-    }
+    take_a(fa0, ra);
+    take_b(fbl, rb);
   }
-
-  auto mfma_quadrant = [&](int qa, int qb, bf16x8 (&fa)[TMQ][2], bf16x8 (&fb)[TNQ][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < TMQ; ++i)
-#pragma unroll
-        for (int j = 0; j < TNQ; ++j)
-          acc[qa][qb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][ks], fa[i][ks], acc[qa][qb][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
 
   for (int t = 0; t < nt; ++t) {
     const char* buf = smem + (t & 1) * BUF;
@@ -791,44 +840,34 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
     const bool more = t + 1 < nt;
     // ---- p1: (lo, lo); prefetch B-hi(t)
     {
-      typename Frag<BKM>::T rb[TNQ][2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(buf + 3 * HALF, SB * wb + 16 * j, ks, lane);
+      typename Frag<BKM>::T rb[2][TNQ];
+      load_b(rb, buf + 3 * HALF);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant(0, 0, fa0, fbl);
+      quadrant(0, 0, fa0, fbl);
       __builtin_amdgcn_sched_barrier(0);
       issue(4 * (t + 2));
       issue(4 * (t + 2) + 1);
       retire(4 * t + 3, 4 * t + 9);  // A-hi(t) for p2's reads
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lgkm0();
+      asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < TNQ; ++j) fbh[j][ks] = fval(rb[j][ks]);
+      take_b(fbh, rb);
     }
     // ---- p2: (lo, hi); prefetch A-hi(t)
     {
-      typename Frag<AK>::T ra[TMQ][2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(buf + HALF, SA * wa + 16 * i, ks, lane);
+      typename Frag<AK>::T ra[2][TMQ];
+      load_a(ra, buf + HALF);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant(0, 1, fa0, fbh);
+      quadrant(0, 1, fa0, fbh);
       __builtin_amdgcn_sched_barrier(0);
       issue(4 * (t + 2) + 2);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lgkm0();
+      asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < TMQ; ++i) fa1[i][ks] = fval(ra[i][ks]);
+      take_a(fa1, ra);
     }
     // ---- p3: (hi, lo); no reads
-    mfma_quadrant(1, 0, fa1, fbl);
+    quadrant(1, 0, fa1, fbl);
     __builtin_amdgcn_sched_barrier(0);
     issue(4 * (t + 2) + 3);
     if (more) retire(4 * t + 5, 4 * t + 11);  // A-lo(t+1), B-lo(t+1) for p4's reads
@@ -836,34 +875,29 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
     __builtin_amdgcn_s_barrier();
     // ---- p4: (hi, hi); prefetch A-lo(t+1), B-lo(t+1)
     {
-      typename Frag<AK>::T ra[TMQ][2];
-      typename Frag<BKM>::T rb[TNQ][2];
+      typename Frag<AK>::T ra[2][TMQ];
+      typename Frag<BKM>::T rb[2][TNQ];
       if (more) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-          for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(nbuf, SA * wa + 16 * i, ks, lane);
-#pragma unroll
-          for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(nbuf + 2 * HALF, SB * wb + 16 * j, ks, lane);
-        }
+        load_a(ra, nbuf);
+        load_b(rb, nbuf + 2 * HALF);
       }
       __builtin_amdgcn_sched_barrier(0);
-      mfma_quadrant(1, 1, fa1, fbh);
+      quadrant(1, 1, fa1, fbh);
       __builtin_amdgcn_sched_barrier(0);
       if (more) {
         retire(4 * t + 6, 4 * t + 11);  // B-hi(t+1) for the next p1's reads
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lgkm0();
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-          for (int i = 0; i < TMQ; ++i) fa0[i][ks] = fval(ra[i][ks]);
-#pragma unroll
-          for (int j = 0; j < TNQ; ++j) fbl[j][ks] = fval(rb[j][ks]);
-        }
+        take_a(fa0, ra);
+        take_b(fbl, rb);
       }
     }
   }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) mfma_drain(acc[x][y]);
 
   const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
   if (a.splitk > 1) {
@@ -896,6 +930,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
 
 using namespace rtdc;
 
+#ifndef RTDC_G4_ONLY  // (-DRTDC_G4_ONLY: a quick build of the 4-wave kernel alone for ISA inspection)
 // Launch the 8-phase kernel (batch 1, no causal modes).  a->splitk is honoured as set.
 // bn: 256 or 192 (output tile columns)
 extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
@@ -962,6 +997,8 @@ extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmaj
 #undef G8P
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+#endif  // RTDC_G4_ONLY
 
 // 4-wave 256x256 kernel (gemm4_kernel): same contract as rtdc_gemm8_launch with bn = 256.
 extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st) {
