@@ -130,12 +130,17 @@ def train_func_per_worker(config: Dict):
         if "rng" in resume_state:
             _set_rng_state(resume_state["rng"], device)
 
-    # hipGraph-captured step (one GPU, every batch full): static input tensors the loader's
-    # batches are copied into, one graph launch per step
-    n_train = len(train_dataloader.dataset) if hasattr(train_dataloader, "dataset") else 0
+    # hipGraph-captured step (every batch full): static input tensors the loader's batches are
+    # copied into, one graph launch per step.  With several workers the step includes the
+    # gradient all-reduce, so it is captured only when every bucket goes through the one-shot
+    # P2P all-reduce (device-resident epochs: graph-capturable, parallel/p2p.py) - the
+    # reference's own 2-worker config (R/train_flow.py:17-18) with its 1-2 MB buckets.
+    sampler = getattr(train_dataloader, "sampler", None)
+    n_train = len(sampler) if (world > 1 and sampler is not None) else (
+        len(train_dataloader.dataset) if hasattr(train_dataloader, "dataset") else 0)
     captured = None
-    use_graph = (device.type == "cuda" and world == 1 and config.get("hipgraph", True) and n_train > 0
-                 and n_train % batch_size == 0)
+    use_graph = (device.type == "cuda" and config.get("hipgraph", True) and n_train > 0
+                 and n_train % batch_size == 0 and (world == 1 or _all_buckets_p2p(model)))
     if use_graph:
         side = torch.cuda.Stream()
         sx = torch.zeros((batch_size, 1, 28, 28), device=device)
@@ -246,6 +251,11 @@ def train_func_per_worker(config: Dict):
     print(f"[my_ray_module] Training completed in {round((tf_full - t0_full) / 60, 3)} minutes!")
 
 
+def _all_buckets_p2p(net) -> bool:
+    eng = getattr(net, "_engine", None)
+    return getattr(net, "p2p", None) is not None and eng is not None and all(eng.p2p_buckets())
+
+
 def train_fashion_mnist(
     num_workers=1,
     use_gpu=False,
@@ -278,11 +288,15 @@ def train_fashion_mnist(
         failure_config=train.FailureConfig(max_failures=max_failures),
     )
     scaling_config = ScalingConfig(num_workers=num_workers, use_gpu=use_gpu)
+    # one node, GPUs: the MLP's two 1-2 MB gradient buckets are latency-bound on a ring, so they
+    # take the one-shot hipIpc all-reduce over xGMI (which also lets the step be graph-captured)
+    torch_config = train.TorchConfig(p2p_max_kb=4096.0 if use_gpu and 1 < num_workers <= 8 else 0.0)
     trainer = TorchTrainer(
         train_loop_per_worker=train_func_per_worker,
         train_loop_config=train_config,
         scaling_config=scaling_config,
         run_config=run_config,
+        torch_config=torch_config,
     )
     return trainer.fit()
 

@@ -6,8 +6,11 @@
 // and mapped by every peer:
 //     [ flag (64 B) | staging parity 0 (cap B) | staging parity 1 (cap B) ]
 // A call with epoch e (a per-communicator counter, identical on every rank because collectives
-// are issued in the same order everywhere) uses staging parity e & 1:
-//   1. copy the local tensor into the own staging slot (stream-ordered before 2);
+// are issued in the same order everywhere) uses staging parity e & 1.  The counter lives in
+// DEVICE memory (one word per rank, never shared): every kernel of a call reads e = counter + 1
+// and a final one-thread kernel advances it, so a call captured into a hipGraph advances the
+// epoch on every replay (a host counter would be frozen into the captured kernel arguments):
+//   1. stage_kernel copies the local tensor into the own staging slot of parity e & 1;
 //   2. oneshot_kernel: block 0 publishes flag = e (system-scope release); every block waits
 //      until all ranks' flags reached e (system-scope acquire loads), then sums its share of
 //      the elements over ranks 0..world-1 IN RANK ORDER (fp32 accumulation) - every rank
@@ -36,11 +39,23 @@ __device__ __forceinline__ unsigned load_flag(const unsigned* p) {
 }
 
 // T: float or bf16_t.  n elements (n * sizeof(T) a multiple of 16), 16-B vectors.
+__global__ __launch_bounds__(256) void stage_kernel(const unsigned* __restrict__ epoch_dev, char* own, long long cap,
+                                                   const uint4* __restrict__ src, long long nv) {
+  const unsigned epoch = *epoch_dev + 1u;
+  uint4* dst = (uint4*)(own + FLAG_BYTES + (long long)(epoch & 1u) * cap);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) dst[i] = src[i];
+}
+
+__global__ void advance_kernel(unsigned* epoch_dev) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *epoch_dev += 1u;
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void oneshot_kernel(Peers peers, int world, int rank, unsigned epoch,
+__global__ __launch_bounds__(256) void oneshot_kernel(Peers peers, int world, int rank, const unsigned* epoch_dev,
                                                       long long cap, T* __restrict__ out, long long n,
                                                       float scale, int* err, long long timeout_ticks) {
   __shared__ int bad;
+  const unsigned epoch = *epoch_dev + 1u;  // advanced by advance_kernel after this call
   if (threadIdx.x == 0) {
     unsigned* mine = (unsigned*)peers.base[rank];
     if (blockIdx.x == 0) __hip_atomic_store(mine, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -107,10 +122,11 @@ __global__ __launch_bounds__(256) void oneshot_kernel(Peers peers, int world, in
 
 using namespace rtdc;
 
-// bases: world mapped allocations (own at [rank]); data: the local tensor (already copied into
-// the own staging slot of parity epoch & 1 by the caller, stream-ordered).  blocks: grid size
-// (few: the kernel reads HBM of every peer; a small grid leaves the CUs to the backward pass).
-extern "C" int rtdc_p2p_oneshot(const void* const* bases, int world, int rank, unsigned epoch, long long cap,
+// One call on stream st: stage (local tensor -> own staging slot), one-shot sum, epoch advance.
+// bases: world mapped allocations (own at [rank]); data: the local tensor, reduced in place.
+// blocks: grid size (few: the kernel reads HBM of every peer; a small grid leaves the CUs to
+// the backward pass).  Every argument is call-invariant, so the call is hipGraph-capturable.
+extern "C" int rtdc_p2p_oneshot(const void* const* bases, int world, int rank, unsigned* epoch_dev, long long cap,
                                 void* data, long long n, int is_bf16, float scale, int* err,
                                 long long timeout_ticks, int blocks, hipStream_t st) {
   if (world < 1 || world > p2p::MAXW || rank < 0 || rank >= world) return 1;
@@ -119,11 +135,14 @@ extern "C" int rtdc_p2p_oneshot(const void* const* bases, int world, int rank, u
   p2p::Peers peers{};
   for (int r = 0; r < world; ++r) peers.base[r] = (const char*)bases[r];
   if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(p2p::stage_kernel, dim3(blocks), dim3(256), 0, st, (const unsigned*)epoch_dev,
+                     (char*)bases[rank], cap, (const uint4*)data, bytes / 16);
   if (is_bf16)
-    hipLaunchKernelGGL(p2p::oneshot_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, peers, world, rank, epoch, cap,
-                       (bf16_t*)data, n, scale, err, timeout_ticks);
+    hipLaunchKernelGGL(p2p::oneshot_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, peers, world, rank,
+                       (const unsigned*)epoch_dev, cap, (bf16_t*)data, n, scale, err, timeout_ticks);
   else
-    hipLaunchKernelGGL(p2p::oneshot_kernel<float>, dim3(blocks), dim3(256), 0, st, peers, world, rank, epoch, cap,
-                       (float*)data, n, scale, err, timeout_ticks);
+    hipLaunchKernelGGL(p2p::oneshot_kernel<float>, dim3(blocks), dim3(256), 0, st, peers, world, rank,
+                       (const unsigned*)epoch_dev, cap, (float*)data, n, scale, err, timeout_ticks);
+  hipLaunchKernelGGL(p2p::advance_kernel, dim3(1), dim3(64), 0, st, epoch_dev);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

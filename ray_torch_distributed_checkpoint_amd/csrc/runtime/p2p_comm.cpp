@@ -11,7 +11,7 @@
 #include <string>
 #include <vector>
 
-extern "C" int rtdc_p2p_oneshot(const void* const* bases, int world, int rank, unsigned epoch, long long cap,
+extern "C" int rtdc_p2p_oneshot(const void* const* bases, int world, int rank, unsigned* epoch_dev, long long cap,
                                 void* data, long long n, int is_bf16, float scale, int* err,
                                 long long timeout_ticks, int blocks, hipStream_t st);
 
@@ -30,6 +30,9 @@ class P2PComm {
     check(hipExtMallocWithFlags(&own_, (size_t)(kFlag + 2 * cap_), hipDeviceMallocUncached), "hipExtMallocWithFlags");
     check(hipMemset(own_, 0, (size_t)(kFlag + 2 * cap_)), "hipMemset");
     check(hipHostMalloc((void**)&err_, sizeof(int), hipHostMallocCoherent), "hipHostMalloc");
+    // device-resident epoch counter (graph-capturable calls: kernels/p2p_allreduce.hip)
+    check(hipMalloc((void**)&epoch_dev_, 64), "hipMalloc");
+    check(hipMemset(epoch_dev_, 0, 64), "hipMemset");
     *err_ = 0;
     int rate_khz = 0;
     if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || rate_khz <= 0)
@@ -43,6 +46,7 @@ class P2PComm {
     for (int r = 0; r < world_; ++r)
       if (r != rank_ && bases_[r]) hipIpcCloseMemHandle(bases_[r]);
     if (own_) hipFree(own_);
+    if (epoch_dev_) hipFree(epoch_dev_);
     if (err_) hipHostFree(err_);
   }
 
@@ -78,12 +82,10 @@ class P2PComm {
     TORCH_CHECK(bytes % 16 == 0, "P2PComm: size must be a multiple of 16 bytes");
     if (*err_ != 0) TORCH_CHECK(false, "P2PComm: an earlier all-reduce timed out waiting for a peer");
     if (bytes == 0) return;
-    const unsigned epoch = ++epoch_;
+    ++epoch_;  // calls issued (host bookkeeping only: the kernels use the device counter)
     hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_).stream();
-    char* slot = (char*)own_ + kFlag + (long long)(epoch & 1u) * cap_;
-    check(hipMemcpyAsync(slot, t.data_ptr(), (size_t)bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     const float scale = average ? 1.f / (float)world_ : 1.f;
-    const int rc = rtdc_p2p_oneshot((const void* const*)bases_.data(), world_, rank_, epoch, cap_, t.data_ptr(),
+    const int rc = rtdc_p2p_oneshot((const void* const*)bases_.data(), world_, rank_, epoch_dev_, cap_, t.data_ptr(),
                                     t.numel(), t.scalar_type() == at::kBFloat16 ? 1 : 0, scale, err_, timeout_ticks_,
                                     blocks_, st);
     TORCH_CHECK(rc == 0, "rtdc_p2p_oneshot failed (" + std::to_string(rc) + ")");
@@ -105,6 +107,7 @@ class P2PComm {
   int device_, blocks_;
   void* own_ = nullptr;
   int* err_ = nullptr;
+  unsigned* epoch_dev_ = nullptr;
   long long timeout_ticks_ = 0;
   std::vector<void*> bases_;
   bool opened_ = false;

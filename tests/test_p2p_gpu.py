@@ -187,3 +187,78 @@ def test_p2p_timeout_poisons_bucket_and_raises():
     assert nan0 and err0 == 1 and raised0 and "timed out" in raised0
     nan1, err1, _ = out[1]
     assert not nan1 and err1 == 0
+
+
+def _toy_graph_worker(rank, world, port, use_graph, q):
+    """The reference's 2-worker toy step (MLP, B = 16, SGD momentum) under DDP with every bucket
+    on the one-shot P2P all-reduce: eager, or captured once into a hipGraph and replayed."""
+    try:
+        import torch.distributed as dist
+
+        dev = _init(rank, world, port)
+        from ray_torch_distributed_checkpoint_amd import ops
+        from ray_torch_distributed_checkpoint_amd.models import NeuralNetwork
+        from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
+        from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+        from ray_torch_distributed_checkpoint_amd.utils.graphs import CapturedStep
+
+        torch.manual_seed(0)
+        ops.manual_seed(1234 + rank)
+        model = NeuralNetwork().to(dev)
+        net = DistributedDataParallel(model, p2p_max_kb=4096.0)
+        assert all(net._engine.p2p_buckets()), "every bucket should take the P2P path"
+        opt = FusedSGD(model.parameters(), lr=1e-2, momentum=0.9)
+        g = torch.Generator().manual_seed(100 + rank)
+        batches = [(torch.randn(16, 1, 28, 28, generator=g).to(dev), torch.randint(0, 10, (16,), generator=g).to(dev))
+                   for _ in range(8)]
+        sx = torch.zeros(16, 1, 28, 28, device=dev)
+        sy = torch.zeros(16, dtype=torch.int64, device=dev)
+
+        def step():
+            opt.zero_grad()
+            loss = ops.cross_entropy(net(sx), sy)
+            loss.backward()
+            opt.step()
+            return loss
+
+        side = torch.cuda.Stream()
+        losses = []
+        cs = None
+        for i, (x, y) in enumerate(batches):
+            sx.copy_(x)
+            sy.copy_(y)
+            if use_graph and i >= 2:
+                if cs is None:
+                    cs = CapturedStep(step, warmup=0)
+                losses.append(cs.replay().detach().clone())
+                continue
+            # eager steps on a side stream before a capture (as CapturedStep's warm-up does)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                losses.append(step().detach().clone())
+            torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        if cs is not None:
+            cs.close()
+        out = ([float(l) for l in losses], {n: p.detach().cpu().numpy() for n, p in model.named_parameters()},
+               net.p2p.error())
+        q.put((rank, "ok", out))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def test_two_worker_toy_step_graph_replay_equals_eager():
+    """The reference config's DDP step (2 workers) captured in a hipGraph - forward, backward,
+    the P2P gradient all-reduce with device-resident epochs, SGD - replays bitwise equal to the
+    eager step on every rank."""
+    eager = _spawn(_toy_graph_worker, 2, False)
+    graph = _spawn(_toy_graph_worker, 2, True)
+    for r in range(2):
+        assert graph[r][2] == 0 and eager[r][2] == 0
+        assert graph[r][0] == eager[r][0], (r, graph[r][0], eager[r][0])
+        for n, v in eager[r][1].items():
+            assert np.array_equal(graph[r][1][n], v), (r, n)
+    for n, v in eager[0][1].items():  # ranks stay in sync
+        assert np.array_equal(eager[1][1][n], v), n
