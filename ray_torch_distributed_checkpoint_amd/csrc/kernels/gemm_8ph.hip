@@ -725,6 +725,20 @@ __device__ __forceinline__ void mfma_drain(f32x4 (&c)[4][4]) {
   asm volatile("s_nop 15" : "+a"(c[0][0]), "+a"(c[0][1]), "+a"(c[0][2]), "+a"(c[0][3]), "+a"(c[1][0]), "+a"(c[1][1]), "+a"(c[1][2]), "+a"(c[1][3]), "+a"(c[2][0]), "+a"(c[2][1]), "+a"(c[2][2]), "+a"(c[2][3]), "+a"(c[3][0]), "+a"(c[3][1]), "+a"(c[3][2]), "+a"(c[3][3]));
 }
 
+// 4 MFMAs (one A fragment x 4 B fragments of one k-slice), accumulators pinned to AGPRs; the
+// unit the interleaved schedule places loads between.  s_nop 1: a VALU write of an operand
+// right before the statement (hazard, cdna_hip_programming.md §5.7 item 2).
+__device__ __forceinline__ void mfma4_agpr(f32x4 (&c)[4], const bf16x8& a, const bf16x8 (&b)[4]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %5, %4, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %6, %4, %1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %2, %7, %4, %2\n\t"
+      "v_mfma_f32_16x16x32_bf16 %3, %8, %4, %3\n\t"
+      : "+a"(c[0]), "+a"(c[1]), "+a"(c[2]), "+a"(c[3])
+      : "v"(a), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]));
+}
+
 // all LDS reads retired, stated through the builtin so hipcc's wait bookkeeping knows it (an
 // asm wait is invisible to it: it then re-waits lgkmcnt(0) before the first use of data it
 // still thinks is in flight - after the next phase's prefetch reads were issued, which
@@ -812,10 +826,6 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TNQ; ++j) f[ks][j] = fval(r[ks][j]);
   };
-  auto quadrant = [&](int qa, int qb, bf16x8 (&fa)[2][TMQ], bf16x8 (&fb)[2][TNQ]) {
-    mfma16_agpr(acc[qa][qb], fa[0], fb[0]);
-    mfma16_agpr(acc[qa][qb], fa[1], fb[1]);
-  };
 
   if (nt > 0) {
     // prologue: K-tiles 0 and 1 in flight; A-lo(0), B-lo(0) into registers (B-hi(0) landed too)
@@ -834,56 +844,93 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
     take_b(fbl, rb);
   }
 
+  // one phase: 8 groups of 4 MFMAs (k-slice ks = g / 4, A block i = g % 4) of quadrant
+  // (qa, qb); after group g, fill(g) places loads - fragment reads for a later phase and DMA
+  // pieces - so they issue while the matrix core works (one wave per SIMD: nothing else
+  // would cover their issue cost)
+  auto phase = [&](int qa, int qb, bf16x8 (&fa)[2][TMQ], bf16x8 (&fb)[2][TNQ], auto&& fill) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      mfma4_agpr(acc[qa][qb][g & 3], fa[g >> 2][g & 3], fb[g >> 2]);
+      __builtin_amdgcn_sched_barrier(0);
+      fill(g);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // DMA piece ii of half-tile event e (kind = e & 3)
+  auto dma = [&](int e, int ii) {
+    if (e >= tev) return;
+    const int j = e >> 2, kind = e & 3;
+    const int k0 = kb + j * gemm::BK;
+    char* base = smem + (j & 1) * BUF;
+    if (kind == 0) sa0.issue_one(k0, base, wave, ii);
+    else if (kind == 1) sb0.issue_one(k0, base + 2 * HALF, wave, ii);
+    else if (kind == 2) sb1.issue_one(k0, base + 3 * HALF, wave, ii);
+    else sa1.issue_one(k0, base + HALF, wave, ii);
+  };
+
   for (int t = 0; t < nt; ++t) {
     const char* buf = smem + (t & 1) * BUF;
     const char* nbuf = smem + ((t + 1) & 1) * BUF;
     const bool more = t + 1 < nt;
-    // ---- p1: (lo, lo); prefetch B-hi(t)
+    const int e2 = 4 * (t + 2);  // events of K-tile t + 2
+    // ---- p1: (lo, lo); reads B-hi(t) (2 per group, groups 0-3); DMA A-lo, B-lo(t+2) (groups 4-7)
     {
       typename Frag<BKM>::T rb[2][TNQ];
-      load_b(rb, buf + 3 * HALF);
-      __builtin_amdgcn_sched_barrier(0);
-      quadrant(0, 0, fa0, fbl);
-      __builtin_amdgcn_sched_barrier(0);
-      issue(4 * (t + 2));
-      issue(4 * (t + 2) + 1);
+      phase(0, 0, fa0, fbl, [&](int g) {
+        if (g < 4) {
+          rb[g >> 1][2 * (g & 1)] = load_fragx<BKM, 128>(buf + 3 * HALF, SB * wb + 32 * (g & 1), g >> 1, lane);
+          rb[g >> 1][2 * (g & 1) + 1] = load_fragx<BKM, 128>(buf + 3 * HALF, SB * wb + 32 * (g & 1) + 16, g >> 1, lane);
+        } else {
+          dma(e2 + 0, g - 4);
+          dma(e2 + 1, g - 4);
+        }
+      });
       retire(4 * t + 3, 4 * t + 9);  // A-hi(t) for p2's reads
       lgkm0();
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       take_b(fbh, rb);
     }
-    // ---- p2: (lo, hi); prefetch A-hi(t)
+    // ---- p2: (lo, hi); reads A-hi(t) (groups 0-3); DMA B-hi(t+2) (groups 4-7)
     {
       typename Frag<AK>::T ra[2][TMQ];
-      load_a(ra, buf + HALF);
-      __builtin_amdgcn_sched_barrier(0);
-      quadrant(0, 1, fa0, fbh);
-      __builtin_amdgcn_sched_barrier(0);
-      issue(4 * (t + 2) + 2);
+      phase(0, 1, fa0, fbh, [&](int g) {
+        if (g < 4) {
+          ra[g >> 1][2 * (g & 1)] = load_fragx<AK, 128>(buf + HALF, SA * wa + 32 * (g & 1), g >> 1, lane);
+          ra[g >> 1][2 * (g & 1) + 1] = load_fragx<AK, 128>(buf + HALF, SA * wa + 32 * (g & 1) + 16, g >> 1, lane);
+        } else {
+          dma(e2 + 2, g - 4);
+        }
+      });
       lgkm0();
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       take_a(fa1, ra);
     }
-    // ---- p3: (hi, lo); no reads
-    quadrant(1, 0, fa1, fbl);
-    __builtin_amdgcn_sched_barrier(0);
-    issue(4 * (t + 2) + 3);
+    // ---- p3: (hi, lo); no reads; DMA A-hi(t+2) (groups 4-7)
+    phase(1, 0, fa1, fbl, [&](int g) {
+      if (g >= 4) dma(e2 + 3, g - 4);
+    });
     if (more) retire(4 * t + 5, 4 * t + 11);  // A-lo(t+1), B-lo(t+1) for p4's reads
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // ---- p4: (hi, hi); prefetch A-lo(t+1), B-lo(t+1)
+    // ---- p4: (hi, hi); reads A-lo(t+1) (groups 0-3), B-lo(t+1) (groups 4-7)
     {
       typename Frag<AK>::T ra[2][TMQ];
       typename Frag<BKM>::T rb[2][TNQ];
-      if (more) {
-        load_a(ra, nbuf);
-        load_b(rb, nbuf + 2 * HALF);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      quadrant(1, 1, fa1, fbh);
-      __builtin_amdgcn_sched_barrier(0);
+      phase(1, 1, fa1, fbh, [&](int g) {
+        if (!more) return;
+        const int h = g & 3;
+        if (g < 4) {
+          ra[h >> 1][2 * (h & 1)] = load_fragx<AK, 128>(nbuf, SA * wa + 32 * (h & 1), h >> 1, lane);
+          ra[h >> 1][2 * (h & 1) + 1] = load_fragx<AK, 128>(nbuf, SA * wa + 32 * (h & 1) + 16, h >> 1, lane);
+        } else {
+          rb[h >> 1][2 * (h & 1)] = load_fragx<BKM, 128>(nbuf + 2 * HALF, SB * wb + 32 * (h & 1), h >> 1, lane);
+          rb[h >> 1][2 * (h & 1) + 1] =
+              load_fragx<BKM, 128>(nbuf + 2 * HALF, SB * wb + 32 * (h & 1) + 16, h >> 1, lane);
+        }
+      });
       if (more) {
         retire(4 * t + 6, 4 * t + 11);  // B-hi(t+1) for the next p1's reads
         lgkm0();

@@ -82,6 +82,12 @@ struct Stager {
       __builtin_amdgcn_global_load_lds((const void*)(src[ii] + koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
     }
   }
+  // one piece (1 KiB per wave) of issue(): lets a schedule interleave the DMA with MFMAs
+  __device__ __forceinline__ void issue_one(int k0, char* lds_tile, int wave, int ii) const {
+    const long long koff = (long long)k0 * kmul;
+    const int piece = wave * PPW + ii;
+    __builtin_amdgcn_global_load_lds((const void*)(src[ii] + koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+  }
 };
 
 // ---- implicit-GEMM convolution stagers ---------------------------------------------------

@@ -428,11 +428,12 @@ def train_workload(model: str = "gpt2-tiny", steps: int = 20, num_workers: int =
                    checkpoint_storage_path: str | None = None, checkpoint=None, resume_mode: str = "exact",
                    max_failures: int = 0, seed: int = 1234, grad_comm_dtype: str = "fp32",
                    bucket_cap_mb: float = 32.0, zero_stage: int = 0, progress_timeout_s: float | None = 300.0,
-                   dataset_size: int = 1 << 20, name: str | None = None, verbose: int = 1):
+                   dataset_size: int = 1 << 20, name: str | None = None, verbose: int = 1,
+                   report_every_n_steps: int | None = None):
     """`train_fashion_mnist`'s counterpart for the bf16 workloads (R/my_ray_module.py:216-251)."""
     cfg = WorkloadConfig(model=model, steps=steps, batch_size_per_worker=batch_size_per_worker, seq_len=seq_len,
                          lr=lr, ckpt_every_n_steps=ckpt_every_n_steps, seed=seed, resume_mode=resume_mode,
-                         checkpoint=checkpoint, dataset_size=dataset_size)
+                         checkpoint=checkpoint, dataset_size=dataset_size, report_every_n_steps=report_every_n_steps)
     run_config = train.RunConfig(
         name=name, storage_path=checkpoint_storage_path, verbose=verbose,
         checkpoint_config=train.CheckpointConfig(num_to_keep=num_checkpoints_to_keep,

@@ -13,7 +13,7 @@ STEPS=${STEPS:-200}
 MORE=${MORE:-250}
 MODEL=${MODEL:-gpt2-small}
 timeout -k 10 400 python -u train_flow.py run --model $MODEL --steps $STEPS --ckpt_every_n_steps 50 \
-  --num_workers 1 > $OUT/run_a.log 2>&1
+  --num_workers 1 --report_every_n_steps 10 > $OUT/run_a.log 2>&1
 rc=$?; echo "RUN A EXIT $rc"; tail -n 3 $OUT/run_a.log
 [ $rc -eq 0 ] || exit $rc
 RID=$(sed -n 's/.*RayTorchTrain\/\([^ ]*\) starting.*/\1/p' $OUT/run_a.log | head -n 1)
@@ -23,7 +23,7 @@ timeout -k 10 400 python -u train_flow.py run --model $MODEL --steps $MORE --ckp
 rc=$?; echo "RUN B EXIT $rc"; tail -n 3 $OUT/run_b.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u train_flow.py run --model $MODEL --steps $MORE --ckpt_every_n_steps 50 \
-  --num_workers 1 > $OUT/run_c.log 2>&1
+  --num_workers 1 --report_every_n_steps 10 > $OUT/run_c.log 2>&1
 rc=$?; echo "RUN C EXIT $rc"; tail -n 3 $OUT/run_c.log
 [ $rc -eq 0 ] || exit $rc
 # collect the trial logs (result.json rows) of the three runs

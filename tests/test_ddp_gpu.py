@@ -117,7 +117,7 @@ def _check(out, ref, tol):
         assert err < tol, f"{n}: relative error {err:.3e}"
 
 
-@pytest.mark.parametrize("comm_dtype,tol", [("fp32", 2e-2), ("bf16", 3e-2)])
+@pytest.mark.parametrize("comm_dtype,tol", [("fp32", 5e-3), ("bf16", 5e-3)])
 def test_ddp_gloo_two_ranks_on_gpu_matches_concatenated_batch(comm_dtype, tol):
     out = _run(2, "gloo", comm_dtype)
     assert out[0][2]["grad_comm_dtype"] == comm_dtype
@@ -125,7 +125,7 @@ def test_ddp_gloo_two_ranks_on_gpu_matches_concatenated_batch(comm_dtype, tol):
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL DDP needs >= 2 GPUs (one rank per GPU)")
-@pytest.mark.parametrize("comm_dtype,tol", [("fp32", 2e-2), ("bf16", 3e-2)])
+@pytest.mark.parametrize("comm_dtype,tol", [("fp32", 5e-3), ("bf16", 5e-3)])
 def test_ddp_rccl_matches_concatenated_batch(comm_dtype, tol):
     world = min(torch.cuda.device_count(), 4)
     out = _run(world, "nccl", comm_dtype)

@@ -45,6 +45,8 @@ class RayTorchTrain(FlowSpec):
                       help="mlp (the reference workload) | gpt2-small | resnet18 | llama3-8b | gpt2-tiny | ...")
     steps = Parameter("steps", default=100, help="optimizer steps (bf16 workloads)")
     ckpt_every_n_steps = Parameter("ckpt_every_n_steps", default=25, help="sharded async checkpoint interval")
+    report_every_n_steps = Parameter("report_every_n_steps", default=0,
+                                     help="metrics rows between checkpoints (0: one row per checkpoint)")
     grad_comm_dtype = Parameter("grad_comm_dtype", default="fp32", help="fp32 | bf16 gradient all-reduce")
     zero_stage = Parameter("zero_stage", default=0, help="1: ZeRO-1 sharded optimizer step (bf16 workloads)")
 
@@ -101,7 +103,8 @@ class RayTorchTrain(FlowSpec):
                 else None, lr=None, ckpt_every_n_steps=int(self.ckpt_every_n_steps),
                 checkpoint_storage_path=current.ray_storage_path, checkpoint=args.get("checkpoint"),
                 resume_mode=mode, max_failures=int(self.max_failures), grad_comm_dtype=self.grad_comm_dtype,
-                zero_stage=int(self.zero_stage))
+                zero_stage=int(self.zero_stage),
+                report_every_n_steps=int(self.report_every_n_steps) or None)
         self.next(self.join)
 
     @step
