@@ -194,6 +194,6 @@ def enable_reproducibility(seed: int = 0) -> None:
     # ...but without its NaN fill of every torch.empty: the native kernels write every element
     # they allocate, and the fill is a full extra write pass over each activation (GPT-2-small:
     # 811 vs 888 samples/s through the trainer, profiles/product_path_gpt2_r3.md)
-    import torch.utils.deterministic
+    import torch.utils.deterministic as _det
 
-    torch.utils.deterministic.fill_uninitialized_memory = False
+    _det.fill_uninitialized_memory = False
