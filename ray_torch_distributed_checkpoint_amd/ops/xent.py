@@ -69,7 +69,9 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, n_valid: int | Non
 # (96 MB), 810.1 (48 MB): the per-chunk GEMM tails cost more than the HBM round trip saves.
 _LM_CHUNK_MB = float(os.environ.get("RTDC_LMHEAD_CHUNK_MB", "0"))
 _chunk_bufs: dict = {}
-_LM_BLASLT = os.environ.get("RTDC_LMHEAD_BLASLT", "1") != "0"
+# RTDC_LMHEAD_BLASLT=1: the logits product on hipBLASLt (A/B only; the default keeps every
+# model GEMM on the hand-written MFMA kernels)
+_LM_BLASLT = os.environ.get("RTDC_LMHEAD_BLASLT", "0") == "1"
 
 
 def _lm_chunk_rows(M: int, Vp: int) -> int:
@@ -106,11 +108,10 @@ class _LMHeadXent(torch.autograd.Function):
         R = _lm_chunk_rows(M, Vp)
         if R >= M:
             # [M, Vp] bf16, softmax gradient written in place.  The logits product is a plain
-            # GEMM (no epilogue - the fused work is the cross-entropy kernel after it), the one
-            # place hipBLASLt is measured ahead of the native persistent kernel on a GPT-2 shape
-            # (1172 vs 985 TF, profiles/gemm_bench_r2_warm.jsonl; step 19.35 -> 19.04 ms,
-            # profiles/lmhead_blaslt_ab.txt), so it runs there; RTDC_LMHEAD_BLASLT=0 keeps it
-            # on the MFMA kernel
+            # GEMM (no epilogue - the fused work is the cross-entropy kernel after it) on the
+            # persistent 8-wave MFMA kernel.  hipBLASLt measures ahead on this shape (1152 vs 996
+            # TF, profiles/gemm_bench_r3_4wave_v2.jsonl: ~0.2 ms/step); RTDC_LMHEAD_BLASLT=1
+            # selects it for A/B runs only
             logits = torch.matmul(x2, ws.t()) if _LM_BLASLT else G.linear_fwd(x2, ws)
             gpu_ext().xent(logits, logits, tgt, loss, None, None, M, vocab, Vp, scale, IGNORE_INDEX)
         else:

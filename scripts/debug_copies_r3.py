@@ -1,9 +1,10 @@
 """Who issues the device copies of a GPT-2 training step?  (~43
 `__amd_rocclr_copyBuffer` dispatches per step were unexplained.)
 
-Runs the bench.py GPT-2-small step under torch.profiler with Python stacks and prints, per
-copy-like op (aten::copy_, aten::clone, aten::contiguous, aten::to/_to_copy, Memcpy/Memset
-runtime events), the count per step grouped by the innermost frames of this repository.
+Runs the bench.py GPT-2-small step under a TorchDispatchMode that sees every ATen op the step
+dispatches (including the ones autograd issues from C++), and prints, per copy-like op
+(copy_, clone, _to_copy, contiguous copies, fills, cat), the count per step grouped by the
+innermost frames of this repository in the Python stack.
 
     python scripts/debug_copies_r3.py [--steps 3] [--model gpt2-small]
 """
@@ -13,11 +14,33 @@ import argparse
 import collections
 import os
 import sys
+import traceback
 
 import torch
+from torch.utils._python_dispatch import TorchDispatchMode
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+KEYS = ("copy", "clone", "_to_copy", "fill", "zero", "cat", "stack", "index", "scatter", "sort")
+
+
+class CopyLog(TorchDispatchMode):
+    def __init__(self):
+        super().__init__()
+        self.by_site = collections.Counter()
+        self.by_op = collections.Counter()
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        name = str(func.overloadpacket.__name__)
+        if any(k in name for k in KEYS):
+            dev = any(isinstance(a, torch.Tensor) and a.is_cuda for a in args)
+            if dev:
+                frames = [f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in traceback.extract_stack()
+                          if ("ray_torch_distributed_checkpoint_amd" in f.filename or f.filename.endswith("bench.py"))]
+                self.by_op[name] += 1
+                self.by_site[(name, " <- ".join(reversed(frames[-3:])) or "(no repo frame)")] += 1
+        return func(*args, **(kwargs or {}))
 
 
 def main():
@@ -27,8 +50,9 @@ def main():
     args = ap.parse_args()
     import bench
 
-    ns = argparse.Namespace(model=args.model, batch=16, seq_len=1024, batch_set=False, seq_len_set=False,
+    ns = argparse.Namespace(model=args.model, batch=None, seq_len=1024, batch_set=False, seq_len_set=False,
                             image_size=224)
+    ns.batch = 16
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     wl = bench.build_workload(ns, dev, 0)
@@ -44,36 +68,17 @@ def main():
     for i in range(3):
         step(i)
     torch.cuda.synchronize()
-    from torch.profiler import ProfilerActivity, profile
-
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    log = CopyLog()
+    with log:
         for i in range(args.steps):
             step(i)
-        torch.cuda.synchronize()
-    keys = ("copy", "clone", "contiguous", "_to_copy", "memcpy", "memset", "fill_", "zero_")
-    by_site = collections.Counter()
-    by_name = collections.Counter()
-    for ev in prof.events():
-        name = ev.name.lower()
-        if not any(k in name for k in keys):
-            continue
-        by_name[ev.name] += 1
-        frames = [f for f in (ev.stack or []) if "ray_torch_distributed_checkpoint_amd" in f or "bench.py" in f]
-        by_site[(ev.name, " <- ".join(frames[:3]) or "(no repo frame)")] += 1
-    print(f"== copy-like events per step ({args.steps} steps profiled)")
-    for n, c in by_name.most_common():
+    torch.cuda.synchronize()
+    print(f"== copy-like ATen ops on device tensors, per step ({args.steps} steps)")
+    for n, c in log.by_op.most_common():
         print(f"{c / args.steps:8.1f}  {n}")
-    print("== by call site (per step)")
-    for (n, site), c in by_site.most_common(40):
-        print(f"{c / args.steps:8.1f}  {n:32s} {site}")
-    kern = collections.Counter()
-    for ev in prof.key_averages():
-        if ev.device_type is not None and "cuda" in str(ev.device_type).lower():
-            kern[ev.key] = ev.count
-    print("== device-side events matching copy/fill (count over the profiled steps)")
-    for k, c in kern.most_common():
-        if any(x in k.lower() for x in ("copy", "fill", "memset", "memcpy")):
-            print(f"{c / args.steps:8.1f}  {k}")
+    print("== by call site (per step), innermost repository frames first")
+    for (n, site), c in log.by_site.most_common(60):
+        print(f"{c / args.steps:8.1f}  {n:20s} {site}")
 
 
 if __name__ == "__main__":
