@@ -107,12 +107,15 @@ _engine_cfg: tuple | None = None
 
 
 def default_writer_threads() -> int:
-    """Writer threads of this rank from a per-NODE budget: half the host's CPUs (CRC32 + pwrite
-    are CPU work) split over the node's ranks (LOCAL_WORLD_SIZE), 2..8 per rank.  A per-rank
+    """Writer threads of this rank from a per-NODE budget: half the CPUs this job may use
+    (cgroup quota / affinity, utils/hostinfo.py; CRC32 + pwrite are CPU work) split over the
+    node's ranks (LOCAL_WORLD_SIZE), 2..8 per rank; the threads run at background priority.  A per-rank
     default of min(8, ncpu/2) gave 8 ranks x 8 writers on one host, which starved the ranks'
     training threads during an async save (VERDICT r2 weak #5)."""
+    from ..utils.hostinfo import available_cpus
+
     local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
-    return max(2, min(8, (os.cpu_count() or 4) // (2 * local)))
+    return max(2, min(8, available_cpus() // (2 * local)))
 
 
 def configure_engine(nslots: int, slot_mb: int, writers: int = 0) -> None:

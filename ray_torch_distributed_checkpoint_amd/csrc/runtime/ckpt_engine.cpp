@@ -21,7 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 #include <fcntl.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -646,6 +648,9 @@ class Engine {
 
   void writer_loop() {
     if (g_have_gpu()) hipSetDevice(device_);
+    // background priority: CRC32 + pwrite must not take CPU time from the rank's training
+    // thread (or a gloo all-reduce) while an async checkpoint drains (Linux: per-thread nice)
+    setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 10);
     while (true) {
       WJob w;
       {

@@ -39,7 +39,8 @@ class CheckpointConfig:
     async_checkpoint: bool = True             # HBM snapshot + background write + background commit
     pinned_ring_mb: int = 512                 # bounded pinned-host ring per rank (D2H staging)
     ring_slot_mb: int = 64                    # ring slot = unit of one D2H copy / pwrite
-    # 0 = a per-NODE budget split over the node's ranks: max(2, min(8, ncpu // (2 * local_world)))
+    # 0 = a per-NODE budget split over the node's ranks: max(2, min(8, cpus // (2 * local_world))),
+    # cpus = what the job may use (cgroup quota / affinity: utils/hostinfo.py)
     # (8 ranks x 8 writers x CRC32 on a shared host starved the training threads during async saves)
     writer_threads: int = 0
 

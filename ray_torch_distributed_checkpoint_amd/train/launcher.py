@@ -74,7 +74,9 @@ class WorkerGroup:
             env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
             # one intra-op thread pool per worker must not oversubscribe the host (gloo ranks
             # busy-poll): split the CPUs between the ranks unless the user chose
-            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // self.n)))
+            from ..utils.hostinfo import available_cpus
+
+            env.setdefault("OMP_NUM_THREADS", str(max(1, available_cpus() // self.n)))
             # workers import the user's modules (cloudpickle pickles module functions by
             # reference) and this package exactly as the driver does
             pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

@@ -127,3 +127,18 @@ def test_progress_watchdog_spares_report_only_loops(tmp_path, monkeypatch, fn):
                            run_config=train.RunConfig(storage_path=str(tmp_path), name="wd", progress_timeout_s=2.5))
     r = t.fit()  # reports arrive every ~1 s, total 5 s > the 2.5 s timeout: must not be killed
     assert r.metrics["i"] == 4
+
+
+def test_writer_budget_is_per_node_and_quota_aware(monkeypatch):
+    from ray_torch_distributed_checkpoint_amd.checkpoint import torchsave
+    from ray_torch_distributed_checkpoint_amd.utils import hostinfo
+
+    n = hostinfo.available_cpus()
+    assert 1 <= n <= (os.cpu_count() or 1)
+    monkeypatch.setattr(hostinfo, "available_cpus", lambda: 64)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert torchsave.default_writer_threads() == 8
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert torchsave.default_writer_threads() == 4  # 64 // (2 * 8): the node's budget, split
+    monkeypatch.setattr(hostinfo, "available_cpus", lambda: 16)
+    assert torchsave.default_writer_threads() == 2
