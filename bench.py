@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (multi-rank rehearsal on 1 GPU)")
     ap.add_argument("--cpu", action="store_true",
                     help="run on the CPU (gloo; a plumbing rehearsal of the N-rank path, e.g. in CI - not a benchmark)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the distributed path (DDP + collectives) even with one rank (RCCL rehearsal)")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="checkpoint phase only (1 process): plan the sharded save/restore as rank "
                          "--simulate-rank of a W-rank data-parallel job and write/read just that rank's "
@@ -100,6 +102,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --force-dist: the multi-GPU code path (process group, DDP with the native bucket engine and
+    # an all-reduce of every bucket, preflight, in-sync check, bucket sweep, rank-sharded
+    # checkpoint) in a 1-rank group - a one-GPU rehearsal of RCCL for the driver's 8-GPU run
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
     if args.cpu:
         dev = torch.device("cpu")
         args.backend = "gloo"
@@ -107,7 +118,7 @@ def main():
         ndev = max(1, torch.cuda.device_count())
         torch.cuda.set_device(local % ndev)
         dev = torch.device("cuda", local % ndev)
-    if world > 1:
+    if dist_on:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -120,7 +131,7 @@ def main():
     if not args.cpu:
         _ext.gpu_ext()  # native kernels are mandatory on the GPU path
     sync = (lambda: None) if args.cpu else torch.cuda.synchronize
-    pre = preflight(world, rank, dev, args) if world > 1 else None
+    pre = preflight(world, rank, dev, args) if dist_on else None
     torch.manual_seed(1234)
     wl = build_workload(args, dev, rank)
     model, opt = wl["model"], wl["opt"]
@@ -128,7 +139,7 @@ def main():
     # end of backward) overlaps the fused optimizer's update of every other parameter
     net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, defer_tail_to_optimizer=True,
                                   grad_comm_dtype=args.grad_comm_dtype, p2p_max_kb=args.p2p_kb,
-                                  zero_stage=args.zero) if world > 1 else model
+                                  zero_stage=args.zero, force_collectives=args.force_dist) if dist_on else model
     B, T = wl["batch"], wl["seq_len"]
     fwd_loss = wl["loss"]
     overlap = None
@@ -136,7 +147,7 @@ def main():
         from ray_torch_distributed_checkpoint_amd.optim import BackwardOverlap
 
         try:
-            overlap = BackwardOverlap(opt, net if world > 1 else None)
+            overlap = BackwardOverlap(opt, net if dist_on else None)
         except ValueError as e:  # e.g. fp32 gradients over gloo (no averaging collective)
             print(f"[bench] optimizer/backward overlap off: {e}", file=sys.stderr)
 
@@ -159,27 +170,27 @@ def main():
     for i in range(args.warmup):
         loss = step(i)
     sync()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
     sync()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     sync()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         tt = torch.tensor([dt], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = tt.item()
     ms_per_step = dt / args.steps * 1e3
     samples_per_s = world * B * args.steps / dt
     final_loss = loss.item()
-    comm_plan = net.comm_plan() if world > 1 else None
+    comm_plan = net.comm_plan() if dist_on else None
     # every rank must hold bitwise the same parameters (and, without ZeRO, optimizer state)
-    in_sync = ranks_in_sync(model, opt, world, dev) if world > 1 else None
+    in_sync = ranks_in_sync(model, opt, world, dev) if dist_on else None
 
     ck = {}
     if not args.no_ckpt:
@@ -192,7 +203,7 @@ def main():
             print(f"[bench] rank {rank}: {ck['ckpt_unmeasured']}", file=sys.stderr, flush=True)
 
     sweep = None
-    if world > 1 and args.sweep and args.zero == 0 and not args.overlap_opt:
+    if dist_on and args.sweep and args.zero == 0 and not args.overlap_opt:
         try:
             sweep = comm_sweep(args, model, opt, net, cur, step, world, sync)
         except Exception as e:  # noqa: BLE001
@@ -223,11 +234,11 @@ def main():
     if wl.get("tokens_per_sample"):
         out["tokens_per_sec"] = round(samples_per_s * wl["tokens_per_sample"], 1)
     # self-description of the communication setup (what ran, on how many ranks)
-    comm = {"world_size": world, "backend": (dist.get_backend() if world > 1 else None),
+    comm = {"world_size": world, "backend": (dist.get_backend() if dist_on else None),
             "optimizer_overlapped_with_backward": overlap is not None,
             "rccl_version": _rccl_version(),
             "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"}
-    if world > 1:
+    if dist_on:
         comm.update(comm_plan)
         comm["allreduce_GB_per_s_needed_at_this_step_time"] = round(
             comm["allreduce_bytes_per_step"] * 2 * (world - 1) / world / (ms_per_step / 1e3) / 1e9, 2)
@@ -239,7 +250,7 @@ def main():
     out.update(ck)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 
@@ -328,7 +339,8 @@ def comm_sweep(args, model, opt, net, cur, step, world, sync) -> list:
     net.detach()
     for dtype in ("fp32", "bf16"):
         for cap in (16.0, 32.0, 64.0, 128.0):
-            w = DistributedDataParallel(model, bucket_cap_mb=cap, defer_tail_to_optimizer=True, grad_comm_dtype=dtype)
+            w = DistributedDataParallel(model, bucket_cap_mb=cap, defer_tail_to_optimizer=True, grad_comm_dtype=dtype,
+                                        force_collectives=args.force_dist)
             cur["net"] = w
             step(0)
             sync()
@@ -424,7 +436,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     if rank == 0:
         shutil.rmtree(path, ignore_errors=True)
         os.makedirs(path, exist_ok=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
 
     from ray_torch_distributed_checkpoint_amd.checkpoint.state_dict import get_state_dict, set_state_dict
@@ -474,14 +486,14 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     sync()
     overlap_ms = (time.perf_counter() - t1) / max(1, args.overlap_steps) * 1e3
     local_write = h.wait()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     h._finish()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t_durable = time.perf_counter() - t0
     nbytes = torch.tensor([float(h.nbytes)], device=dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(nbytes)
     if rank == 0:
         shutil.rmtree(path, ignore_errors=True)  # keep one checkpoint on disk at a time
@@ -489,7 +501,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     path2 = path + "_sync"
     if rank == 0:
         shutil.rmtree(path2, ignore_errors=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     sync()
     t2 = time.perf_counter()
@@ -500,25 +512,25 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     # posix_fadvise(DONTNEED) after its fsync, so the bytes come from the device)
     def restore():
         sync()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         t3 = time.perf_counter()
         sd = state()
         dcp.load(sd, path2, simulate=sim)
         set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
         sync()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         return time.perf_counter() - t3
 
     t_restore_warm = restore()
     resident = drop_page_cache(path2)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t_restore = restore()
     vals = torch.tensor([t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm, resident],
                         device=dev, dtype=torch.float64)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
     t_resume, t_durable, t_sync, t_restore, overlap_ms, local_write, t_restore_warm, resident = vals.tolist()
     if rank == 0:

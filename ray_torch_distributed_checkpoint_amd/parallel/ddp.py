@@ -67,7 +67,7 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: float = 2.0, broadcast_buffers: bool = True, device_ids=None,
                  output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  defer_tail_to_optimizer: bool = False, grad_comm_dtype: str = "fp32", p2p_max_kb: float = 0.0,
-                 zero_stage: int = 0, p2p_timeout_s: float = 30.0):
+                 zero_stage: int = 0, p2p_timeout_s: float = 30.0, force_collectives: bool = False):
         super().__init__()
         if grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
@@ -82,6 +82,10 @@ class DistributedDataParallel(nn.Module):
         self.defer_tail = defer_tail_to_optimizer
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # force_collectives: run the whole communication path (native engine, RCCL all-reduce
+        # of every bucket, buffer broadcasts) even in a 1-rank group - a one-GPU rehearsal of the
+        # multi-GPU code path against the real backend (an all-reduce over one rank is the identity)
+        self._collective = self.world_size > 1 or (force_collectives and dist.is_initialized())
         self.broadcast_buffers = broadcast_buffers
         params = [p for p in module.parameters() if p.requires_grad]
         self.zero = zero_stage == 1 and self.world_size > 1
@@ -110,7 +114,7 @@ class DistributedDataParallel(nn.Module):
         backend = dist.get_backend(process_group) if dist.is_initialized() else "gloo"
         self._use_avg = backend == "nccl"
         # one flat broadcast of all parameters from rank 0
-        if self.world_size > 1:
+        if self._collective:
             dist.broadcast(self.space.data, src=0, group=process_group)
             self.space.refresh_shadows()
         self._bufspace = None
@@ -132,7 +136,7 @@ class DistributedDataParallel(nn.Module):
                 self._bufspace = (flat, None)
             else:
                 self._bufspace = (flat, list(zip(bufs, views)))
-            if self.world_size > 1:
+            if self._collective:
                 self._sync_buffers()
         # static bucket plan over the flat gradient buffer (caps in communicated bytes)
         self.buckets: list[_Bucket] = []
@@ -167,9 +171,9 @@ class DistributedDataParallel(nn.Module):
         self._comm = None
         self.p2p = None
         self.p2p_max_bytes = 0
-        if self.world_size > 1 and grad_comm_dtype == "bf16":
+        if self._collective and grad_comm_dtype == "bf16":
             self._comm = torch.empty(self.space.numel, dtype=torch.bfloat16, device=dev)
-        if self.world_size > 1:
+        if self._collective:
             self._verify_plan_across_ranks()
             self._engine = self._native_engine(process_group)
             self._attach_p2p(process_group, p2p_max_kb)
@@ -296,7 +300,7 @@ class DistributedDataParallel(nn.Module):
 
     def forward(self, *args, **kwargs):
         self.space.wait_pending_tail()
-        if self.world_size > 1 and self.broadcast_buffers and self._bufspace is not None and self.training:
+        if self._collective and self.broadcast_buffers and self._bufspace is not None and self.training:
             self._sync_buffers()
         return self.module(*args, **kwargs)
 

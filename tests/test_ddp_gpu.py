@@ -41,7 +41,7 @@ def _batch(world, dev):
     return torch.randint(0, 1000, (world * B, T + 1), generator=g).to(dev)
 
 
-def _worker(rank, world, port, backend, comm_dtype, q):
+def _worker(rank, world, port, backend, comm_dtype, q, force=False):
     try:
         import torch.distributed as dist
 
@@ -54,7 +54,8 @@ def _worker(rank, world, port, backend, comm_dtype, q):
         from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
 
         model = _model(dev)
-        net = DistributedDataParallel(model, grad_comm_dtype=comm_dtype, bucket_cap_mb=0.25, first_bucket_mb=0.05)
+        net = DistributedDataParallel(model, grad_comm_dtype=comm_dtype, bucket_cap_mb=0.25, first_bucket_mb=0.05,
+                                      force_collectives=force)
         data = _batch(world, dev)[rank * B:(rank + 1) * B]
         for _ in range(2):  # second step: buckets reused, fresh-gradient mode
             net.space.zero_grad(set_to_none=True)
@@ -71,13 +72,13 @@ def _worker(rank, world, port, backend, comm_dtype, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def _run(world, backend, comm_dtype):
+def _run(world, backend, comm_dtype, force=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, backend, comm_dtype, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, backend, comm_dtype, q, force)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}
@@ -130,6 +131,24 @@ def test_ddp_rccl_matches_concatenated_batch(comm_dtype, tol):
     world = min(torch.cuda.device_count(), 4)
     out = _run(world, "nccl", comm_dtype)
     _check(out, _reference(world), tol)
+
+
+@pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
+def test_ddp_rccl_one_rank_forced_collectives(comm_dtype):
+    """RCCL on a one-GPU box: a 1-rank nccl group with force_collectives runs the real multi-GPU
+    path - native bucket engine, c10d RCCL all-reduce (AVG) of every bucket on its side stream,
+    bf16 rounding/widening - and must leave exactly the single-process gradient (fp32: an
+    all-reduce over one rank is the identity) or its bf16 rounding."""
+    out = _run(1, "nccl", comm_dtype, force=True)
+    plan = out[0][2]
+    assert plan["engine"] == "native" and plan["grad_comm_dtype"] == comm_dtype and out[0][1] > 3
+    ref = _reference(1)
+    for n, v in ref.items():
+        g = torch.from_numpy(out[0][0][n])
+        if comm_dtype == "fp32":
+            assert torch.equal(g, v), n
+        else:
+            assert torch.equal(g, v.to(torch.bfloat16).float()), n
 
 
 def _losses(path):
