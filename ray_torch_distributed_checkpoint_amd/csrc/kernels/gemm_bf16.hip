@@ -105,11 +105,28 @@ __device__ __forceinline__ void conv_tile_stats(const GemmArgs& a, const f32x4 (
   }
 }
 
-template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0>
-__global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
+// outstanding glds allowed at an NS-stage wait: `ahead` later stages of LPS loads each
+// (wave-uniform; immediates only)
+template <int LPS>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// NS = 2: two LDS stages, every k-step ends with vmcnt(0) + __syncthreads() (two blocks/CU).
+// NS = 3 / 4 (the implicit-GEMM convolutions' thin tiles, one block/CU): NS-1 k-tiles in flight
+// across each barrier - at step t the wait retires only tile t (counted vmcnt, never 0 before
+// the last steps), a raw s_barrier publishes it, then tile t+NS-1 is issued into the stage that
+// step t-1 read (every wave passed the barrier after consuming its fragments: WAR-safe).  With
+// 9-18 k-tiles per tile and 128-256 x 64 outputs the 2-stage loop exposed one global-load
+// latency per k-step (the N = 64 convolutions ran at 300-430 TF).
+template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0, int NS = 2>
+__global__ __launch_bounds__(CFG::NT, NS == 2 ? 2 : 1) void gemm_bf16_kernel(GemmArgs a) {
   using namespace gemm;
   constexpr int BM = CFG::BM, BN = CFG::BN, TM = CFG::TM, TN = CFG::TN, WN = CFG::WN, NW = CFG::NW;
-  __shared__ __attribute__((aligned(16))) char smem[2 * CFG::STAGE];
+  static_assert(NS >= 2 && NS <= 4, "2..4 LDS stages");
+  __shared__ __attribute__((aligned(16))) char smem[NS * CFG::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -174,17 +191,40 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
 #define BUF_A(s) (smem + (s) * CFG::STAGE)
 #define BUF_B(s) (smem + (s) * CFG::STAGE + CFG::A_BYTES)
 
-  if (nt > 0) {
-    sa.issue(kb, BUF_A(0), wave);
-    sb.issue(kb, BUF_B(0), wave);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  if constexpr (NS == 2) {
+    if (nt > 0) {
+      sa.issue(kb, BUF_A(0), wave);
+      sb.issue(kb, BUF_B(0), wave);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nt) {
+        sa.issue(kb + s * BK, BUF_A(s), wave);
+        sb.issue(kb + s * BK, BUF_B(s), wave);
+      }
   }
   for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) {
-      sa.issue(kb + (t + 1) * BK, BUF_A(cur ^ 1), wave);
-      sb.issue(kb + (t + 1) * BK, BUF_B(cur ^ 1), wave);
+    int cur;
+    if constexpr (NS == 2) {
+      cur = t & 1;
+      if (t + 1 < nt) {
+        sa.issue(kb + (t + 1) * BK, BUF_A(cur ^ 1), wave);
+        sb.issue(kb + (t + 1) * BK, BUF_B(cur ^ 1), wave);
+      }
+    } else {
+      constexpr int LPS = (BM / 8) / NW + (BN / 8) / NW;  // glds per thread per stage
+      cur = t % NS;
+      wait_stages<LPS>(min(NS - 2, nt - 1 - t));
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + NS - 1 < nt) {
+        const int st = (t + NS - 1) % NS;
+        sa.issue(kb + (t + NS - 1) * BK, BUF_A(st), wave);
+        sb.issue(kb + (t + NS - 1) * BK, BUF_B(st), wave);
+      }
     }
     const char* tA = BUF_A(cur);
     const char* tB = BUF_B(cur);
@@ -210,8 +250,10 @@ __global__ __launch_bounds__(CFG::NT, 2) void gemm_bf16_kernel(GemmArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[j], va[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (NS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 #undef BUF_A
 #undef BUF_B
@@ -361,10 +403,29 @@ static inline long long ntiles(const GemmArgs& a) {
   return (long long)((a.M + CFG::BM - 1) / CFG::BM) * ((a.N + CFG::BN - 1) / CFG::BN);
 }
 
-template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0>
+template <class CFG, bool AK, bool BKM, typename OutT, int GM = 0, int NS = 2>
 static void launch_cfg(const GemmArgs& a, int batch, hipStream_t st) {
   dim3 grid((unsigned)ntiles<CFG>(a), a.splitk > 1 ? a.splitk : 1, batch), block(CFG::NT);
-  hipLaunchKernelGGL((gemm_bf16_kernel<CFG, AK, BKM, OutT, GM>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<CFG, AK, BKM, OutT, GM, NS>), grid, block, 0, st, a);
+}
+
+// LDS stages of the implicit-GEMM convolution kernels (RTDC_CONV_NS=2|3|4; see the NS note at
+// gemm_bf16_kernel)
+static int conv_stages() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_CONV_NS");
+    v = (e && e[0] >= '2' && e[0] <= '4') ? e[0] - '0' : 2;
+  }
+  return v;
+}
+template <class CFG, bool AK, bool BKM, typename OutT, int GM>
+static void launch_conv(const GemmArgs& a, hipStream_t st) {
+  switch (conv_stages()) {
+    case 3: launch_cfg<CFG, AK, BKM, OutT, GM, 3>(a, 1, st); break;
+    case 4: launch_cfg<CFG, AK, BKM, OutT, GM, 4>(a, 1, st); break;
+    default: launch_cfg<CFG, AK, BKM, OutT, GM, 2>(a, 1, st); break;
+  }
 }
 
 template <bool AK, bool BKM, typename OutT>
@@ -576,18 +637,18 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
     if (a.M != a.cv_npix) return 1;
     // stats rows are per BM-row tile: 256 (256x64 tiles) or 128
     if (a.stats_mean) {
-      if (a.N <= 64) launch_cfg<Cfg256x64, true, true, bf16_t, 3>(a, 1, stream);
-      else launch_cfg<Cfg128x128, true, true, bf16_t, 3>(a, 1, stream);
+      if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 3>(a, stream);
+      else launch_conv<Cfg128x128, true, true, bf16_t, 3>(a, stream);
     } else {
-      if (a.N <= 64) launch_cfg<Cfg256x64, true, true, bf16_t, 1>(a, 1, stream);
-      else launch_cfg<Cfg128x128, true, true, bf16_t, 1>(a, 1, stream);
+      if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 1>(a, stream);
+      else launch_conv<Cfg128x128, true, true, bf16_t, 1>(a, stream);
     }
   } else if (mode == 2) {
     if (a.K < a.cv_npix || a.stats_mean) return 1;
     const bool narrow = a.M <= 64;
-    a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a));
-    if (narrow) launch_cfg<Cfg64x256, false, false, float, 2>(a, 1, stream);
-    else launch_cfg<Cfg128x128, false, false, float, 2>(a, 1, stream);
+    a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a), conv_stages() > 2 ? 256 : 512);
+    if (narrow) launch_conv<Cfg64x256, false, false, float, 2>(a, stream);
+    else launch_conv<Cfg128x128, false, false, float, 2>(a, stream);
     if (a.splitk > 1) launch_splitk_reduce<float>(a, stream);
   } else {
     return 1;
