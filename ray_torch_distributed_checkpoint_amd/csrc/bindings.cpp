@@ -19,6 +19,7 @@ extern "C" {
 int rtdc_gemm_bf16(const rtdc::GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
                    hipStream_t stream);
 int rtdc_gemm_f32(const rtdc::GemmF32Args* args, hipStream_t st);
+int rtdc_gemm8_grouped(const rtdc::GemmArgs* args, int n, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 int rtdc_conv_gemm(const rtdc::GemmArgs* args, int mode, hipStream_t stream);
 int rtdc_layernorm_fwd(const void* x, const void* g, const void* b, void* y, float* mean, float* rstd,
                        int M, int D, float eps, hipStream_t st);
@@ -159,6 +160,45 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
   TORCH_CHECK(!(act == 3 || act == 4 || act == 6) || a.aux_in, "activation backward needs aux_in");
   check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream()),
            "gemm_bf16");
+}
+
+// Independent plain products C_i = A_i . B_i in ONE launch of the 8-wave kernel (gemm_8ph.hip
+// gemm8g_kernel): dims = [M, N, K, lda, ldb, ldc] per product.  Layouts / output dtype shared;
+// currently the weight-gradient form (both operands MN-major, fp32 C).
+static void gemm_bf16_grouped(std::vector<Tensor> A, std::vector<Tensor> B, std::vector<Tensor> C,
+                              std::vector<int64_t> dims, bool a_kmajor, bool b_kmajor) {
+  const size_t n = A.size();
+  TORCH_CHECK(n >= 1 && n <= 8 && B.size() == n && C.size() == n && dims.size() == 6 * n,
+              "gemm_bf16_grouped: 1..8 products, 6 dims each");
+  std::vector<rtdc::GemmArgs> args(n);
+  const bool fp32 = C[0].scalar_type() == at::kFloat;
+  for (size_t i = 0; i < n; ++i) {
+    check_dev(A[i], "A");
+    check_dev(B[i], "B");
+    check_dev(C[i], "C");
+    TORCH_CHECK(A[i].scalar_type() == at::kBFloat16 && B[i].scalar_type() == at::kBFloat16, "A/B must be bf16");
+    TORCH_CHECK((C[i].scalar_type() == at::kFloat) == fp32, "gemm_bf16_grouped: one output dtype");
+    const int64_t* d = &dims[6 * i];
+    const int64_t M = d[0], N = d[1], K = d[2];
+    TORCH_CHECK(K % 64 == 0 && M % 8 == 0 && N % 8 == 0 && d[3] % 8 == 0 && d[4] % 8 == 0 && d[5] % 4 == 0,
+                "gemm_bf16_grouped: need K%64==0, M%8==0, N%8==0 and 16-B leading dims");
+    // the operands must cover what the kernel reads (MN-major: K rows of ld elements)
+    TORCH_CHECK(A[i].numel() >= (a_kmajor ? M * d[3] : K * d[3]) && B[i].numel() >= (b_kmajor ? N * d[4] : K * d[4]) &&
+                    C[i].numel() >= M * d[5],
+                "gemm_bf16_grouped: operand smaller than its dims");
+    rtdc::GemmArgs& a = args[i];
+    a = rtdc::GemmArgs{};
+    a.A = (const uint16_t*)A[i].data_ptr();
+    a.B = (const uint16_t*)B[i].data_ptr();
+    a.C = C[i].data_ptr();
+    a.M = (int)M; a.N = (int)N; a.K = (int)K;
+    a.lda = (int)d[3]; a.ldb = (int)d[4]; a.ldc = (int)d[5];
+    a.batch_inner = 1;
+    a.alpha = 1.f;
+    a.splitk = 1;
+    a.tile_cfg = -1;
+  }
+  check_rc(rtdc_gemm8_grouped(args.data(), (int)n, a_kmajor, b_kmajor, fp32, cur_stream()), "gemm_bf16_grouped");
 }
 
 static void gemm_f32(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c10::optional<Tensor> bias,
@@ -766,6 +806,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.doc() = "MI355X (gfx950) kernels and native checkpoint engine";
   m.def("gemm_bf16", &gemm_bf16);
+  m.def("gemm_bf16_grouped", &gemm_bf16_grouped);
   m.def("gemm_f32", &gemm_f32);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);

@@ -300,8 +300,11 @@ __device__ __forceinline__ void wait_vm(int allowed) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool AK, bool BKM, typename OutT, int BN = 256>
-__global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
+// The kernel body over one (tile, K-slice): `bid` = the product's flat tile id, `ks` = the split-K
+// slice.  gemm8_kernel runs one product (bid = blockIdx.x, ks = blockIdx.y); gemm8g_kernel a
+// group of independent products in one launch.
+template <bool AK, bool BKM, typename OutT, int BN>
+__device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, const int ks) {
   // BN = 256: waves 2 (A) x 4 (B), quadrant 64x32; BN = 192: waves 4 x 2, quadrant 32x48
   constexpr int BH = BN / 2, WA = BN == 256 ? 2 : 4, WB = 8 / WA;
   constexpr int SA = 128 / WA, SB = BH / WB, TMQ = SA / 16, TNQ = SB / 16;
@@ -315,14 +318,14 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   int tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, tm, tn);
+  tile_coords(bid, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   int kb = 0, ke = a.K;
   if (a.splitk > 1) {
     const int ktiles = a.K / gemm::BK;
     const int per = (ktiles + a.splitk - 1) / a.splitk;
-    kb = blockIdx.y * per * gemm::BK;
+    kb = ks * per * gemm::BK;
     ke = min(a.K, kb + per * gemm::BK);
   }
   const int nt = ke > kb ? (ke - kb) / gemm::BK : 0;
@@ -448,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
   // ---- epilogue: lane holds C[m][n..n+3] of every (quadrant, i, j) fragment ----
   const float alpha = a.alpha_dev ? a.alpha * *a.alpha_dev : a.alpha;
   if (a.splitk > 1) {
-    float* Wp = a.ws + (long long)blockIdx.y * a.M * a.N;
+    float* Wp = a.ws + (long long)ks * a.M * a.N;
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
@@ -470,6 +473,33 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
     return;
   }
   tile_epilogue<OutT, TMQ, TNQ, SA, SB, BH, false>(a, acc, m0, n0, wa, wb, lane, alpha);
+}
+
+template <bool AK, bool BKM, typename OutT, int BN = 256>
+__global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
+  gemm8_body<AK, BKM, OutT, BN>(a, blockIdx.x, blockIdx.y);
+}
+
+// ---- grouped launch: independent products (same layouts, 256x256 tiles, no split-K) in one
+// grid - block b works on tile b - start[p] of product p.  The weight gradients of GPT-2's
+// linears are 9..36 tiles each with K = 16384: alone each one needs split-K slabs + a reduce
+// kernel to fill the chip; two layers' eight products together are 216 full-K tiles, one
+// round, with no slab traffic (ops/gemm.py WgradGroup).
+constexpr int G8_MAX_GROUP = 8;
+struct GemmGroup {
+  GemmArgs g[G8_MAX_GROUP];
+  int start[G8_MAX_GROUP + 1];
+  int n;
+};
+
+template <bool AK, bool BKM, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm8g_kernel(GemmGroup gg) {
+  const int b = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < G8_MAX_GROUP; ++i) p += (i < gg.n && b >= gg.start[i]) ? 1 : 0;
+  p = __builtin_amdgcn_readfirstlane(p);
+  gemm8_body<AK, BKM, OutT, 256>(gg.g[p], b - gg.start[p], 0);
 }
 
 // ---- persistent variant: one block per CU walks its tiles; the K-tile event stream runs on
@@ -1046,6 +1076,35 @@ extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmaj
 }
 
 #endif  // RTDC_G4_ONLY
+
+// Grouped 8-wave launch (gemm8g_kernel): n <= 8 products, every one K % 64 == 0, splitk 1,
+// 256x256 tiles; layouts and output dtype shared.  Returns 1 for an unsupported group.
+extern "C" int rtdc_gemm8_grouped(const GemmArgs* args, int n, int a_kmajor, int b_kmajor, int out_fp32,
+                                  hipStream_t st) {
+  if (n < 1 || n > g8::G8_MAX_GROUP) return 1;
+  g8::GemmGroup gg{};
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& a = args[i];
+    if (a.K % gemm::BK != 0 || a.K < gemm::BK || a.splitk > 1 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
+    gg.g[i] = a;
+    gg.g[i].splitk = 1;
+    gg.start[i] = tiles;
+    tiles += ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  }
+  gg.start[n] = tiles;
+  gg.n = n;
+  dim3 grid((unsigned)tiles, 1, 1), block(512);
+#define G8G(AK, BKM, T) hipLaunchKernelGGL((g8::gemm8g_kernel<AK, BKM, T>), grid, block, 0, st, gg)
+  if (out_fp32) {
+    if (!a_kmajor && !b_kmajor) G8G(false, false, float);
+    else return 1;
+  } else {
+    return 1;
+  }
+#undef G8G
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 // 4-wave 256x256 kernel (gemm4_kernel): same contract as rtdc_gemm8_launch with bn = 256.
 extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st) {

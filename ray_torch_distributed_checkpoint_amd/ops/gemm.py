@@ -116,10 +116,116 @@ def _round_split_rows(rows: int, cols: int, k: int, device) -> int:
     return tm_main * 256
 
 
-def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0, alpha_dev=None):
-    """dw[N,K] (fp32) = alpha (* alpha_dev[0]) * dy[M,N]^T @ x[M,K]."""
+# ---- grouped weight gradients ---------------------------------------------------------------
+# GPT-2's linear weight gradients are small outputs over a long K (tokens): 9..36 tiles of
+# 256x256 each with K = 16384.  Launched one by one each needs split-K fp32 slabs plus a reduce
+# kernel to fill 256 CUs (and the 768x768 one still runs at ~420 TF).  Deferred and launched
+# together (gemm_8ph.hip gemm8g_kernel), two layers' eight products are 216 full-K tiles - one
+# round of the chip, no slabs, no reduce.  A deferred product writes its output (a parameter's
+# slice of the flat gradient buffer, handed to autograd before the kernel ran) at the flush, so
+# every consumer of a parameter's "gradient ready" event goes through `when_grad_ready` (DDP
+# bucket marks, the backward-overlapped optimizer), and the flush runs at the latest when the
+# backward pass ends (an autograd final callback; DDP's finalize and the fused optimizers flush
+# first too).  RTDC_WGRAD_GROUP=0 launches every weight gradient immediately.
+_GROUP_ON = os.environ.get("RTDC_WGRAD_GROUP", "1") != "0"
+_GROUP_MAX = 8        # products per launch (gemm8g_kernel)
+_GROUP_TILES = 200    # flush once the pending products fill ~a round of 256 CUs
+
+
+class _WgradGroup:
+    def __init__(self):
+        self.items = []      # (dy, x2d, out, tiles)
+        self.tiles = 0
+        self.ptrs = set()    # data_ptr of every pending output
+        self.waiters = []    # (callback) in registration order, run after the flush
+        self.cb_queued = False
+
+    def add(self, dy, x2d, out, tiles) -> bool:
+        if not self.cb_queued:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+            except RuntimeError:  # not inside a backward pass: nothing would flush - run now
+                return False
+            self.cb_queued = True
+        # keep an alias, not `out` itself: AccumulateGrad adopts the returned tensor as p.grad
+        # without a copy only while nothing else references it (otherwise it clones the still
+        # unwritten buffer)
+        self.items.append((dy, x2d, out.view(out.shape), tiles))
+        self.tiles += tiles
+        self.ptrs.add(out.data_ptr())
+        if self.tiles >= _GROUP_TILES or len(self.items) >= _GROUP_MAX:
+            self.flush()
+        return True
+
+    def _end_of_backward(self):
+        self.cb_queued = False
+        self.flush()
+
+    def pending(self, t) -> bool:
+        return t is not None and bool(self.ptrs) and t.data_ptr() in self.ptrs
+
+    def flush(self):
+        if self.items:
+            items, self.items, self.tiles = self.items, [], 0
+            for i in range(0, len(items), _GROUP_MAX):
+                chunk = items[i:i + _GROUP_MAX]
+                dims = []
+                for dy, x2d, out, _ in chunk:
+                    M, N = dy.shape
+                    K = x2d.shape[1]
+                    dims += [N, K, M, N, K, K]
+                gpu_ext().gemm_bf16_grouped([c[0] for c in chunk], [c[1] for c in chunk], [c[2] for c in chunk],
+                                            dims, False, False)
+            self.ptrs = set()
+        waiters, self.waiters = self.waiters, []
+        for fn in waiters:
+            fn()
+
+
+_WG = _WgradGroup()
+
+
+def flush_wgrads() -> None:
+    """Launch every deferred weight gradient now (and run the gradient-ready callbacks that
+    waited for them)."""
+    _WG.flush()
+
+
+def when_grad_ready(p: torch.Tensor, fn) -> None:
+    """Run fn() once p's gradient is final: now, or right after the flush that writes it."""
+    if _WG.pending(p.grad):
+        _WG.waiters.append(fn)
+    else:
+        fn()
+
+
+def _groupable(dy, x2d, out, accumulate, alpha, alpha_dev) -> int:
+    """Tiles of a weight gradient that may be deferred into a grouped launch, else 0: plain
+    products that would otherwise split K (fewer than 200 output tiles, long K)."""
+    if not (_GROUP_ON and dy.is_cuda and out is not None and not accumulate and alpha == 1.0 and alpha_dev is None
+            and out.dtype == torch.float32 and out.is_contiguous() and dy.is_contiguous() and x2d.is_contiguous()
+            and dy.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16):
+        return 0
     M, N = dy.shape
     K = x2d.shape[1]
+    tiles = ((N + 255) // 256) * ((K + 255) // 256)
+    if M % 64 or N % 8 or K % 8 or M < 64 * 64 or tiles >= _GROUP_TILES or N < 256 or K < 256:
+        return 0
+    for t in (dy, x2d, out):
+        if t.data_ptr() % 16:
+            return 0
+    return tiles
+
+
+def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0, alpha_dev=None):
+    """dw[N,K] (fp32) = alpha (* alpha_dev[0]) * dy[M,N]^T @ x[M,K].  A product written into a
+    flat-buffer gradient slice during backward may be deferred into a grouped launch (see
+    `_WgradGroup`): its `out` is final after `flush_wgrads()` / at the end of backward."""
+    M, N = dy.shape
+    K = x2d.shape[1]
+    tiles = _groupable(dy, x2d, out, accumulate, alpha, alpha_dev)
+    if tiles and _WG.add(dy, x2d, out, tiles):
+        return out
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
     split = _round_split_rows(N, K, M, dy.device) if (_ROUND_SPLIT and dy.is_cuda and dy.is_contiguous()

@@ -251,6 +251,9 @@ class _FlatOptimizer(torch.optim.Optimizer):
         return sd
 
     def zero_grad(self, set_to_none: bool = True):
+        from ..ops.gemm import flush_wgrads
+
+        flush_wgrads()  # (a deferred weight gradient must not land after the reset)
         if self._space is not None and self._space.grad is not None:
             self._space.zero_grad(set_to_none=set_to_none)
         else:
@@ -408,10 +411,13 @@ class FusedAdamW(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        from ..ops.gemm import flush_wgrads
+
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        flush_wgrads()  # weight gradients deferred into a grouped launch (normally flushed by backward's end)
         if self._flat_mode():
             if self._use_native() and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("FusedAdamW computes bias corrections on the host per step: not graph-capturable "
@@ -516,10 +522,13 @@ class FusedSGD(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        from ..ops.gemm import flush_wgrads
+
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        flush_wgrads()  # weight gradients deferred into a grouped launch (normally flushed by backward's end)
         if self._flat_mode():
             self._flat_step()
             return loss

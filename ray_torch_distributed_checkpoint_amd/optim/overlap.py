@@ -93,6 +93,12 @@ class BackwardOverlap:
         p.grad = v
 
     def _hook(self, p) -> None:
+        from ..ops.gemm import when_grad_ready
+
+        # (a weight gradient deferred into a grouped GEMM launch is final only after its flush)
+        when_grad_ready(p, lambda: self._hook_final(p))
+
+    def _hook_final(self, p) -> None:
         if p in self.updated:
             raise RuntimeError("BackwardOverlap: a second gradient for a parameter already updated this step "
                                "(gradient accumulation over several backward passes needs the plain optimizer "

@@ -49,6 +49,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops.gemm import flush_wgrads, when_grad_ready
 from ..optim.flat import FlatParamSpace
 
 
@@ -320,6 +321,11 @@ class DistributedDataParallel(nn.Module):
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        # a weight gradient deferred into a grouped GEMM launch is written at its flush: the
+        # bucket may only count it (and launch its collective) after that kernel is enqueued
+        when_grad_ready(p, lambda: self._grad_final(p))
+
+    def _grad_final(self, p):
         g = p.grad
         seg_view = None
         if g is not None:
@@ -357,6 +363,7 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._callback_queued = False
+        flush_wgrads()  # deferred weight gradients (and the bucket marks waiting on them) first
         self._steps += 1
         if self._engine is not None:
             if self.p2p is not None and self.p2p.error():
