@@ -130,6 +130,11 @@ def _round_split_rows(rows: int, cols: int, k: int, device) -> int:
 _GROUP_ON = os.environ.get("RTDC_WGRAD_GROUP", "1") != "0"
 _GROUP_MAX = 8        # products per launch (gemm8g_kernel)
 _GROUP_TILES = 200    # flush once the pending products fill ~a round of 256 CUs
+# Grouped launches inside backward go to a side stream, so the next layer's backward kernels
+# can take the CUs a 216-tile group leaves idle (one 8-wave block fills a CU); the compute
+# stream joins it at the end of backward.  -0.17 ms/step on GPT-2-small
+# (profiles/wgrad_group_ab_r3.txt); RTDC_WGRAD_SIDE=0 keeps them on the compute stream.
+_GROUP_SIDE = os.environ.get("RTDC_WGRAD_SIDE", "1") != "0"
 
 
 class _WgradGroup:
@@ -139,6 +144,8 @@ class _WgradGroup:
         self.ptrs = set()    # data_ptr of every pending output
         self.waiters = []    # (callback) in registration order, run after the flush
         self.cb_queued = False
+        self.side = None     # RTDC_WGRAD_SIDE stream
+        self.side_busy = False
 
     def add(self, dy, x2d, out, tiles) -> bool:
         if not self.cb_queued:
@@ -159,25 +166,52 @@ class _WgradGroup:
 
     def _end_of_backward(self):
         self.cb_queued = False
-        self.flush()
+        self.flush(join=True)
 
     def pending(self, t) -> bool:
         return t is not None and bool(self.ptrs) and t.data_ptr() in self.ptrs
 
-    def flush(self):
-        if self.items:
-            items, self.items, self.tiles = self.items, [], 0
-            for i in range(0, len(items), _GROUP_MAX):
-                chunk = items[i:i + _GROUP_MAX]
-                dims = []
-                for dy, x2d, out, _ in chunk:
-                    M, N = dy.shape
-                    K = x2d.shape[1]
-                    dims += [N, K, M, N, K, K]
-                gpu_ext().gemm_bf16_grouped([c[0] for c in chunk], [c[1] for c in chunk], [c[2] for c in chunk],
-                                            dims, False, False)
-            self.ptrs = set()
+    def _launch(self, items):
+        for i in range(0, len(items), _GROUP_MAX):
+            chunk = items[i:i + _GROUP_MAX]
+            dims = []
+            for dy, x2d, out, _ in chunk:
+                M, N = dy.shape
+                K = x2d.shape[1]
+                dims += [N, K, M, N, K, K]
+            gpu_ext().gemm_bf16_grouped([c[0] for c in chunk], [c[1] for c in chunk], [c[2] for c in chunk],
+                                        dims, False, False)
+
+    def flush(self, join: bool = False):
+        """Launch the pending products, then run the callbacks waiting for them.  join=False
+        (a flush inside backward) may leave them running on the side stream; join=True makes
+        the current stream wait for everything launched there."""
+        items, self.items, self.tiles = self.items, [], 0
         waiters, self.waiters = self.waiters, []
+        if (items and _GROUP_SIDE and not join and items[0][0].is_cuda
+                and not torch.cuda.is_current_stream_capturing()):
+            cur = torch.cuda.current_stream(items[0][0].device)
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=items[0][0].device)
+            self.side.wait_stream(cur)  # operands written
+            with torch.cuda.stream(self.side):
+                self._launch(items)
+                for dy, x2d, _, _ in items:  # the compute stream may recycle them before the kernel ran
+                    dy.record_stream(self.side)
+                    x2d.record_stream(self.side)
+                self.ptrs = set()
+                self.side_busy = True
+                # (a DDP bucket / overlapped update triggered by these gradients is ordered
+                # behind the grouped kernel: its events are recorded on this stream)
+                for fn in waiters:
+                    fn()
+            return
+        if items:
+            self._launch(items)
+            self.ptrs = set()
+        if self.side_busy and join:
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+            self.side_busy = False
         for fn in waiters:
             fn()
 
@@ -187,14 +221,22 @@ _WG = _WgradGroup()
 
 def flush_wgrads() -> None:
     """Launch every deferred weight gradient now (and run the gradient-ready callbacks that
-    waited for them)."""
-    _WG.flush()
+    waited for them); the current stream is ordered after all of them."""
+    _WG.flush(join=True)
 
 
 def when_grad_ready(p: torch.Tensor, fn) -> None:
-    """Run fn() once p's gradient is final: now, or right after the flush that writes it."""
+    """Run fn() once p's gradient is final: now, or right after the flush that writes it.
+    While grouped launches run on the side stream (RTDC_WGRAD_SIDE), fn runs with the side
+    stream current, joined to the compute stream first: whatever fn enqueues (a DDP bucket's
+    collective may cover gradients of both streams) is ordered after both."""
     if _WG.pending(p.grad):
         _WG.waiters.append(fn)
+    elif _WG.side_busy:
+        side = _WG.side
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        with torch.cuda.stream(side):
+            fn()
     else:
         fn()
 

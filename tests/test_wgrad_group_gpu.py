@@ -79,9 +79,9 @@ def test_model_backward_grouped_equals_immediate():
     launched = []
     orig = G._WgradGroup.flush
 
-    def spy(self):
+    def spy(self, *a, **k):
         launched.append(len(self.items))
-        return orig(self)
+        return orig(self, *a, **k)
 
     G._WgradGroup.flush = spy
     try:
@@ -119,9 +119,9 @@ def _worker(rank, world, port, q):
         flushed = []
         orig = G._WgradGroup.flush
 
-        def spy(self):
+        def spy(self, *a, **k):
             flushed.append(len(self.items))
-            return orig(self)
+            return orig(self, *a, **k)
 
         G._WgradGroup.flush = spy
         net.space.zero_grad(set_to_none=True)
