@@ -397,6 +397,8 @@ using Cfg128x256 = TileCfg<128, 256, 2, 4>;
 using Cfg256x256 = TileCfg<256, 256, 2, 4>;
 using Cfg256x64 = TileCfg<256, 64, 4, 1>;   // narrow outputs (Cout = 64 convolutions)
 using Cfg64x256 = TileCfg<64, 256, 1, 4>;   // short outputs (Cout = 64 weight gradients)
+using Cfg256x64w8 = TileCfg<256, 64, 8, 1>; // narrow outputs, 8 waves of 32x64 (RTDC_CONV64_W8)
+using Cfg128x128w8 = TileCfg<128, 128, 4, 2>; // 8 waves of 32x64 (RTDC_CONV128_W8)
 
 template <class CFG>
 static inline long long ntiles(const GemmArgs& a) {
@@ -411,6 +413,29 @@ static void launch_cfg(const GemmArgs& a, int batch, hipStream_t st) {
 
 // LDS stages of the implicit-GEMM convolution kernels (RTDC_CONV_NS=2|3|4; see the NS note at
 // gemm_bf16_kernel)
+// The N <= 64 implicit-GEMM convolutions (ResNet stem / layer1) on 256x64 tiles of 8 waves
+// (32x64 each: 97-102 VGPRs, four waves per SIMD with two blocks per CU) instead of 4 waves of
+// 64x64 (169 registers, two waves per SIMD): ResNet-18 8.74 vs 8.88 ms/step
+// (profiles/conv_w8_ab_r3.txt).  RTDC_CONV64_W8=0 restores the 4-wave tiles.
+static bool conv64_w8() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_CONV64_W8");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+// RTDC_CONV128_W8=1: the N > 64 implicit-GEMM convolutions on 128x128 tiles of 8 waves (32x64
+// each) instead of 4 (64x64)
+static bool conv128_w8() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_CONV128_W8");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 static int conv_stages() {
   static int v = -1;
   if (v < 0) {
@@ -637,10 +662,14 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
     if (a.M != a.cv_npix) return 1;
     // stats rows are per BM-row tile: 256 (256x64 tiles) or 128
     if (a.stats_mean) {
-      if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 3>(a, stream);
+      if (a.N <= 64 && conv64_w8()) launch_cfg<Cfg256x64w8, true, true, bf16_t, 3>(a, 1, stream);
+      else if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 3>(a, stream);
+      else if (conv128_w8()) launch_cfg<Cfg128x128w8, true, true, bf16_t, 3>(a, 1, stream);
       else launch_conv<Cfg128x128, true, true, bf16_t, 3>(a, stream);
     } else {
-      if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 1>(a, stream);
+      if (a.N <= 64 && conv64_w8()) launch_cfg<Cfg256x64w8, true, true, bf16_t, 1>(a, 1, stream);
+      else if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 1>(a, stream);
+      else if (conv128_w8()) launch_cfg<Cfg128x128w8, true, true, bf16_t, 1>(a, 1, stream);
       else launch_conv<Cfg128x128, true, true, bf16_t, 1>(a, stream);
     }
   } else if (mode == 2) {
@@ -648,6 +677,7 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
     const bool narrow = a.M <= 64;
     a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a), conv_stages() > 2 ? 256 : 512);
     if (narrow) launch_conv<Cfg64x256, false, false, float, 2>(a, stream);
+    else if (conv128_w8()) launch_cfg<Cfg128x128w8, false, false, float, 2>(a, 1, stream);
     else launch_conv<Cfg128x128, false, false, float, 2>(a, stream);
     if (a.splitk > 1) launch_splitk_reduce<float>(a, stream);
   } else {
