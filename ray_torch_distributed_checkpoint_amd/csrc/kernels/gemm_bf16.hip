@@ -399,6 +399,7 @@ using Cfg256x64 = TileCfg<256, 64, 4, 1>;   // narrow outputs (Cout = 64 convolu
 using Cfg64x256 = TileCfg<64, 256, 1, 4>;   // short outputs (Cout = 64 weight gradients)
 using Cfg256x64w8 = TileCfg<256, 64, 8, 1>; // narrow outputs, 8 waves of 32x64 (RTDC_CONV64_W8)
 using Cfg128x128w8 = TileCfg<128, 128, 4, 2>; // 8 waves of 32x64 (RTDC_CONV128_W8)
+using Cfg64x256w8 = TileCfg<64, 256, 1, 8>;   // 8 waves of 64x32 (RTDC_CONV64WG_W8)
 
 template <class CFG>
 static inline long long ntiles(const GemmArgs& a) {
@@ -425,12 +426,22 @@ static bool conv64_w8() {
   }
   return v == 1;
 }
-// RTDC_CONV128_W8=1: the N > 64 implicit-GEMM convolutions on 128x128 tiles of 8 waves (32x64
-// each) instead of 4 (64x64)
+// The N > 64 implicit-GEMM convolutions (forward, dgrad, weight gradient) on 128x128 tiles of 8
+// waves (32x64 each) instead of 4 (64x64): ResNet-18 8.56 vs 8.71 ms/step
+// (profiles/conv_w8_ab_r3.txt).  RTDC_CONV128_W8=0 restores the 4-wave tiles.
 static bool conv128_w8() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RTDC_CONV128_W8");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+// RTDC_CONV64WG_W8=1: the Cout = 64 weight gradients on 64x256 tiles of 8 waves (64x32 each)
+static bool conv64wg_w8() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_CONV64WG_W8");
     v = (e && e[0] == '1') ? 1 : 0;
   }
   return v == 1;
@@ -676,7 +687,8 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
     if (a.K < a.cv_npix || a.stats_mean) return 1;
     const bool narrow = a.M <= 64;
     a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a), conv_stages() > 2 ? 256 : 512);
-    if (narrow) launch_conv<Cfg64x256, false, false, float, 2>(a, stream);
+    if (narrow && conv64wg_w8()) launch_cfg<Cfg64x256w8, false, false, float, 2>(a, 1, stream);
+    else if (narrow) launch_conv<Cfg64x256, false, false, float, 2>(a, stream);
     else if (conv128_w8()) launch_cfg<Cfg128x128w8, false, false, float, 2>(a, 1, stream);
     else launch_conv<Cfg128x128, false, false, float, 2>(a, stream);
     if (a.splitk > 1) launch_splitk_reduce<float>(a, stream);
