@@ -168,8 +168,8 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
 static void gemm_bf16_grouped(std::vector<Tensor> A, std::vector<Tensor> B, std::vector<Tensor> C,
                               std::vector<int64_t> dims, bool a_kmajor, bool b_kmajor) {
   const size_t n = A.size();
-  TORCH_CHECK(n >= 1 && n <= 8 && B.size() == n && C.size() == n && dims.size() == 6 * n,
-              "gemm_bf16_grouped: 1..8 products, 6 dims each");
+  TORCH_CHECK(n >= 1 && n <= 10 && B.size() == n && C.size() == n && dims.size() == 6 * n,
+              "gemm_bf16_grouped: 1..10 products, 6 dims each");
   std::vector<rtdc::GemmArgs> args(n);
   const bool fp32 = C[0].scalar_type() == at::kFloat;
   for (size_t i = 0; i < n; ++i) {

@@ -485,12 +485,13 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs a) {
 // linears are 9..36 tiles each with K = 16384: alone each one needs split-K slabs + a reduce
 // kernel to fill the chip; two layers' eight products together are 216 full-K tiles, one
 // round, with no slab traffic (ops/gemm.py WgradGroup).
-constexpr int G8_MAX_GROUP = 8;
+constexpr int G8_MAX_GROUP = 10;  // (10 x GemmArgs: the kernel argument stays < 4 KiB)
 struct GemmGroup {
   GemmArgs g[G8_MAX_GROUP];
   int start[G8_MAX_GROUP + 1];
   int n;
 };
+static_assert(sizeof(GemmGroup) <= 4096, "kernel argument segment");
 
 template <bool AK, bool BKM, typename OutT>
 __global__ __launch_bounds__(512, 1) void gemm8g_kernel(GemmGroup gg) {

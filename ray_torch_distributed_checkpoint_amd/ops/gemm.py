@@ -128,8 +128,9 @@ def _round_split_rows(rows: int, cols: int, k: int, device) -> int:
 # backward pass ends (an autograd final callback; DDP's finalize and the fused optimizers flush
 # first too).  RTDC_WGRAD_GROUP=0 launches every weight gradient immediately.
 _GROUP_ON = os.environ.get("RTDC_WGRAD_GROUP", "1") != "0"
-_GROUP_MAX = 8        # products per launch (gemm8g_kernel)
-_GROUP_TILES = 200    # flush once the pending products fill ~a round of 256 CUs
+_GROUP_MAX = 10       # products per launch (gemm8g_kernel G8_MAX_GROUP)
+_GROUP_TILES = 200    # products with fewer output tiles than this are deferred
+_ROUND = 256          # tiles per round (one 8-wave block per CU); groups are packed up to it
 # Grouped launches inside backward go to a side stream, so the next layer's backward kernels
 # can take the CUs a 216-tile group leaves idle (one 8-wave block fills a CU); the compute
 # stream joins it at the end of backward.  -0.17 ms/step on GPT-2-small
@@ -157,16 +158,28 @@ class _WgradGroup:
         # keep an alias, not `out` itself: AccumulateGrad adopts the returned tensor as p.grad
         # without a copy only while nothing else references it (otherwise it clones the still
         # unwritten buffer)
+        # greedy packing into rounds of the chip: launch the pending group first when this
+        # product would not fit the round any more (GPT-2: 252-tile groups of 9 products)
+        if self.items and (self.tiles + tiles > _ROUND or len(self.items) >= _GROUP_MAX):
+            self.flush()
         self.items.append((dy, x2d, out.view(out.shape), tiles))
         self.tiles += tiles
         self.ptrs.add(out.data_ptr())
-        if self.tiles >= _GROUP_TILES or len(self.items) >= _GROUP_MAX:
+        if self.tiles >= _ROUND:
             self.flush()
         return True
 
     def _end_of_backward(self):
         self.cb_queued = False
         self.flush(join=True)
+
+    def _launch_split(self, items):
+        """A remainder far below a round (the last layer's products): each product on its own
+        with split-K slabs, which spreads it over the chip."""
+        for dy, x2d, out, _ in items:
+            M, N = dy.shape
+            K = x2d.shape[1]
+            gemm_bf16(dy, x2d, out, N, K, M, N, K, K, False, False)
 
     def pending(self, t) -> bool:
         return t is not None and bool(self.ptrs) and t.data_ptr() in self.ptrs
@@ -207,7 +220,10 @@ class _WgradGroup:
                     fn()
             return
         if items:
-            self._launch(items)
+            if join and sum(it[3] for it in items) * 2 < _ROUND:
+                self._launch_split(items)
+            else:
+                self._launch(items)
             self.ptrs = set()
         if self.side_busy and join:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)
