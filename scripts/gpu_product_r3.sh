@@ -6,7 +6,7 @@
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
-OUT=gpurun_out/product_r3
+OUT=${OUT:-gpurun_out/product_r3}
 mkdir -p $OUT
 export RTDC_HOME=/tmp/rtdc_home
 STEPS=${STEPS:-200}
