@@ -70,7 +70,7 @@ def main():
         delta = torch.empty((B * H, T), dtype=torch.float32, device="cuda")
         dyc = dy.contiguous()
         t_kf = min(timeit(lambda: ext.flash_fwd(q_, o_, lse, B, T, H, Hkv, Dh, scale), args.reps) for _ in range(3))
-        t_kb = min(timeit(lambda: ext.flash_bwd(q_, o_, dyc, lse, delta, dqkv, B, T, H, Hkv, Dh, scale), args.reps)
+        t_kb = min(timeit(lambda: ext.flash_bwd(q_, o_, dyc, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, None), args.reps)
                    for _ in range(3))
         q = qkv.detach()[..., : H * Dh].view(B, T, H, Dh).transpose(1, 2).contiguous().requires_grad_(True)
         k = qkv.detach()[..., H * Dh:(H + Hkv) * Dh].view(B, T, Hkv, Dh).transpose(1, 2)

@@ -17,7 +17,7 @@ namespace py = pybind11;
 
 extern "C" {
 int rtdc_gemm_bf16(const rtdc::GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
-                   hipStream_t stream);
+                   hipStream_t stream, int* cs_rows_out);
 int rtdc_gemm_f32(const rtdc::GemmF32Args* args, hipStream_t st);
 int rtdc_gemm8_grouped(const rtdc::GemmArgs* args, int n, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 int rtdc_conv_gemm(const rtdc::GemmArgs* args, int mode, hipStream_t stream);
@@ -27,12 +27,15 @@ int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rstd, int M, 
                      hipStream_t st);
 int rtdc_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean, const float* rstd,
                        const void* dres, void* dx, float* ws, float* dg, float* db, float* dxsum, int M, int D,
-                       int nwaves, int accumulate, hipStream_t st);
+                       int nwaves, int accumulate, hipStream_t st, int* nblk_out);
 int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, const float* rstd, const void* dres,
                      void* dx, float* ws, float* dg, float* dxsum, int M, int D, int nwaves, int accumulate,
                      hipStream_t st);
 int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out, int accumulate,
                 int is_bf16, hipStream_t st);
+int rtdc_colsum_partial(const void* X, int M, int N, int ld, float* ws, int nblk, int is_bf16, hipStream_t st);
+int rtdc_colsum_multi(const float* const* ws, float* const* out, const int* W, const int* D, const int* accumulate,
+                      int n, hipStream_t st);
 int rtdc_xent(const void* logits, void* dlogits, const int64_t* target, float* loss, float* lse,
               int64_t* argmax, int M, int V, int ld, float grad_scale, int ignore_index, int is_bf16,
               hipStream_t st);
@@ -43,6 +46,7 @@ int rtdc_sgd(const void* chunks, int nchunks, float* p, const float* g, float* b
              float momentum, float dampening, float wd, int nesterov, int first, float grad_scale,
              hipStream_t st);
 int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st);
+int rtdc_f32_to_bf16_t(const float* x, void* y, int R, int C, hipStream_t st);
 int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float* partial, hipStream_t st);
 int rtdc_softmax_fwd(const void* S, void* P, float* lse, long long rows, int T, int causal, hipStream_t st);
 int rtdc_softmax_bwd(const void* P, const void* dP, void* dS, long long rows, int T, int causal,
@@ -86,6 +90,9 @@ int rtdc_stem_dw_s2d(const float* dwp, float* dw, int Cout, hipStream_t st);
 int rtdc_bn_relu_maxpool(const void* x, void* y, void* arg, const float* mean, const float* rstd, const float* gamma,
                          const float* beta, int B, int H, int W, int C, int Ho, int Wo, int K, int s, int p,
                          hipStream_t st);
+int rtdc_pool_bn_bwd(const void* dy, const void* arg, const void* x, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, void* dx, float* dgamma, float* dbeta, float* ws, int nblk,
+                     int B, int H, int W, int C, int Ho, int Wo, hipStream_t st);
 int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
                 const float* beta, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu,
                 float* ws, int nblk, hipStream_t st);
@@ -93,7 +100,7 @@ int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, in
                  int K, int s, int p, int backward, hipStream_t st);
 int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st);
 int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
-                   int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st);
+                   int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws, hipStream_t st);
 }
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -110,7 +117,9 @@ static void check_dev(const Tensor& t, const char* name) {
 }
 
 // ---------------------------------------------------------------------------------- GEMMs
-static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c10::optional<Tensor> bias,
+// Returns the number of deferred column-sum partial rows left in cs_ws (cs_ws given without
+// cs_out: see rtdc_gemm_bf16), else 0.
+static int64_t gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c10::optional<Tensor> bias,
                       c10::optional<Tensor> aux_in, c10::optional<Tensor> aux_out, int64_t M, int64_t N,
                       int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool a_kmajor, bool b_kmajor,
                       int64_t batch, int64_t batch_inner, int64_t sA0, int64_t sA1, int64_t sB0, int64_t sB1,
@@ -154,12 +163,19 @@ static void gemm_bf16(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> Cin, c
     a.cs_out = cs_out->data_ptr<float>();
     a.cs_ws = cs_ws->data_ptr<float>();
     a.cs_ws_elems = cs_ws->numel();
+  } else if (cs_ws.has_value()) {  // deferred: partial rows only
+    TORCH_CHECK(cs_ws->scalar_type() == at::kFloat && batch == 1, "gemm_bf16: cs_ws needs fp32 scratch, batch 1");
+    a.cs_ws = cs_ws->data_ptr<float>();
+    a.cs_ws_elems = cs_ws->numel();
   }
   TORCH_CHECK(act >= 0 && act <= 6, "gemm_bf16: act 0..6");
   TORCH_CHECK(!(act == 2 || act == 5) || a.aux_out, "gelu forward needs aux_out");
   TORCH_CHECK(!(act == 3 || act == 4 || act == 6) || a.aux_in, "activation backward needs aux_in");
-  check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream()),
+  int cs_rows = 0;
+  check_rc(rtdc_gemm_bf16(&a, a_kmajor, b_kmajor, C.scalar_type() == at::kFloat, (int)batch, cur_stream(),
+                          &cs_rows),
            "gemm_bf16");
+  return cs_rows;
 }
 
 // Independent plain products C_i = A_i . B_i in ONE launch of the 8-wave kernel (gemm_8ph.hip
@@ -248,18 +264,22 @@ static void rmsnorm_fwd(Tensor x, Tensor g, Tensor y, Tensor rstd, double eps) {
            "rmsnorm_fwd");
 }
 // dxsum (optional, fp32 [D]): column sums of dx, produced by the same kernel
-static void layernorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
-                          Tensor dx, Tensor ws, Tensor dg, Tensor db, c10::optional<Tensor> dxsum, int64_t nwaves,
-                          bool accumulate) {
+// defer=true: only the partial rows [nz][nblk][D] are written to ws (nz = 2 + has dxsum: dgamma,
+// dbeta, colsum(dx)); returns nblk, and the caller reduces them later (colsum_multi).  Else 0.
+static int64_t layernorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, c10::optional<Tensor> dres,
+                             Tensor dx, Tensor ws, Tensor dg, Tensor db, c10::optional<Tensor> dxsum, int64_t nwaves,
+                             bool accumulate, bool defer) {
   const int D = (int)x.size(-1), M = (int)(x.numel() / D);
   const int nz = 2 + (dxsum.has_value() ? 1 : 0);
   TORCH_CHECK(ws.numel() >= nz * (nwaves / 4 + 64) * D, "layernorm_bwd workspace too small");
   if (dxsum.has_value()) TORCH_CHECK(dxsum->numel() >= D && dxsum->scalar_type() == at::kFloat, "dxsum: fp32 [D]");
+  int nblk = 0;
   check_rc(rtdc_layernorm_bwd(dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr<float>(),
                               rstd.data_ptr<float>(), ptr_or_null(dres), dx.data_ptr(), ws.data_ptr<float>(),
                               dg.data_ptr<float>(), db.data_ptr<float>(), (float*)ptr_or_null(dxsum), M, D,
-                              (int)nwaves, accumulate, cur_stream()),
+                              (int)nwaves, accumulate, cur_stream(), defer ? &nblk : nullptr),
            "layernorm_bwd");
+  return defer ? nblk : 0;
 }
 static void rmsnorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor rstd, c10::optional<Tensor> dres, Tensor dx,
                         Tensor ws, Tensor dg, c10::optional<Tensor> dxsum, int64_t nwaves, bool accumulate) {
@@ -271,6 +291,36 @@ static void rmsnorm_bwd(Tensor dy, Tensor x, Tensor g, Tensor rstd, c10::optiona
                             dx.data_ptr(), ws.data_ptr<float>(), dg.data_ptr<float>(), (float*)ptr_or_null(dxsum), M,
                             D, (int)nwaves, accumulate, cur_stream()),
            "rmsnorm_bwd");
+}
+static void colsum_partial(Tensor X, int64_t M, int64_t N, int64_t ld, Tensor ws, int64_t nblk) {
+  TORCH_CHECK(ws.numel() >= nblk * N && ws.scalar_type() == at::kFloat, "colsum_partial workspace too small");
+  check_rc(rtdc_colsum_partial(X.data_ptr(), (int)M, (int)N, (int)ld, ws.data_ptr<float>(), (int)nblk,
+                               X.scalar_type() == at::kBFloat16, cur_stream()),
+           "colsum_partial");
+}
+// n <= 32 deferred reductions out_j (+)= sum of the W_j partial rows ws_j [W_j][D_j], one launch
+static void colsum_multi(std::vector<Tensor> ws, std::vector<Tensor> out, std::vector<int64_t> W,
+                         std::vector<int64_t> D, std::vector<int64_t> accumulate) {
+  const size_t n = ws.size();
+  TORCH_CHECK(n >= 1 && n <= 32 && out.size() == n && W.size() == n && D.size() == n && accumulate.size() == n,
+              "colsum_multi: 1..32 jobs");
+  std::vector<const float*> wp(n);
+  std::vector<float*> op(n);
+  std::vector<int> wi(n), di(n), ai(n);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(ws[i].is_cuda() && ws[i].scalar_type() == at::kFloat && ws[i].numel() >= W[i] * D[i],
+                "colsum_multi: fp32 ws [W][D]");
+    TORCH_CHECK(out[i].is_cuda() && out[i].scalar_type() == at::kFloat && out[i].numel() >= D[i] &&
+                    out[i].is_contiguous(),
+                "colsum_multi: fp32 out [D]");
+    wp[i] = ws[i].data_ptr<float>();
+    op[i] = out[i].data_ptr<float>();
+    wi[i] = (int)W[i];
+    di[i] = (int)D[i];
+    ai[i] = accumulate[i] ? 1 : 0;
+  }
+  check_rc(rtdc_colsum_multi(wp.data(), op.data(), wi.data(), di.data(), ai.data(), (int)n, cur_stream()),
+           "colsum_multi");
 }
 static void colsum(Tensor X, int64_t M, int64_t N, int64_t ld, Tensor ws, int64_t nblk, Tensor out,
                    bool accumulate) {
@@ -335,6 +385,15 @@ static void sgd(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, c10::optiona
 }
 static void f32_to_bf16(Tensor x, Tensor y) {
   check_rc(rtdc_f32_to_bf16(x.data_ptr<float>(), y.data_ptr(), (long long)x.numel(), cur_stream()), "f32_to_bf16");
+}
+static void f32_to_bf16_t(Tensor x, Tensor y) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.scalar_type() == at::kFloat && x.is_contiguous(),
+              "f32_to_bf16_t: contiguous fp32 [R, C]");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 2 &&
+                  y.size(0) == x.size(1) && y.size(1) == x.size(0),
+              "f32_to_bf16_t: contiguous bf16 [C, R]");
+  check_rc(rtdc_f32_to_bf16_t(x.data_ptr<float>(), y.data_ptr(), (int)x.size(0), (int)x.size(1), cur_stream()),
+           "f32_to_bf16_t");
 }
 static void sumsq(Tensor chunks, int64_t nchunks, Tensor g, Tensor partial) {
   check_chunks(chunks, nchunks, "sumsq");
@@ -418,12 +477,17 @@ static void flash_fwd(Tensor qkv, Tensor out, Tensor lse, int64_t B, int64_t T, 
                           (int)Dh, (float)scale, cur_stream()),
            "flash_fwd");
 }
+// cs_ws (optional fp32 [B*T/16][W], W = (H + 2 Hkv) Dh): per 16-row group column sums of dqkv
 static void flash_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, Tensor dqkv, int64_t B, int64_t T,
-                      int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+                      int64_t H, int64_t Hkv, int64_t Dh, double scale, c10::optional<Tensor> cs_ws) {
   TORCH_CHECK(dout.is_contiguous() && dqkv.is_contiguous(), "flash_bwd: contiguous tensors expected");
+  if (cs_ws.has_value())
+    TORCH_CHECK(cs_ws->is_cuda() && cs_ws->scalar_type() == at::kFloat && cs_ws->is_contiguous() &&
+                    cs_ws->numel() >= B * T / 16 * (H + 2 * Hkv) * Dh,
+                "flash_bwd: cs_ws fp32 [B*T/16][W]");
   check_rc(rtdc_flash_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                           delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)T, (int)H, (int)Hkv, (int)Dh,
-                          (float)scale, cur_stream()),
+                          (float)scale, cs_ws.has_value() ? cs_ws->data_ptr<float>() : nullptr, cur_stream()),
            "flash_bwd");
 }
 
@@ -686,6 +750,26 @@ static void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t K, int64_t s, in
                         cur_stream()),
            "maxpool_fwd");
 }
+// ResNet stem: maxpool3s2(relu(BN(x))) backward in two gather passes; False = shape unsupported
+static bool pool_bn_bwd(Tensor dy, Tensor arg, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, Tensor dx,
+                        Tensor dgamma, Tensor dbeta, Tensor ws, int64_t nblk) {
+  TORCH_CHECK(dy.is_contiguous() && arg.is_contiguous() && x.is_contiguous() && dx.is_contiguous() && x.dim() == 4 &&
+                  dy.dim() == 4,
+              "pool_bn_bwd: contiguous NHWC tensors expected");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && arg.scalar_type() == at::kByte &&
+                  gamma.scalar_type() == at::kFloat && beta.scalar_type() == at::kFloat,
+              "pool_bn_bwd: bf16 activations, uint8 argmax, fp32 parameters");
+  const int C = (int)x.size(3);
+  TORCH_CHECK(ws.numel() >= 2 * nblk * C && dgamma.numel() >= C && dbeta.numel() >= C, "pool_bn_bwd: buffers too small");
+  const int rc = rtdc_pool_bn_bwd(dy.data_ptr(), arg.data_ptr(), x.data_ptr(), mean.data_ptr<float>(),
+                                  rstd.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(), dx.data_ptr(),
+                                  dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ws.data_ptr<float>(), (int)nblk,
+                                  (int)x.size(0), (int)x.size(1), (int)x.size(2), C, (int)dy.size(1), (int)dy.size(2),
+                                  cur_stream());
+  if (rc == 1) return false;
+  check_rc(rc, "pool_bn_bwd");
+  return true;
+}
 static void maxpool_bwd(Tensor dy, Tensor arg, Tensor dx, int64_t K, int64_t s, int64_t p) {
   TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous(), "maxpool_bwd: contiguous tensors expected");
   check_rc(rtdc_maxpool(nullptr, nullptr, arg.data_ptr(), dy.data_ptr(), dx.data_ptr(), (int)dx.size(0),
@@ -812,11 +896,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("colsum_partial", &colsum_partial);
+  m.def("colsum_multi", &colsum_multi);
   m.def("colsum", &colsum);
   m.def("xent", &xent);
   m.def("adamw", &adamw);
   m.def("sgd", &sgd);
   m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("f32_to_bf16_t", &f32_to_bf16_t);
   m.def("sumsq", &sumsq);
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
@@ -849,6 +936,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nchw_to_nhwc_bf16", &nchw_to_nhwc_bf16);
   m.def("copy2d", &copy2d);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("pool_bn_bwd", &pool_bn_bwd);
   m.def("avgpool", &avgpool);
 
   m.def("grad_status", &grad_status, "per-parameter gradient placement: 0 none, 1 flat slice, 2 elsewhere");

@@ -59,7 +59,25 @@ struct Args {
   int xcd_remap;  // 1: the blocks of one head share an XCD (and its L2); 2: + heavy blocks first
                   // across all the XCD's heads
   int diag;       // timing-only builds (wrong results): bit 1 skips the loop's DMA waits
+  // optional [B*T/16][W] fp32: per 16-row group, the column sums of the bf16 dQ / dK / dV rows
+  // the backward kernels store (the qkv projection's bias gradient, reduced later without
+  // re-reading dqkv: ops/gemm.py offer_colsum_partials)
+  float* cs_ws;
 };
+
+// column sums over a wave's 16 rows of its stored fragment values v (lane = row (lane & 15) x
+// 4 columns 4g..4g+3 of each 16-column block d): one partial row per 16-row group
+template <int DT>
+__device__ __forceinline__ void wave_colsum16(const f32x4 (&v)[DT], float mul, float* dst, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    float s[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[r] = row16_sum(bf2f(f2bf(v[d][r] * mul)));
+    if ((lane & 15) == 0) *(f32x4*)(dst + 16 * d + 4 * g) = f32x4{s[0], s[1], s[2], s[3]};
+  }
+}
 
 // (block-in-head, head) of this workgroup
 __device__ __forceinline__ void grid_pos(const Args& a, int& x, int& y) {
@@ -654,6 +672,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
         make_uint2(pack_bf2(dk[d][0] * a.scale, dk[d][1] * a.scale), pack_bf2(dk[d][2] * a.scale, dk[d][3] * a.scale));
     *(uint2*)(krow + vcol + 16 * d + 4 * g) = make_uint2(pack_bf2(dv[d][0], dv[d][1]), pack_bf2(dv[d][2], dv[d][3]));
   }
+  if (a.cs_ws) {
+    float* crow = a.cs_ws + (((long long)b * a.T + k0w) >> 4) * W;
+    wave_colsum16<DT>(dk, a.scale, crow + kcol, lane);
+    wave_colsum16<DT>(dv, 1.f, crow + vcol, lane);
+  }
 }
 
 // ------------------------------------------------------------------------------ dQ
@@ -782,6 +805,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
   for (int d = 0; d < DT; ++d)
     *(uint2*)(qrow + 16 * d + 4 * g) =
         make_uint2(pack_bf2(dq[d][0] * a.scale, dq[d][1] * a.scale), pack_bf2(dq[d][2] * a.scale, dq[d][3] * a.scale));
+  if (a.cs_ws)
+    wave_colsum16<DT>(dq, a.scale, a.cs_ws + (((long long)b * a.T + qb * BQ + wave * 16) >> 4) * W + qcol, lane);
 }
 
 }  // namespace fa
@@ -846,13 +871,15 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
 }
 
 extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
-                              void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, hipStream_t st) {
+                              void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws,
+                              hipStream_t st) {
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
   // dQ first: it also computes the row terms delta = rowsum(dO * O) that dK/dV read
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.dout = (const bf16_t*)dout; a.lse = (float*)lse;
   a.delta = delta;
   a.dqkv = (bf16_t*)dqkv;
+  a.cs_ws = cs_ws;
   a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd(); a.diag = fa_diag();
   dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H);
   const int ns = fa_ns(Dh);

@@ -729,6 +729,152 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
   }
 }
 
+// ResNet stem backward, maxpool(relu(BN(x))) with the pool's input gradient never stored:
+// pass 1 gathers g = maxpool'(dy) at every BN-output position (rounded to bf16 exactly as
+// maxpool3s2_bwd_kernel stores it), masks it by the ReLU recomputed from x and reduces
+// (sum g, sum g * xhat) per channel into per-block partial rows (bn_reduce_kernel's mode 1
+// format, merged by bn_bwd_finalize_kernel); pass 2 gathers g again and writes
+// dx = A g + B x + D (bn_bwd_apply_kernel<2>'s arithmetic).  Against maxpool backward + BN
+// reduce + BN apply this drops the full-resolution gradient's write and its two re-reads
+// (3 x B*H*W*C bf16).  A thread keeps one 8-channel group (grid stride % (C/8) == 0).
+template <int C>
+__device__ __forceinline__ void pool3s2_gather(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, int b,
+                                               int h, int w, int c, int Ho, int Wo, float* g) {
+  int hos[2], khs[2], nh = 0, wos[2], kws[2], nw = 0;
+  if (h & 1) {
+    if ((h + 1) / 2 < Ho) { hos[nh] = (h + 1) / 2; khs[nh++] = 0; }
+    hos[nh] = (h - 1) / 2; khs[nh++] = 2;
+  } else {
+    if (h / 2 < Ho) { hos[nh] = h / 2; khs[nh++] = 1; }
+  }
+  if (w & 1) {
+    if ((w + 1) / 2 < Wo) { wos[nw] = (w + 1) / 2; kws[nw++] = 0; }
+    wos[nw] = (w - 1) / 2; kws[nw++] = 2;
+  } else {
+    if (w / 2 < Wo) { wos[nw] = w / 2; kws[nw++] = 1; }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = 0.f;
+  for (int a = 0; a < nh; ++a)
+    for (int bb = 0; bb < nw; ++bb) {
+      const size_t o = ((size_t)(b * Ho + hos[a]) * Wo + wos[bb]) * C + c;
+      const uint2 a8 = *(const uint2*)(arg + o);
+      const uint4 g4 = *(const uint4*)(dy + o);
+      const uint32_t tap = khs[a] * 3 + kws[bb];
+      const uint32_t gw[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t ae = ((e < 4 ? a8.x : a8.y) >> (8 * (e & 3))) & 0xffu;
+        const float v = __uint_as_float((e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] << 16));
+        if (ae == tap) g[e] += v;
+      }
+    }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = bf2f(f2bf(g[e]));  // the stored bf16 gradient
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void pool_bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
+                                                                const uint8_t* __restrict__ arg,
+                                                                const bf16_t* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, int B, int H, int W,
+                                                                int Ho, int Wo, float* __restrict__ out0,
+                                                                float* __restrict__ out1) {
+  constexpr int CG = C / 8;
+  __shared__ float red[2][256][8];
+  const int total = B * H * W * CG;
+  const int i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  const int c = (i0 % CG) * 8;
+  float ka[8], kb[8], m8[8], r8[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    m8[e] = mean[c + e];
+    r8[e] = rstd[c + e];
+    ka[e] = r8[e] * gamma[c + e];
+    kb[e] = beta[c + e] - m8[e] * ka[e];
+    s1[e] = s2[e] = 0.f;
+  }
+  for (int i = i0; i < total; i += stride) {
+    const int pix = i / CG;
+    const int q = pix / W, w = pix - q * W;
+    const int b = q / H, h = q - b * H;
+    float g[8], xv[8];
+    unpack8(*(const uint4*)(x + (size_t)pix * C + c), xv);
+    pool3s2_gather<C>(dy, arg, b, h, w, c, Ho, Wo, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gm = fmaf(xv[e], ka[e], kb[e]) > 0.f ? g[e] : 0.f;
+      s1[e] += gm;
+      s2[e] += gm * (xv[e] - m8[e]) * r8[e];
+    }
+  }
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][t][e] = s1[e];
+    red[1][t][e] = s2[e];
+  }
+  __syncthreads();
+  if (t < CG) {  // threads t, t + CG, t + 2 CG, ... of this block share channel group t (fixed order)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float A = 0.f, Bq = 0.f;
+      for (int l = t; l < 256; l += CG) {
+        A += red[0][l][e];
+        Bq += red[1][l][e];
+      }
+      out0[(long long)blockIdx.x * C + t * 8 + e] = A;
+      out1[(long long)blockIdx.x * C + t * 8 + e] = Bq;
+    }
+  }
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ arg,
+                                                               const bf16_t* __restrict__ x,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               const float* __restrict__ dbeta,
+                                                               const float* __restrict__ dgamma,
+                                                               bf16_t* __restrict__ dx, int B, int H, int W, int Ho,
+                                                               int Wo) {
+  constexpr int CG = C / 8;
+  const int total = B * H * W * CG;
+  const float invN = 1.f / ((float)B * H * W);
+  const int i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  const int c = (i0 % CG) * 8;
+  float kA[8], kB[8], kD[8], ka[8], kb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float r = rstd[c + e], gr = gamma[c + e] * r;
+    kA[e] = gr;
+    kB[e] = -gr * r * dgamma[c + e] * invN;
+    kD[e] = -gr * dbeta[c + e] * invN - kB[e] * mean[c + e];
+    ka[e] = rstd[c + e] * gamma[c + e];
+    kb[e] = beta[c + e] - mean[c + e] * ka[e];
+  }
+  for (int i = i0; i < total; i += stride) {
+    const int pix = i / CG;
+    const int q = pix / W, w = pix - q * W;
+    const int b = q / H, h = q - b * H;
+    float g[8], xv[8], o[8];
+    unpack8(*(const uint4*)(x + (size_t)pix * C + c), xv);
+    pool3s2_gather<C>(dy, arg, b, h, w, c, Ho, Wo, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gm = fmaf(xv[e], ka[e], kb[e]) > 0.f ? g[e] : 0.f;
+      o[e] = fmaf(kA[e], gm, fmaf(kB[e], xv[e], kD[e]));
+    }
+    *(uint4*)(dx + (size_t)pix * C + c) = pack8(o);
+  }
+}
+
 // Network input NCHW fp32 -> NHWC bf16 in one pass (the permute + cast + contiguous of ATen
 // are three): a thread takes 8 consecutive pixels of one image - 2 x 16-B loads per channel,
 // C x 16-B stores of the interleaved row (HW % 8 == 0).
@@ -978,6 +1124,25 @@ extern "C" int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, v
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(gsz((long long)B * H * W * C / 8)), dim3(256), 0, st, (const bf16_t*)dy,
                        (const uint8_t*)arg, (bf16_t*)dx, B, H, W, C, Ho, Wo, K, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Stem backward of maxpool3s2(relu(BN(x))) (pool_bn_bwd_*_kernel): dy [B][Ho][Wo][C] + argmax ->
+// dx [B][H][W][C], dgamma, dbeta.  ws: 2 * nblk * C floats.  Returns 1 for an unsupported shape.
+extern "C" int rtdc_pool_bn_bwd(const void* dy, const void* arg, const void* x, const float* mean, const float* rstd,
+                                const float* gamma, const float* beta, void* dx, float* dgamma, float* dbeta, float* ws,
+                                int nblk, int B, int H, int W, int C, int Ho, int Wo, hipStream_t st) {
+  if (C != 64 || Ho != (H - 1) / 2 + 1 || Wo != (W - 1) / 2 + 1 || (long long)B * H * W * C >= (1LL << 31) ||
+      nblk < 1)
+    return 1;
+  hipLaunchKernelGGL(pool_bn_bwd_reduce_kernel<64>, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const uint8_t*)arg, (const bf16_t*)x, mean, rstd, gamma, beta, B, H, W, Ho, Wo, ws,
+                     ws + (long long)nblk * C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
+                     (const float*)(ws + (long long)nblk * C), nblk, C, dbeta, dgamma);
+  hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<64>, dim3(gsz((long long)B * H * W * C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, mean, rstd, gamma, beta,
+                     (const float*)dbeta, (const float*)dgamma, (bf16_t*)dx, B, H, W, Ho, Wo);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -586,8 +586,12 @@ static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, doub
   return best;
 }
 
+// cs_rows_out (optional): with cs_ws set and cs_out null the column sums are DEFERRED - the
+// 8-wave gelu-backward epilogue leaves its partial rows in cs_ws, *cs_rows_out = their count
+// (0: this kernel choice wrote none; the caller reduces C itself).
 extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int batch,
-                              hipStream_t stream) {
+                              hipStream_t stream, int* cs_rows_out) {
+  if (cs_rows_out) *cs_rows_out = 0;
   GemmArgs a = *args;
   if (a.K % gemm::BK != 0 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
   int cfg = pick_cfg(a, batch, a_kmajor, b_kmajor);
@@ -636,6 +640,10 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   if (a.splitk > 1) {
     if (out_fp32) launch_splitk_reduce<float>(a, stream);
     else launch_splitk_reduce<bf16_t>(a, stream);
+  }
+  if (!a.cs_out && a.cs_ws && cs_rows_out && big && (a.act == 3 || a.act == 6) && !out_fp32 && a.splitk == 1) {
+    const int W = ((a.M + 255) / 256) * (bn == 256 ? 2 : 4);
+    if ((long long)W * a.N <= a.cs_ws_elems) *cs_rows_out = W;
   }
   if (a.cs_out) {
     // column sums of C: the 8-wave gelu-backward epilogue left one partial row per (row tile,

@@ -439,6 +439,58 @@ __global__ __launch_bounds__(1024) void colsum_wide_kernel(const float* __restri
   }
 }
 
+// Deferred column-sum reductions of one backward window in ONE launch (ops/gemm.py: the bias /
+// LayerNorm-parameter gradients of two layers flushed with their grouped weight gradients):
+// job j = ws_j [W_j][D_j] partial rows -> out_j [D_j]; block b works on 64 columns of the job
+// whose block range holds b.  Per job the body, and so the summation order, is
+// colsum_wide_kernel's: the result is bitwise the non-deferred one.
+constexpr int kMultiJobs = 32;
+struct ColsumJobs {
+  const float* ws[kMultiJobs];
+  float* out[kMultiJobs];
+  int W[kMultiJobs];
+  int D[kMultiJobs];
+  int start[kMultiJobs + 1];
+  int accumulate;  // bit j: out_j += sum
+  int n;
+};
+static_assert(sizeof(ColsumJobs) <= 4096, "kernel argument segment");
+
+__global__ __launch_bounds__(1024) void colsum_multi_kernel(ColsumJobs jobs) {
+  __shared__ float part[16][64];
+  const int b = blockIdx.x;
+  int j = 0;
+#pragma unroll
+  for (int i = 1; i < kMultiJobs; ++i) j += (i < jobs.n && b >= jobs.start[i]) ? 1 : 0;
+  j = __builtin_amdgcn_readfirstlane(j);
+  const float* __restrict__ ws = jobs.ws[j];
+  const int W = jobs.W[j], D = jobs.D[j];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int d = (b - jobs.start[j]) * 64 + lane;
+  float acc = 0.f;
+  if (d < D) {
+    for (int w0 = wv; w0 < W; w0 += 16 * kWideU) {
+      float v[kWideU];
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) {
+        const int w = w0 + 16 * u;
+        v[u] = w < W ? ws[(long long)w * D + d] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) acc += v[u];
+    }
+  }
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && d < D) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += part[i][lane];
+    float* o = jobs.out[j] + d;
+    *o = ((jobs.accumulate >> j) & 1) ? *o + t : t;
+  }
+}
+
 static bool colsum_wide_enabled() {
   static int v = -1;  // RTDC_COLSUM_WIDE=0: the two-launch form (A/B)
   if (v < 0) {
@@ -588,7 +640,8 @@ static int resident_blocks4(size_t lds, int cpl4) {
 template <bool RMS>
 static int launch_norm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                            const float* rstd, const void* dres, void* dx, float* ws, float* dg,
-                           float* db, float* dxsum, int M, int D, int nwaves, int accumulate, hipStream_t st) {
+                           float* db, float* dxsum, int M, int D, int nwaves, int accumulate, hipStream_t st,
+                           int* nblk_out = nullptr) {
   if (D % 8 != 0 || nwaves % 4 != 0) return 1;
   const int cpl = (D / 8 + 63) / 64;
   const bool cs = dxsum != nullptr;
@@ -639,6 +692,10 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
 #undef LC
 #undef L
 #undef L4
+  if (nblk_out) {  // deferred: the caller reduces the [nz][nblk][D] partials (rtdc_colsum_multi)
+    *nblk_out = nblk;
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   // one reduction launch pair for all of them; the colsum of dx is never accumulated, so it
   // gets its own pair when dgamma/dbeta accumulate
   if (!cs || !accumulate) {
@@ -662,9 +719,9 @@ extern "C" int rtdc_rmsnorm_fwd(const void* x, const void* g, void* y, float* rs
 extern "C" int rtdc_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                                   const float* rstd, const void* dres, void* dx, float* ws,
                                   float* dg, float* db, float* dxsum, int M, int D, int nwaves,
-                                  int accumulate, hipStream_t st) {
+                                  int accumulate, hipStream_t st, int* nblk_out) {
   return launch_norm_bwd<false>(dy, x, g, mean, rstd, dres, dx, ws, dg, db, dxsum, M, D, nwaves,
-                                accumulate, st);
+                                accumulate, st, nblk_out);
 }
 extern "C" int rtdc_rmsnorm_bwd(const void* dy, const void* x, const void* g, const float* rstd,
                                 const void* dres, void* dx, float* ws, float* dg, float* dxsum, int M,
@@ -678,6 +735,44 @@ extern "C" int rtdc_colsum_rows(const float* ws, int W, int D, float* tmp, float
   colsum_ws_reduce(ws, W, D, tmp, outs1(out), accumulate, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+// n <= 32 deferred reductions (see colsum_multi_kernel); every W_j <= kWideMaxRows
+extern "C" int rtdc_colsum_multi(const float* const* ws, float* const* out, const int* W, const int* D,
+                                 const int* accumulate, int n, hipStream_t st) {
+  if (n < 1 || n > kMultiJobs) return 1;
+  ColsumJobs jobs{};
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (W[i] < 1 || W[i] > kWideMaxRows || D[i] < 1) return 1;
+    jobs.ws[i] = ws[i];
+    jobs.out[i] = out[i];
+    jobs.W[i] = W[i];
+    jobs.D[i] = D[i];
+    jobs.start[i] = blocks;
+    if (accumulate[i]) jobs.accumulate |= 1 << i;
+    blocks += (D[i] + 63) / 64;
+  }
+  jobs.start[n] = blocks;
+  jobs.n = n;
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3((unsigned)blocks), dim3(1024), 0, st, jobs);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// stage 1 only (the partial rows ws [nblk][N]); the reduction is deferred to rtdc_colsum_multi
+extern "C" int rtdc_colsum_partial(const void* X, int M, int N, int ld, float* ws, int nblk, int is_bf16,
+                                   hipStream_t st) {
+  const bool vec = N % 8 == 0 && ld % 8 == 0;
+  const int rpb = (M + nblk - 1) / nblk;
+  dim3 grid(nblk, (N + 511) / 512), block(256);
+#define CS(T, V) hipLaunchKernelGGL((colsum_partial_kernel<T, V>), grid, block, 0, st, (const T*)X, M, N, ld, rpb, ws)
+  if (is_bf16) {
+    if (vec) CS(bf16_t, true); else CS(bf16_t, false);
+  } else {
+    if (vec) CS(float, true); else CS(float, false);
+  }
+#undef CS
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 extern "C" int rtdc_colsum(const void* X, int M, int N, int ld, float* ws, int nblk, float* out,
                            int accumulate, int is_bf16, hipStream_t st) {
   // ws: [nblk][N] partials followed by [64][N] level-2 rows

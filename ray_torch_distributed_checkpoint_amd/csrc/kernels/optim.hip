@@ -135,6 +135,46 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restric
   }
 }
 
+// y[c][r] = bf16(x[r][c]) for a row-major fp32 [R][C] matrix: the K-major image of a weight for
+// the products that read it transposed (ops/shadow.py shadow_t_of).  64x64 tiles through LDS
+// (padded rows: conflict-free column reads), 16-B loads, 8-B stores.
+__global__ __launch_bounds__(256) void f32_to_bf16_t_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                           int R, int C) {
+  __shared__ float t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = ty + 16 * i, r = r0 + rr, c = c0 + 4 * tx;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < R) {
+      if (c + 4 <= C && (C & 3) == 0) {
+        const f32x4 q = *(const f32x4*)(x + (long long)r * C + c);
+        v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = c + e < C ? x[(long long)r * C + c + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[rr][4 * tx + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cc = ty + 16 * i, c = c0 + cc, r = r0 + 4 * tx;
+    if (c >= C) continue;
+    bf16_t* o = y + (long long)c * R + r;
+    if (r + 4 <= R && (R & 3) == 0) {
+      *(uint2*)o = make_uint2(pack_bf2(t[4 * tx][cc], t[4 * tx + 1][cc]), pack_bf2(t[4 * tx + 2][cc], t[4 * tx + 3][cc]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (r + e < R) o[e] = f2bf(t[4 * tx + e][cc]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void bf16_to_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
                                                          long long n, float scale) {
   for (long long i = (blockIdx.x * 256LL + threadIdx.x) * 4; i < n; i += gridDim.x * 256LL * 4) {
@@ -198,6 +238,13 @@ extern "C" int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, (bf16_t*)y, n);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_f32_to_bf16_t(const float* x, void* y, int R, int C, hipStream_t st) {
+  if (R <= 0 || C <= 0) return 0;
+  hipLaunchKernelGGL(f32_to_bf16_t_kernel, dim3((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64)), dim3(256), 0,
+                     st, x, (bf16_t*)y, R, C);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -129,7 +129,13 @@ class _FlashAttention(torch.autograd.Function):
         B, T, H, Hkv, Dh, scale = ctx.dims
         dqkv = torch.empty_like(qkv)
         delta = torch.empty((B * H, T), dtype=torch.float32, device=qkv.device)
-        gpu_ext().flash_bwd(qkv, out, dout.contiguous(), lse, delta, dqkv, B, T, H, Hkv, Dh, scale)
+        # the column sums of dqkv (the qkv projection's bias gradient) as per-16-row partials
+        # written by the kernels on the way out, offered to that projection's colsum()
+        Wd = qkv.shape[-1]
+        cs = torch.empty((B * T // 16, Wd), dtype=torch.float32, device=qkv.device) if G.partials_wanted() else None
+        gpu_ext().flash_bwd(qkv, out, dout.contiguous(), lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs)
+        if cs is not None:
+            G.offer_colsum_partials(dqkv, cs)
         return dqkv, None, None, None, None, None
 
 

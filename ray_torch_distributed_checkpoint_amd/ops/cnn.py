@@ -459,6 +459,12 @@ def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, trainin
                             num_batches_tracked, residual_grad_to)
 
 
+# stem backward without the full-resolution pool gradient (RTDC_POOL_BN_FUSED=0: maxpool backward
+# + BatchNorm reduce + apply); partial rows of the statistics pass
+_POOL_BN_FUSED = os.environ.get("RTDC_POOL_BN_FUSED", "1") != "0"
+_POOL_BN_BLOCKS = 1024
+
+
 class _BNReluMaxPool(torch.autograd.Function):
     """maxpool(relu(BN(x))) for the ResNet stem without storing the full-resolution BN output:
     bn_fwd computes the statistics only, one kernel normalises + rectifies + pools; the
@@ -501,8 +507,6 @@ class _BNReluMaxPool(torch.autograd.Function):
         k, s, p = ctx.pool
         C = x.shape[-1]
         N = x.numel() // C
-        dz = torch.empty_like(x)  # gradient at the (never stored) BN output
-        gpu_ext().maxpool_bwd(dy.contiguous(), arg, dz, k, s, p)
         dx = torch.empty_like(x)
         w, b = ctx.params
         dgamma, dbeta = grad_target(w), grad_target(b)
@@ -510,6 +514,15 @@ class _BNReluMaxPool(torch.autograd.Function):
             dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
         if dbeta is None:
             dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        dy = dy.contiguous()
+        if (k, s, p) == (3, 2, 1) and _POOL_BN_FUSED and b is not None and b.dtype == torch.float32:
+            # the pool's input gradient is gathered twice (statistics pass, apply pass) and never
+            # stored (cnn.hip pool_bn_bwd_*_kernel)
+            ws = G.workspace(x.device, 2 * _POOL_BN_BLOCKS * C, "bn")
+            if gpu_ext().pool_bn_bwd(dy, arg, x, mean, rstd, weight, b, dx, dgamma, dbeta, ws, _POOL_BN_BLOCKS):
+                return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        dz = torch.empty_like(x)  # gradient at the (never stored) BN output
+        gpu_ext().maxpool_bwd(dy, arg, dz, k, s, p)
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
         gpu_ext().bn_bwd(dz, x, x, mean, rstd, weight, b, dx, None, dgamma, dbeta, 2, ws, nblk)
@@ -595,6 +608,15 @@ class _Classifier(torch.autograd.Function):
         N = w.shape[0]
         Np, Mp = _ceil(N, 64), _ceil(Bn, 64)
         ws = shadow_of(w)
+        if N % 8 == 0 and Mp == Bn and K % 64 == 0:
+            # N is an output axis of the forward and of the weight gradient: no padding; only
+            # the input-gradient GEMM reduces over N (padded in backward)
+            xc = x.contiguous()
+            y = G.linear_fwd(xc, ws, bias=b)
+            ctx.save_for_backward(xc, ws)
+            ctx.meta = (Bn, N, Np, Mp, True)
+            ctx.params = (w, b)
+            return y
         # padded operands live in persistent zero buffers: one DMA copy of the live rows each
         wp, bp = ws, b
         if Np != N:
@@ -609,7 +631,7 @@ class _Classifier(torch.autograd.Function):
             _copy_rows(xp, x.contiguous(), Bn, K)
         y = G.linear_fwd(xp, wp, bias=bp)
         ctx.save_for_backward(xp, wp)
-        ctx.meta = (Bn, N, Np, Mp)
+        ctx.meta = (Bn, N, Np, Mp, False)
         ctx.params = (w, b)
         if Np == N and Mp == Bn:
             return y
@@ -620,13 +642,29 @@ class _Classifier(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xp, wp = ctx.saved_tensors
-        Bn, N, Np, Mp = ctx.meta
+        Bn, N, Np, Mp, direct = ctx.meta
         dy = dy.contiguous()
+        w, b = ctx.params
+        if direct:
+            dx = dw = db = None
+            if ctx.needs_input_grad[0]:
+                if Np != N:  # zero-padded reduction axis (persistent buffers: live rows copied)
+                    dyp = _padded_buffer(("fc_dy", Bn, N), (Bn, Np), torch.bfloat16, dy.device)
+                    _copy_rows(dyp, dy, Bn, N)
+                    wpp = _padded_buffer(("fc_w", id(w)), (Np, wp.shape[1]), wp.dtype, wp.device)
+                    _copy_rows(wpp, wp, N, wp.shape[1])
+                    dx = G.linear_dgrad(dyp, wpp)
+                else:
+                    dx = G.linear_dgrad(dy, wp)
+            if ctx.needs_input_grad[1]:
+                dw = G.linear_wgrad(dy, xp, out=grad_target(w))
+            if ctx.needs_input_grad[2]:
+                db = G.colsum(dy, out=grad_target(b))
+            return dx, dw, db
         dyp = dy
         if Np != N or Mp != Bn:
             dyp = _padded_buffer(("fc_dy", Bn, N), (Mp, Np), torch.bfloat16, dy.device)
             _copy_rows(dyp, dy, Bn, N)
-        w, b = ctx.params
         dx = G.linear_dgrad(dyp, wp)[:Bn] if ctx.needs_input_grad[0] else None
         tw, tb = grad_target(w), grad_target(b)
         dw = db = None

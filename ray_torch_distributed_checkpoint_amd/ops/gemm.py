@@ -50,11 +50,17 @@ def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, 
         # split-K slabs for long-K / small-output GEMMs (weight gradients); the launcher decides
         ws = workspace(C.device, min(16 * M * N, SPLITK_WS_ELEMS), "splitk")
     cs_ws = None
-    if colsum_out is not None:
+    defer = colsum_out is not None and batch == 1 and _deferrable(colsum_out)
+    if defer:
+        # partial rows into a buffer of their own; the reduction joins the deferred window
+        cs_ws = torch.empty(4 * ((M + 255) // 256) * N, dtype=torch.float32, device=C.device)
+    elif colsum_out is not None:
         cs_ws = workspace(C.device, (max(4 * ((M + 255) // 256), _COLSUM_BLOCKS) + 64) * N, "colsum_gemm")
-    gpu_ext().gemm_bf16(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
-                        batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act, causal,
-                        ws, tile_cfg, alpha_dev, colsum_out, cs_ws)
+    rows = gpu_ext().gemm_bf16(A, B, C, Cin, bias, aux_in, aux_out, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
+                               batch, batch_inner, sA0, sA1, sB0, sB1, sC0, sC1, float(alpha), float(beta), act,
+                               causal, ws, tile_cfg, alpha_dev, None if defer else colsum_out, cs_ws)
+    if defer and not (rows and _WG.add_job(cs_ws, rows, N, colsum_out, False)):
+        colsum(C, out=colsum_out)  # this kernel left no partial rows (or nothing would flush them)
     return C
 
 
@@ -136,11 +142,28 @@ _ROUND = 256          # tiles per round (one 8-wave block per CU); groups are pa
 # stream joins it at the end of backward.  -0.17 ms/step on GPT-2-small
 # (profiles/wgrad_group_ab_r3.txt); RTDC_WGRAD_SIDE=0 keeps them on the compute stream.
 _GROUP_SIDE = os.environ.get("RTDC_WGRAD_SIDE", "1") != "0"
+# Deferred column sums: the bias / LayerNorm-parameter gradients are reductions of per-block
+# partial rows; inside backward each leaves its partial rows in a buffer of its own and the
+# reductions of a whole window run as ONE launch with the grouped weight gradients' flush
+# (norm.hip colsum_multi_kernel; same per-reduction order, so bitwise the immediate result).
+# ~4 reduction launches per GPT-2 layer otherwise.  RTDC_COLSUM_DEFER=0 reduces immediately.
+_DEFER_ON = os.environ.get("RTDC_COLSUM_DEFER", "1") != "0"
+_JOBS_MAX = 32  # reductions per launch (norm.hip kMultiJobs)
+
+
+def _deferrable(out) -> bool:
+    """A reduction into `out` may be deferred: a parameter's slice of a flat gradient buffer
+    (FlatParamSpace), which AccumulateGrad adopts as p.grad without reading it.  Any other
+    tensor handed to autograd may be cloned (read) right away - before the deferred kernel."""
+    return (_DEFER_ON and _GROUP_ON and out is not None and out.is_cuda and out.dtype == torch.float32
+            and out.is_contiguous() and out.dim() == 1 and out._base is not None
+            and getattr(out._base, "_rtdc_flat_grad", False))
 
 
 class _WgradGroup:
     def __init__(self):
         self.items = []      # (dy, x2d, out, tiles)
+        self.jobs = []       # deferred column sums [ws, W, D, out alias, accumulate]
         self.tiles = 0
         self.ptrs = set()    # data_ptr of every pending output
         self.waiters = []    # (callback) in registration order, run after the flush
@@ -148,13 +171,36 @@ class _WgradGroup:
         self.side = None     # RTDC_WGRAD_SIDE stream
         self.side_busy = False
 
-    def add(self, dy, x2d, out, tiles) -> bool:
+    def _arm(self) -> bool:
         if not self.cb_queued:
             try:
                 torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
             except RuntimeError:  # not inside a backward pass: nothing would flush - run now
                 return False
             self.cb_queued = True
+        return True
+
+    def add_job(self, ws, W, D, out, accumulate) -> bool:
+        """Defer `out (+)= column sums of the W partial rows ws[W][D]` to the next flush (False:
+        not inside backward - the caller reduces now)."""
+        if W < 1 or W > 4096 or not self._arm():
+            return False
+        if len(self.jobs) >= _JOBS_MAX:
+            self.flush()
+        # an alias, not `out` itself (see add())
+        self.jobs.append([ws, int(W), int(D), out.view(out.shape), bool(accumulate)])
+        self.ptrs.add(out.data_ptr())
+        return True
+
+    def pending_job(self, t):
+        for j in self.jobs:
+            if j[3].data_ptr() == t.data_ptr() and j[2] == t.numel():
+                return j
+        return None
+
+    def add(self, dy, x2d, out, tiles) -> bool:
+        if not self._arm():
+            return False
         # keep an alias, not `out` itself: AccumulateGrad adopts the returned tensor as p.grad
         # without a copy only while nothing else references it (otherwise it clones the still
         # unwritten buffer)
@@ -195,23 +241,37 @@ class _WgradGroup:
             gpu_ext().gemm_bf16_grouped([c[0] for c in chunk], [c[1] for c in chunk], [c[2] for c in chunk],
                                         dims, False, False)
 
+    @staticmethod
+    def _launch_jobs(jobs):
+        for i in range(0, len(jobs), _JOBS_MAX):
+            chunk = jobs[i:i + _JOBS_MAX]
+            gpu_ext().colsum_multi([j[0] for j in chunk], [j[3] for j in chunk], [j[1] for j in chunk],
+                                   [j[2] for j in chunk], [int(j[4]) for j in chunk])
+
     def flush(self, join: bool = False):
-        """Launch the pending products, then run the callbacks waiting for them.  join=False
-        (a flush inside backward) may leave them running on the side stream; join=True makes
-        the current stream wait for everything launched there."""
+        """Launch the pending products and column sums, then run the callbacks waiting for
+        them.  join=False (a flush inside backward) may leave them running on the side stream;
+        join=True makes the current stream wait for everything launched there."""
         items, self.items, self.tiles = self.items, [], 0
+        jobs, self.jobs = self.jobs, []
         waiters, self.waiters = self.waiters, []
-        if (items and _GROUP_SIDE and not join and items[0][0].is_cuda
+        dev_t = items[0][0] if items else (jobs[0][0] if jobs else None)
+        if (dev_t is not None and _GROUP_SIDE and not join and dev_t.is_cuda
                 and not torch.cuda.is_current_stream_capturing()):
-            cur = torch.cuda.current_stream(items[0][0].device)
+            cur = torch.cuda.current_stream(dev_t.device)
             if self.side is None:
-                self.side = torch.cuda.Stream(device=items[0][0].device)
+                self.side = torch.cuda.Stream(device=dev_t.device)
             self.side.wait_stream(cur)  # operands written
             with torch.cuda.stream(self.side):
-                self._launch(items)
+                if items:
+                    self._launch(items)
+                if jobs:
+                    self._launch_jobs(jobs)
                 for dy, x2d, _, _ in items:  # the compute stream may recycle them before the kernel ran
                     dy.record_stream(self.side)
                     x2d.record_stream(self.side)
+                for j in jobs:
+                    j[0].record_stream(self.side)
                 self.ptrs = set()
                 self.side_busy = True
                 # (a DDP bucket / overlapped update triggered by these gradients is ordered
@@ -224,7 +284,9 @@ class _WgradGroup:
                 self._launch_split(items)
             else:
                 self._launch(items)
-            self.ptrs = set()
+        if jobs:
+            self._launch_jobs(jobs)
+        self.ptrs = set()
         if self.side_busy and join:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)
             self.side_busy = False
@@ -312,6 +374,31 @@ def offer_colsum(t: torch.Tensor, sums: torch.Tensor) -> None:
     _offered.append((weakref.ref(t), t.data_ptr(), t.numel(), t.shape[-1], t._version, sums))
 
 
+# Per-row-group partial column sums a producer wrote on the way out ([W][N] fp32 rows, e.g. the
+# flash-attention backward's dqkv): colsum() of the same matrix reduces them (deferred when it
+# can) instead of reading the matrix.
+_offered_partials: list = []
+
+
+def partials_wanted() -> bool:
+    return _DEFER_ON
+
+
+def offer_colsum_partials(t: torch.Tensor, rows: torch.Tensor) -> None:
+    _offered_partials[:] = [e for e in _offered_partials if e[0]() is not None][-3:]
+    _offered_partials.append((weakref.ref(t), t.data_ptr(), t.numel(), t.shape[-1], t._version, rows))
+
+
+def _take_partials(x2d: torch.Tensor):
+    for k, (ref, ptr, numel, last, ver, rows) in enumerate(_offered_partials):
+        t = ref()
+        if (t is not None and ptr == x2d.data_ptr() and numel == x2d.numel() and last == x2d.shape[-1]
+                and x2d.is_contiguous() and t._version == ver):
+            del _offered_partials[k]
+            return rows
+    return None
+
+
 def _take_colsum(x2d: torch.Tensor):
     for k, (ref, ptr, numel, last, ver, sums) in enumerate(_offered):
         t = ref()
@@ -328,16 +415,42 @@ def colsum(x2d: torch.Tensor, out=None, accumulate=False):
     M, N = x2d.shape
     sums = _take_colsum(x2d)
     if sums is not None:
-        if out is None:
-            return sums
+        if out is None or out.data_ptr() == sums.data_ptr():
+            return sums if out is None else out
+        job = _WG.pending_job(sums)
+        if job is not None and not accumulate and _deferrable(out):
+            # the sums are a deferred reduction: aim it at `out` instead of copying later
+            _WG.ptrs.discard(sums.data_ptr())
+            job[3] = out.view(out.shape)
+            _WG.ptrs.add(out.data_ptr())
+            return out
+        if job is not None:
+            flush_wgrads()
         if accumulate:
             out.add_(sums)
-        elif out.data_ptr() != sums.data_ptr():
+        else:
             out.copy_(sums)
+        return out
+    rows = _take_partials(x2d) if x2d.is_cuda else None
+    if rows is not None and rows.shape[0] <= 4096 and rows.shape[1] == N:
+        if _deferrable(out) and _WG.add_job(rows.view(-1), rows.shape[0], N, out, accumulate):
+            return out
+        if out is None:
+            out = torch.empty((N,), dtype=torch.float32, device=x2d.device)
+            accumulate = False
+        gpu_ext().colsum_multi([rows.view(-1)], [out], [rows.shape[0]], [N], [int(accumulate)])
+        return out
+    nblk = min(_COLSUM_BLOCKS, max(1, M // 64))
+    if (x2d.is_cuda and _deferrable(out) and x2d.dtype in (torch.bfloat16, torch.float32)
+            and nblk >= 64 and x2d.stride(1) == 1):
+        ws = torch.empty(nblk * N, dtype=torch.float32, device=x2d.device)
+        gpu_ext().colsum_partial(x2d, M, N, x2d.stride(0), ws, nblk)
+        if _WG.add_job(ws, nblk, N, out, accumulate):
+            return out
+        gpu_ext().colsum_multi([ws], [out], [nblk], [N], [int(accumulate)])
         return out
     if out is None:
         out = torch.empty((N,), dtype=torch.float32, device=x2d.device)
-    nblk = min(_COLSUM_BLOCKS, max(1, M // 64))
     ws = workspace(x2d.device, (nblk + 64) * N, "colsum")
     gpu_ext().colsum(x2d, M, N, x2d.stride(0), ws, nblk, out, accumulate)
     return out

@@ -147,6 +147,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, relu
 # Measured neutral on GPT-2-small (profiles/gelu_save_grad_ab.txt): the dgrad epilogue is not
 # bound by its two transcendentals, so the numerics stay on the original pair.
 _GELU_SAVE_GRAD = os.environ.get("RTDC_GELU_SAVE_GRAD", "0") == "1"
+# c_proj's dgrad (dpre = dy . W_proj, M x 4C outputs over K = C) reads W_proj N-major; only the
+# K-major x K-major form has the persistent 8-wave kernel (gemm_8ph.hip gemm8p_kernel, whose
+# next-tile loads and epilogue stores overlap MFMA work - 3 tile rounds at GPT-2 shapes).  The
+# forward writes a K-major bf16 image of W_proj (one transposing conversion from the fp32 master,
+# C x 4C) and the backward runs the dgrad on it.  Measured neutral on GPT-2-small (17.62 vs
+# 17.56 ms/step, alternating runs on one MI355X, profiles/dgrad_kmajor_colsum_defer_ab_r3.txt):
+# opt-in, RTDC_DGRAD_KMAJOR=1.
+_DGRAD_KMAJOR = os.environ.get("RTDC_DGRAD_KMAJOR", "0") == "1"
+
+
+def _kmajor_image(w: torch.Tensor):
+    """bf16 [in, out] image of an fp32 [out, in] master weight (None when not applicable)."""
+    if not (_DGRAD_KMAJOR and w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.is_contiguous()):
+        return None
+    t = torch.empty((w.shape[1], w.shape[0]), dtype=torch.bfloat16, device=w.device)
+    gpu_ext().f32_to_bf16_t(w.detach(), t)
+    return t
 
 
 class _FusedMLP(torch.autograd.Function):
@@ -165,6 +182,7 @@ class _FusedMLP(torch.autograd.Function):
                          aux_out=pre)
         res2 = residual.reshape(-1, C) if residual is not None else None
         y = G.linear_fwd(g, wps, bias=b_proj, residual=res2)
+        ctx.wp_t = _kmajor_image(w_proj) if ctx.needs_input_grad[0] or ctx.needs_input_grad[1] else None
         ctx.save_for_backward(x2, wfs, wps, pre, g)
         ctx.has_res = residual is not None
         ctx.in_shape = x.shape
@@ -185,8 +203,14 @@ class _FusedMLP(torch.autograd.Function):
         db_fc = grad_target(b_fc)
         if db_fc is None and b_fc is not None:
             db_fc = torch.empty(b_fc.shape, dtype=torch.float32, device=dy2.device)
-        dpre = G.linear_dgrad(dy2, wps, act_bwd=G.ACT_MUL if _GELU_SAVE_GRAD else G.ACT_GELU_BWD, aux_in=pre,
-                              colsum_out=db_fc)
+        act = G.ACT_MUL if _GELU_SAVE_GRAD else G.ACT_GELU_BWD
+        wp_t, ctx.wp_t = ctx.wp_t, None
+        if wp_t is not None:
+            M, H = pre.shape
+            dpre = torch.empty((M, H), dtype=torch.bfloat16, device=dy2.device)
+            G.gemm_bf16(dy2, wp_t, dpre, M, H, C, C, C, H, True, True, aux_in=pre, act=act, colsum_out=db_fc)
+        else:
+            dpre = G.linear_dgrad(dy2, wps, act_bwd=act, aux_in=pre, colsum_out=db_fc)
         dw_fc = G.linear_wgrad(dpre, x2, out=grad_target(w_fc))
         dx = G.linear_dgrad(dpre, wfs).view(ctx.in_shape)
         return dx, dw_fc, db_fc, dw_proj, db_proj, (dy if ctx.has_res else None)

@@ -74,7 +74,23 @@ class _LayerNorm(torch.autograd.Function):
             dxsum = grad_target(ctx.sum_param)
             if dxsum is None:
                 dxsum = torch.empty(D, dtype=torch.float32, device=xc.device)
-        gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, dres, dx, wsp, dg, db, dxsum, nw, False)
+        outs = [dg, db] + ([dxsum] if dxsum is not None else [])
+        if all(G._deferrable(o) for o in outs):
+            # partial rows into a buffer of their own, reduced with the deferred window (gemm.py)
+            part = torch.empty(len(outs) * (nw // 4 + 64) * D, dtype=torch.float32, device=xc.device)
+            nblk = gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, dres, dx, part, dg, db, dxsum, nw,
+                                           False, True)
+            rows = part[: len(outs) * nblk * D].view(len(outs), nblk * D)
+            done = [G._WG.add_job(rows[z], nblk, D, o, False) for z, o in enumerate(outs)]
+            if not all(done):
+                if any(done):
+                    G.flush_wgrads()
+                gpu_ext().colsum_multi([rows[z] for z, d in enumerate(done) if not d],
+                                       [o for o, d in zip(outs, done) if not d],
+                                       [nblk] * done.count(False), [D] * done.count(False), [0] * done.count(False))
+        else:
+            gpu_ext().layernorm_bwd(dy.contiguous(), xc, ws, mean, rstd, dres, dx, wsp, dg, db, dxsum, nw, False,
+                                    False)
         if dxsum is not None:
             G.offer_colsum(dx, dxsum)
         return dx, dg, db, None, None, None

@@ -138,6 +138,7 @@ class FlatParamSpace:
         self.grad = None
         if grads:
             self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
+            self.grad._rtdc_flat_grad = True  # (ops/gemm.py _deferrable: a gradient slot autograd adopts)
             for p, s in zip(uniq, self.segments):
                 p.grad = self.view(self.grad, s)
         self.shadow = None

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-3 pass Y: bisect test_adamw_overlap_bitwise_equal over the two new knobs, then the
+# GPT-2 bench A/B (default vs RTDC_DGRAD_KMAJOR=0 vs RTDC_COLSUM_DEFER=0, two rounds).
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for v in base RTDC_COLSUM_DEFER=0 RTDC_DGRAD_KMAJOR=0; do
+  e=$([ $v = base ] && echo "" || echo "$v")
+  env $e timeout -k 10 200 python -u -m pytest tests/test_optim_overlap_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/y_overlap_$v.log 2>&1
+  echo "OVERLAP TESTS $v EXIT $? $(tail -n 1 gpurun_out/y_overlap_$v.log)"
+done
+for r in 1 2; do
+  for v in base RTDC_DGRAD_KMAJOR=0 RTDC_COLSUM_DEFER=0; do
+    e=$([ $v = base ] && echo "" || echo "$v")
+    env $e timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-ckpt > gpurun_out/gpt2_y_${v}_r$r.log 2>&1
+    rc=$?; echo "GPT2 $v r$r EXIT $rc $(tail -n 1 gpurun_out/gpt2_y_${v}_r$r.log | grep -o '"ms_per_step": [0-9.]*')"
+    [ $rc -eq 0 ] || exit $rc
+  done
+done

@@ -240,6 +240,45 @@ def test_fused_mlp():
     _close(bp.grad, ps[4].grad, 1e-4)
 
 
+@pytest.mark.parametrize("R,C", [(768, 3072), (100, 72), (65, 130)])
+def test_f32_to_bf16_transposed(R, C):
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+
+    w = torch.randn(R, C, device=DEV)
+    t = torch.empty(C, R, dtype=torch.bfloat16, device=DEV)
+    gpu_ext().f32_to_bf16_t(w, t)
+    assert torch.equal(t, w.t().contiguous().to(torch.bfloat16))
+
+
+def test_fused_mlp_kmajor_dgrad_matches(monkeypatch):
+    """GPT-2 shape (3 tile rounds): c_proj's dgrad on the K-major weight image (persistent
+    kernel) against the N-major kernel - same products, same K order."""
+    import importlib
+
+    from ray_torch_distributed_checkpoint_amd.ops import fused_mlp
+
+    L = importlib.import_module("ray_torch_distributed_checkpoint_amd.ops.linear")
+    torch.manual_seed(5)
+    M, C = 16384, 768
+    x0 = _bf(M, C)
+    wf = (torch.randn(4 * C, C, device=DEV) * 0.02).requires_grad_(True)
+    bfc = (torch.randn(4 * C, device=DEV) * 0.1).requires_grad_(True)
+    wp = (torch.randn(C, 4 * C, device=DEV) * 0.02).requires_grad_(True)
+    bp = (torch.randn(C, device=DEV) * 0.1).requires_grad_(True)
+    g = _bf(M, C)
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(L, "_DGRAD_KMAJOR", on)
+        x = x0.clone().requires_grad_(True)
+        for p in (wf, bfc, wp, bp):
+            p.grad = None
+        fused_mlp(x, wf, bfc, wp, bp).backward(g)
+        torch.cuda.synchronize()
+        grads.append([t.grad.float().clone() for t in (x, wf, bfc)])
+    for a, b in zip(*grads):
+        _close(a, b, 1e-2)
+
+
 @pytest.mark.parametrize("H,Hkv", [(4, 4), (4, 2)])
 def test_causal_attention(H, Hkv):
     from ray_torch_distributed_checkpoint_amd.ops import causal_attention
@@ -257,6 +296,27 @@ def test_causal_attention(H, Hkv):
     ref.backward(g.float())
     _close(out, ref, 2e-2)
     _close(qkv.grad, qr.grad, 3e-2)
+
+
+@pytest.mark.parametrize("H,Hkv,Dh", [(4, 4, 64), (4, 2, 128)])
+def test_flash_bwd_colsum_partials(H, Hkv, Dh):
+    """The flash backward's per-16-row column sums of dqkv (the qkv bias gradient, offered to
+    the projection's colsum) equal the column sums of the dqkv it stored."""
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(6)
+    Bn, T = 2, 256
+    W = (H + 2 * Hkv) * Dh
+    qkv = _bf(Bn, T, W).requires_grad_(True)
+    out = causal_attention(qkv, H, Hkv)
+    out.backward(_bf(Bn, T, H * Dh))
+    d2 = qkv.grad.view(-1, W)
+    ref = d2.float().sum(0)
+    cs = G.colsum(d2)  # takes the offered partials
+    torch.cuda.synchronize()
+    _close(cs, ref, 1e-5)
+    assert G._take_partials(d2) is None  # consumed
 
 
 def test_layernorm_rmsnorm():

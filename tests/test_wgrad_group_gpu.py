@@ -107,6 +107,63 @@ def test_small_remainder_goes_split_k_and_equals_immediate():
         assert torch.equal(a[n], b[n]), n
 
 
+def test_deferred_colsums_bitwise_equal_immediate():
+    """Bias / LayerNorm-parameter gradients reduced in the deferred window (one colsum_multi
+    launch per flush) are bitwise the immediate reductions."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(7)
+    data = torch.randint(0, 1024, (4, 1025), generator=g).to(dev)
+    njobs = []
+    orig = G._WgradGroup._launch_jobs
+
+    def spy(jobs):
+        njobs.append(len(jobs))
+        return orig(jobs)
+
+    G._WgradGroup._launch_jobs = staticmethod(spy)
+    try:
+        a = _grads(True, data, n_layer=3)
+    finally:
+        G._WgradGroup._launch_jobs = staticmethod(orig)
+    # per layer: ln_1 / ln_2 (dgamma, dbeta, dx colsum = the residual projections' biases),
+    # c_attn bias, c_fc bias; + ln_f
+    assert sum(njobs) >= 3 * 8, njobs
+    assert not G._WG.jobs
+    old = G._DEFER_ON
+    G._DEFER_ON = False
+    try:
+        b = _grads(True, data, n_layer=3)
+    finally:
+        G._DEFER_ON = old
+    for n in a:
+        if n.endswith("c_attn.bias"):
+            # from the flash backward's 16-row partials (RTDC_COLSUM_DEFER=0: a pass over dqkv):
+            # another summation order
+            err = (a[n] - b[n]).abs().max() / b[n].abs().max()
+            assert err < 1e-5, f"{n}: {err:.3e}"
+        else:
+            assert torch.equal(a[n], b[n]), n
+
+
+def test_colsum_multi_matches_sum():
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+
+    torch.manual_seed(8)
+    dev = torch.device("cuda", 0)
+    shapes = [(768, 768), (64, 2304), (3, 100), (4096, 72)]
+    ws = [torch.randn(W, D, device=dev) for W, D in shapes]
+    outs = [torch.randn(D, device=dev) for _, D in shapes]
+    base = [o.clone() for o in outs]
+    acc = [0, 1, 0, 1]
+    gpu_ext().colsum_multi([w.reshape(-1) for w in ws], outs, [W for W, _ in shapes], [D for _, D in shapes], acc)
+    torch.cuda.synchronize()
+    for w, o, b, a in zip(ws, outs, base, acc):
+        ref = w.double().sum(0) + (b.double() if a else 0.0)
+        assert torch.allclose(o.double(), ref, rtol=1e-5, atol=1e-4)
+
+
 def test_greedy_packing_fills_rounds():
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
 
