@@ -95,7 +95,7 @@ int rtdc_pool_bn_bwd(const void* dy, const void* arg, const void* x, const float
                      int B, int H, int W, int C, int Ho, int Wo, hipStream_t st);
 int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* gamma,
                 const float* beta, void* dx, void* dres, float* dgamma, float* dbeta, long long N, int C, int relu,
-                float* ws, int nblk, hipStream_t st);
+                float* ws, int nblk, const float* psum, const float* psumx, int p_nblk, hipStream_t st);
 int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, int B, int H, int W, int C, int Ho, int Wo,
                  int K, int s, int p, int backward, hipStream_t st);
 int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st);
@@ -516,10 +516,11 @@ static void swiglu_bwd(Tensor gu, Tensor dh, Tensor dgu) {
 // X is NHWC [B, H, W, Cx]; the window is KH x KW (K = KH*KW*Cx in mode 1, N in mode 2).
 // stats_mean/stats_m2 (mode 1, optional): fused BatchNorm statistics per output row tile,
 // [ceil(M/128)][N] fp32; returns the rows per statistics tile (128 or 256).
-static int64_t conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K,
-                         int64_t ld_other, int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad,
-                         c10::optional<Tensor> ws, c10::optional<Tensor> stats_mean, c10::optional<Tensor> stats_m2,
-                         c10::optional<Tensor> accumulate) {
+static int64_t conv_gemm_impl(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K,
+                              int64_t ld_other, int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad,
+                              c10::optional<Tensor> ws, c10::optional<Tensor> stats_mean,
+                              c10::optional<Tensor> stats_m2, c10::optional<Tensor> accumulate,
+                              const std::vector<Tensor>* bnb) {
   check_dev(X, "X");
   check_dev(other, "other");
   TORCH_CHECK(X.is_contiguous() && X.dim() == 4 && X.scalar_type() == at::kBFloat16, "conv_gemm: X must be NHWC bf16");
@@ -565,8 +566,44 @@ static int64_t conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t
     a.Cin = accumulate->data_ptr();
     a.beta = 1.f;
   }
+  if (bnb) {  // [x, mean, rstd, gamma, beta (, y)]: BatchNorm-backward statistics into stats_mean / stats_m2
+    TORCH_CHECK(mode == 1 && (bnb->size() == 5 || bnb->size() == 6) && stats_mean.has_value() && stats_m2.has_value(),
+                "conv_gemm_bnb: mode 1, [x, mean, rstd, gamma, beta (, y)] and both statistics buffers");
+    const Tensor& x = (*bnb)[0];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.numel() == C.numel(),
+                "conv_gemm_bnb: x must match C");
+    for (int i = 1; i < 5; ++i)
+      TORCH_CHECK((*bnb)[i].is_cuda() && (*bnb)[i].scalar_type() == at::kFloat && (*bnb)[i].numel() >= N,
+                  "conv_gemm_bnb: fp32 [N] BatchNorm parameters");
+    a.bnb_x = (const uint16_t*)x.data_ptr();
+    a.bnb_mean = (*bnb)[1].data_ptr<float>();
+    a.bnb_rstd = (*bnb)[2].data_ptr<float>();
+    a.bnb_gamma = (*bnb)[3].data_ptr<float>();
+    a.bnb_beta = (*bnb)[4].data_ptr<float>();
+    if (bnb->size() == 6) {  // ReLU mask from the BN + residual output y
+      const Tensor& y = (*bnb)[5];
+      TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.numel() == C.numel(),
+                  "conv_gemm_bnb: y must match C");
+      a.bnb_y = (const uint16_t*)y.data_ptr();
+    }
+  }
   check_rc(rtdc_conv_gemm(&a, (int)mode, cur_stream()), "conv_gemm");
   return bm;
+}
+static int64_t conv_gemm(Tensor X, Tensor other, Tensor C, int64_t mode, int64_t M, int64_t N, int64_t K,
+                         int64_t ld_other, int64_t Ho, int64_t Wo, int64_t KW, int64_t stride, int64_t pad,
+                         c10::optional<Tensor> ws, c10::optional<Tensor> stats_mean, c10::optional<Tensor> stats_m2,
+                         c10::optional<Tensor> accumulate) {
+  return conv_gemm_impl(X, other, C, mode, M, N, K, ld_other, Ho, Wo, KW, stride, pad, ws, stats_mean, stats_m2,
+                        accumulate, nullptr);
+}
+// stride-1 dgrad whose output is the gradient at relu(BN(x)): also the BatchNorm-backward
+// partial sums (sum g, sum g*xhat) per row tile - returns the tile height (rows per partial)
+static int64_t conv_gemm_bnb(Tensor X, Tensor other, Tensor C, int64_t M, int64_t N, int64_t K, int64_t ld_other,
+                             int64_t Ho, int64_t Wo, int64_t KW, int64_t pad, Tensor psum, Tensor psumx,
+                             c10::optional<Tensor> accumulate, std::vector<Tensor> bnb) {
+  return conv_gemm_impl(X, other, C, 1, M, N, K, ld_other, Ho, Wo, KW, 1, pad, c10::nullopt, psum, psumx, accumulate,
+                        &bnb);
 }
 
 // x: NHWC bf16 [B,H,W,C]; cols: [B*Ho*Wo, Kp] with K = KH*KW*C real columns (rest zero).
@@ -675,8 +712,16 @@ static void bn_relu_maxpool(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Te
 }
 static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, c10::optional<Tensor> beta,
                    Tensor dx, c10::optional<Tensor> dres, Tensor dgamma, Tensor dbeta, int64_t relu, Tensor ws,
-                   int64_t nblk) {
+                   int64_t nblk, c10::optional<Tensor> psum, c10::optional<Tensor> psumx) {
   const int64_t C = x.size(-1), N = x.numel() / C;
+  int64_t p_nblk = 0;
+  if (psum.has_value()) {  // [p_nblk][C] partials of (sum g, sum g*xhat) from dy's producer
+    TORCH_CHECK(psumx.has_value() && psum->scalar_type() == at::kFloat && psumx->scalar_type() == at::kFloat &&
+                    psum->dim() == 2 && psum->size(1) == C && psumx->sizes() == psum->sizes() &&
+                    psum->is_contiguous() && psumx->is_contiguous(),
+                "bn_bwd: psum / psumx fp32 [nblk][C]");
+    p_nblk = psum->size(0);
+  }
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dx.is_contiguous(), "bn_bwd: contiguous tensors expected");
   TORCH_CHECK(ws.numel() >= 2 * nblk * C, "bn_bwd: workspace too small");
   TORCH_CHECK(relu >= 0 && relu <= 2, "bn_bwd: relu mode 0/1/2");
@@ -685,7 +730,8 @@ static void bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tens
   check_rc(rtdc_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), relu == 2 ? beta->data_ptr<float>() : nullptr, dx.data_ptr(),
                        ptr_or_null(dres), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), N, (int)C, (int)relu,
-                       ws.data_ptr<float>(), (int)nblk, cur_stream()),
+                       ws.data_ptr<float>(), (int)nblk, psum.has_value() ? psum->data_ptr<float>() : nullptr,
+                       psumx.has_value() ? psumx->data_ptr<float>() : nullptr, (int)p_nblk, cur_stream()),
            "bn_bwd");
 }
 // mean cross-entropy from per-row losses: out[0] = loss, out[1] = divisor (device count of
@@ -921,6 +967,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("im2col", &im2col);
   m.def("conv_gemm", &conv_gemm);
+  m.def("conv_gemm_bnb", &conv_gemm_bnb);
   m.def("col2im", &col2im);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);

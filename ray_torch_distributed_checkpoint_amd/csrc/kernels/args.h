@@ -42,6 +42,16 @@ struct GemmArgs {
   float* cs_out;
   float* cs_ws;
   long long cs_ws_elems;
+  // optional fused BatchNorm-BACKWARD statistics (implicit-GEMM stride-1 dgrad, mode 1): the
+  // output C is the gradient g at the output of relu(BN(x)) with x = bnb_x ([M][N], ld = ldc);
+  // per row-tile t and column n: sum g*mask and sum g*mask*xhat -> stats_mean / stats_m2
+  // (mask = BN(x) > 0 recomputed from x, xhat = (x - mean) * rstd)
+  const uint16_t* bnb_x;
+  const float* bnb_mean;
+  const float* bnb_rstd;
+  const float* bnb_gamma;
+  const float* bnb_beta;
+  const uint16_t* bnb_y;  // optional: mask = bnb_y > 0 (BN + residual + ReLU output) instead
 };
 
 // fp32 MFMA GEMM (gemm_f32.hip)

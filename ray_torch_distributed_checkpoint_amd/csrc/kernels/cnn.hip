@@ -1064,17 +1064,24 @@ extern "C" int rtdc_bn_relu_maxpool(const void* x, void* y, void* arg, const flo
 }
 
 // relu: 0 none, 1 mask from y, 2 mask recomputed from x (needs beta; y unused)
+// psum / psumx (optional, p_nblk rows each): the (sum g, sum g*xhat) partials already reduced by
+// the producer of dy (conv_gemm_bnb: the dgrad GEMM epilogue) - the statistics pass is skipped
 extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd,
                            const float* gamma, const float* beta, void* dx, void* dres, float* dgamma, float* dbeta,
-                           long long N, int C, int relu, float* ws, int nblk, hipStream_t st) {
+                           long long N, int C, int relu, float* ws, int nblk, const float* psum, const float* psumx,
+                           int p_nblk, hipStream_t st) {
   const int R = (int)((N + nblk - 1) / nblk);
   if (C % 8 != 0 || N * C >= (1LL << 31) || relu < 0 || relu > 2 || (relu == 2 && !beta)) return 1;
-  hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)(relu == 1 ? y : nullptr), (const bf16_t*)x, mean, rstd, N, C, R, 1, ws,
-                     ws + (long long)nblk * C, relu == 2 ? gamma : (const float*)nullptr,
-                     relu == 2 ? beta : (const float*)nullptr);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
-                     (const float*)(ws + (long long)nblk * C), nblk, C, dbeta, dgamma);
+  if (psum) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, st, psum, psumx, p_nblk, C, dbeta, dgamma);
+  } else {
+    hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)(relu == 1 ? y : nullptr), (const bf16_t*)x, mean, rstd, N, C, R, 1, ws,
+                       ws + (long long)nblk * C, relu == 2 ? gamma : (const float*)nullptr,
+                       relu == 2 ? beta : (const float*)nullptr);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, st, (const float*)ws,
+                       (const float*)(ws + (long long)nblk * C), nblk, C, dbeta, dgamma);
+  }
 #define BWA(R)                                                                                          \
   hipLaunchKernelGGL(bn_bwd_apply_kernel<R>, dim3(gsz(N * (C / 8))), dim3(256), 0, st, (const bf16_t*)dy, \
                      (const bf16_t*)y, (const bf16_t*)x, mean, rstd, gamma, (const float*)dbeta,           \

@@ -105,6 +105,80 @@ __device__ __forceinline__ void conv_tile_stats(const GemmArgs& a, const f32x4 (
   }
 }
 
+// Per-column BatchNorm-backward partials of this block's output tile (GM 4), in a pass after
+// the epilogue: each lane re-reads the bf16 gradient values it just stored (L2-hot), x (and
+// y), one 16-column block at a time (`unroll 1`: the per-column constants and sums stay ~30
+// registers - kept in registers across the epilogue they cost the 8-wave tiles a wave per SIMD,
+// +0.9 ms on ResNet-18); the 16 lanes sharing a column and then the WM waves are added in fixed
+// order -> stats_mean[tile][n] = sum g*mask, stats_m2 = sum g*mask*xhat.
+template <class CFG, typename OutT>
+__device__ __forceinline__ void bnb_tile_stats(const GemmArgs& a, const OutT* C, int m0, int n0, int wm, int wn,
+                                               int lane, char* smem) {
+  constexpr int TM = CFG::TM, TN = CFG::TN, WM = CFG::WM, BN = CFG::BN, BM = CFG::BM;
+  float* sh = (float*)smem;  // [WM][BN][2]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's C stores are complete
+  __syncthreads();                                  // staging buffers are free
+#pragma unroll 1
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (TN * 16) + j * 16 + 4 * (lane >> 4);
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n < a.N) {  // (N % 8 == 0: the lane's 4 columns are all in range)
+      float mu[4], rs[4], ka[4], kb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mu[r] = a.bnb_mean[n + r];
+        rs[r] = a.bnb_rstd[n + r];
+        // the forward's ReLU argument t = fma(x, rstd*gamma, beta - mean*rstd*gamma) (bn_apply_kernel)
+        ka[r] = rs[r] * a.bnb_gamma[n + r];
+        kb[r] = a.bnb_beta[n + r] - mu[r] * ka[r];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
+        if (m >= a.M) continue;
+        const long long off = (long long)m * a.ldc + n;
+        float gv[4], xv[4], yv[4];
+        load4<OutT>(C + off, gv);  // as stored (bf16)
+        load4<bf16_t>((const bf16_t*)a.bnb_x + off, xv);
+        if (a.bnb_y) load4<bf16_t>((const bf16_t*)a.bnb_y + off, yv);  // (wave-uniform)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool on = a.bnb_y ? yv[r] > 0.f : fmaf(xv[r], ka[r], kb[r]) > 0.f;
+          const float gm = on ? gv[r] : 0.f;
+          s1[r] += gm;
+          s2[r] += gm * (xv[r] - mu[r]) * rs[r];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] = row16_sum(s1[r]);
+      s2[r] = row16_sum(s2[r]);
+    }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * (TN * 16) + j * 16 + 4 * (lane >> 4) + r;
+        sh[(wm * BN + col) * 2] = s1[r];
+        sh[(wm * BN + col) * 2 + 1] = s2[r];
+      }
+    }
+  }
+  __syncthreads();
+  const int tile = m0 / BM;
+  for (int col = threadIdx.x; col < BN; col += CFG::NT) {
+    const int nn = n0 + col;
+    if (nn >= a.N) continue;
+    float S = 0.f, Q = 0.f;
+    for (int w = 0; w < WM; ++w) {
+      S += sh[(w * BN + col) * 2];
+      Q += sh[(w * BN + col) * 2 + 1];
+    }
+    a.stats_mean[(long long)tile * a.N + nn] = S;
+    a.stats_m2[(long long)tile * a.N + nn] = Q;
+  }
+}
+
 // outstanding glds allowed at an NS-stage wait: `ahead` later stages of LPS loads each
 // (wave-uniform; immediates only)
 template <int LPS>
@@ -177,12 +251,14 @@ __global__ __launch_bounds__(CFG::NT, NS == 2 ? 2 : 1) void gemm_bf16_kernel(Gem
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // GM 1: gathered A (implicit-GEMM convolution); 3: the same plus fused BatchNorm statistics
-  using SA = std::conditional_t<GM == 1 || GM == 3, ConvStagerK<BM, NW>, Stager<AK, BM, NW>>;
+  // GM 1: gathered A (implicit-GEMM convolution); 3: the same plus fused BatchNorm statistics;
+  // 4: gathered A plus fused BatchNorm-backward statistics of the output (bnb_*)
+  constexpr bool GATHER_A = GM == 1 || GM == 3 || GM == 4;
+  using SA = std::conditional_t<GATHER_A, ConvStagerK<BM, NW>, Stager<AK, BM, NW>>;
   using SB = std::conditional_t<GM == 2, ConvStagerMN<BN, NW>, Stager<BKM, BN, NW>>;
   SA sa;
   SB sb;
-  if constexpr (GM == 1 || GM == 3) sa.init(a, A, a.M, m0, wave, lane);
+  if constexpr (GATHER_A) sa.init(a, A, a.M, m0, wave, lane);
   else sa.init(A, a.lda, a.M, m0, wave, lane);
   if constexpr (GM == 2) sb.init(a, B, a.N, n0, wave, lane);
   else sb.init(B, a.ldb, a.N, n0, wave, lane);
@@ -334,6 +410,7 @@ __global__ __launch_bounds__(CFG::NT, NS == 2 ? 2 : 1) void gemm_bf16_kernel(Gem
     }
   }
   if constexpr (GM == 3) conv_tile_stats<CFG>(a, acc, alpha, m0, n0, wm, wn, lane, smem);
+  if constexpr (GM == 4) bnb_tile_stats<CFG>(a, C, m0, n0, wm, wn, lane, smem);
 }
 
 // out[m][n] = sum_s ws[s][m][n] (+ beta * Cin[m][n]).  A block owns 64 float4 column groups
@@ -680,7 +757,12 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
   if (mode == 1) {
     if (a.M != a.cv_npix) return 1;
     // stats rows are per BM-row tile: 256 (256x64 tiles) or 128
-    if (a.stats_mean) {
+    if (a.bnb_x) {
+      // BatchNorm-backward statistics of the (stride-1 dgrad) output: 8-wave tiles only
+      if (!a.stats_mean || !a.stats_m2 || !a.bnb_mean || !a.bnb_rstd || !a.bnb_gamma || !a.bnb_beta) return 1;
+      if (a.N <= 64) launch_cfg<Cfg256x64w8, true, true, bf16_t, 4>(a, 1, stream);
+      else launch_cfg<Cfg128x128w8, true, true, bf16_t, 4>(a, 1, stream);
+    } else if (a.stats_mean) {
       if (a.N <= 64 && conv64_w8()) launch_cfg<Cfg256x64w8, true, true, bf16_t, 3>(a, 1, stream);
       else if (a.N <= 64) launch_conv<Cfg256x64, true, true, bf16_t, 3>(a, stream);
       else if (conv128_w8()) launch_cfg<Cfg128x128w8, true, true, bf16_t, 3>(a, 1, stream);

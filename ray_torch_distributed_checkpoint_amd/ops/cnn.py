@@ -23,6 +23,7 @@ CPU tensors run the PyTorch reference of every op (NHWC in, NHWC out).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -115,8 +116,11 @@ def _implicit_ok(C: int, M: int) -> bool:
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, bn_stats=False, stash=None):
+    def forward(ctx, x, w, stride, pad, bn_stats=False, stash=None, bnb=None):
         ctx.stash = stash
+        # x = relu(BN(xb) (+ residual)): (xb, mean, rstd, gamma, beta (, y = x: the ReLU mask source
+        # when a residual was added)) for the dgrad epilogue's BatchNorm-backward statistics
+        ctx.bnb = None if bnb is None else (tuple(bnb[:5]) + ((x,) if len(bnb) > 5 else ()))
         B, H, W, C = x.shape
         Cout, Cin, KH, KW = w.shape
         assert Cin == C, (x.shape, w.shape)
@@ -189,14 +193,29 @@ class _Conv2d(torch.autograd.Function):
                     # gradient of x from its other consumer is added in the epilogue (beta = 1)
                     s = shadow_of_w(ctx, wm, Cout, C, KH, KW)
                     Kt = KH * KW * Cout
-                    gpu_ext().conv_gemm(dy, s, dx.view(B * H * W, C), 1, B * H * W, C, Kt, Kt, H, W, KW, 1,
-                                        KH - 1 - pad, None, None, None,
-                                        None if acc is None else acc.view(B * H * W, C))
+                    bnb = ctx.bnb if _BNB_FUSED else None
+                    # only when this kernel writes the COMPLETE gradient of x (the last of x's
+                    # consumers to run backward adds the others' contributions here)
+                    complete = ctx.stash is None or ctx.stash.left == 0
+                    if bnb is not None and complete and bnb[0].shape == dx.shape:
+                        # dx is the gradient at relu(BN(xb)): the BatchNorm backward's statistics
+                        # (sum g, sum g*xhat per channel) are reduced in this GEMM's epilogue
+                        Mx = B * H * W
+                        bm = 256 if C <= 64 else 128
+                        nt = (Mx + bm - 1) // bm
+                        ps = torch.empty((2, nt, C), dtype=torch.float32, device=dy.device)
+                        gpu_ext().conv_gemm_bnb(dy, s, dx.view(Mx, C), Mx, C, Kt, Kt, H, W, KW, KH - 1 - pad,
+                                                ps[0], ps[1], None if acc is None else acc.view(Mx, C), list(bnb))
+                        _offer_bnb(dx, ps)
+                    else:
+                        gpu_ext().conv_gemm(dy, s, dx.view(B * H * W, C), 1, B * H * W, C, Kt, Kt, H, W, KW, 1,
+                                            KH - 1 - pad, None, None, None,
+                                            None if acc is None else acc.view(B * H * W, C))
                 else:
                     dcols = G.linear_dgrad(dy2, wm)  # [Mp, K]
                     gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad, acc)
                 dx = _depart(ctx.stash, dx)
-            return dx, dw, None, None, None, None
+            return dx, dw, None, None, None, None, None
         cols = saved
         if ctx.needs_input_grad[1]:
             dwm = G.linear_wgrad(dy2, cols)  # [Cout, Kp] fp32
@@ -218,7 +237,30 @@ class _Conv2d(torch.autograd.Function):
                 dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
                 gpu_ext().col2im(dcols[:M] if Mp > M else dcols, dx, Ho, Wo, KH, KW, stride, pad, acc)
             dx = _depart(ctx.stash, dx)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
+
+
+# BatchNorm-backward statistics handed from a stride-1 dgrad (conv_gemm_bnb) to the BatchNorm
+# backward that consumes its output: keyed by the gradient tensor (weakref, data_ptr, numel,
+# version).  Opt-in (RTDC_BNB_FUSED=1): measured 8.69 / 8.70 vs 8.53 / 8.69 ms/step on
+# ResNet-18 (profiles/bnb_dgrad_stats_ab_r3.txt) - the epilogue pass re-reads the tile and x
+# with 8-B lane accesses, no cheaper than bn_reduce_kernel's 16-B streaming pass it replaces.
+_BNB_FUSED = os.environ.get("RTDC_BNB_FUSED", "0") == "1"
+_bnb_offers: list = []
+
+
+def _offer_bnb(g: torch.Tensor, partials: torch.Tensor) -> None:
+    _bnb_offers[:] = [e for e in _bnb_offers if e[0]() is not None][-3:]
+    _bnb_offers.append((weakref.ref(g), g.data_ptr(), g.numel(), g._version, partials))
+
+
+def _take_bnb(g: torch.Tensor):
+    for k, (ref, ptr, numel, ver, part) in enumerate(_bnb_offers):
+        t = ref()
+        if t is not None and ptr == g.data_ptr() and numel == g.numel() and t._version == ver and g.is_contiguous():
+            del _bnb_offers[k]
+            return part
+    return None
 
 
 def _arrive(stash):
@@ -284,7 +326,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, bn_s
         require_dtype(x, "conv2d")
     else:
         return conv2d_ref(x, w, stride, pad)
-    y = _Conv2d.apply(x, w, stride, pad, bn_stats, grad_accum)
+    y = _Conv2d.apply(x, w, stride, pad, bn_stats, grad_accum, getattr(x, "_rtdc_bnb", None))
     st = getattr(y.grad_fn, "stats", None) if y.grad_fn is not None else None
     if st is not None:
         y._rtdc_bn_stats = st  # (mean [tiles, C], M2 [tiles, C], rows per tile)
@@ -401,6 +443,14 @@ class _BatchNorm(torch.autograd.Function):
         # residual was added before the ReLU (mode 1: y > 0)
         ctx.relu = 0 if not relu else (1 if residual is not None or not _BN_MASK_FROM_X else 2)
         ctx.save_for_backward(x, y if ctx.relu == 1 else None, mean, rstd, weight)
+        # y = relu(BN(x)): a stride-1 convolution of y reduces this BatchNorm's backward
+        # statistics in its dgrad epilogue (conv2d / _Conv2d.backward)
+        ctx.bnb = None
+        if (training and ctx.relu and weight.dtype == torch.float32 and bias is not None
+                and bias.dtype == torch.float32):
+            # (mode 1: the mask source is y itself - the consumer substitutes its own input, so
+            # no reference from y's grad_fn back to y)
+            ctx.bnb = (x, mean, rstd, weight, bias) + (("y",) if ctx.relu == 1 else ())
         ctx.params = (weight, bias)
         ctx.has_res = residual is not None
         return y
@@ -421,8 +471,10 @@ class _BatchNorm(torch.autograd.Function):
             dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
+        part = _take_bnb(dy) if ctx.relu else None
         gpu_ext().bn_bwd(dy, y if ctx.relu == 1 else x, x, mean, rstd, weight, b if ctx.relu == 2 else None, dx,
-                         dres, dgamma, dbeta, ctx.relu, ws, nblk)
+                         dres, dgamma, dbeta, ctx.relu, ws, nblk, None if part is None else part[0],
+                         None if part is None else part[1])
         if dres is not None and ctx.res_stash is not None:
             # the shortcut's gradient: normally added by the block's convolution(s) of the same
             # input inside their dgrad kernels
@@ -455,8 +507,12 @@ def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, trainin
         if training and num_batches_tracked is not None:
             num_batches_tracked.add_(1)
         return batch_norm_ref(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
-    return _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
-                            num_batches_tracked, residual_grad_to)
+    y = _BatchNorm.apply(x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
+                         num_batches_tracked, residual_grad_to)
+    bnb = getattr(y.grad_fn, "bnb", None) if y.grad_fn is not None else None
+    if bnb is not None:
+        y._rtdc_bnb = bnb
+    return y
 
 
 # stem backward without the full-resolution pool gradient (RTDC_POOL_BN_FUSED=0: maxpool backward
@@ -525,7 +581,7 @@ class _BNReluMaxPool(torch.autograd.Function):
         gpu_ext().maxpool_bwd(dy, arg, dz, k, s, p)
         nblk = _bn_blocks(N, C)
         ws = G.workspace(x.device, 2 * nblk * C, "bn")
-        gpu_ext().bn_bwd(dz, x, x, mean, rstd, weight, b, dx, None, dgamma, dbeta, 2, ws, nblk)
+        gpu_ext().bn_bwd(dz, x, x, mean, rstd, weight, b, dx, None, dgamma, dbeta, 2, ws, nblk, None, None)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 

@@ -4,8 +4,8 @@ The token-table gradient is a scatter-add where rows repeat; instead of float at
 summation order changes run to run) the token ids are stably sorted once and the native
 kernel sums each run of equal ids in original token order: bitwise-reproducible gradients,
 required for bit-exact resume (BASELINE config 5).  The sort is the native
-one-workgroup radix sort (`data_ops.hip` sort_ids) on a side stream under the forward pass -
-no rocprim / ATen sort kernels in the step."""
+one-workgroup radix sort (`data_ops.hip` sort_ids) on a side stream under the LM head's
+cross-entropy kernel - no rocprim / ATen sort kernels in the step."""
 from __future__ import annotations
 
 import torch
@@ -38,6 +38,46 @@ def _side_stream(device) -> torch.cuda.Stream:
     return s
 
 
+class _PendingSort:
+    """The backward's token sort, launched on the side stream when a kernel that tolerates one
+    busy CU runs (`launch_pending_sorts`, called before the LM head's cross-entropy kernel).
+    Launched right after the embedding, the one-workgroup sort held a CU during the first
+    layer's persistent GEMM (one block per CU, every CU needed): qkv 123 vs 72 us."""
+
+    def __init__(self, idx_c, rows):
+        self.idx_c, self.rows, self.out = idx_c, rows, None
+
+    def launch(self, side: bool = True):
+        if self.out is None:
+            dev = self.idx_c.device
+            cur = torch.cuda.current_stream(dev)
+            if side:
+                st = _side_stream(dev)
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    sidx, perm = sort_ids(self.idx_c.reshape(-1), self.rows)
+                    done = torch.cuda.Event()
+                    done.record(st)
+                sidx.record_stream(cur)
+                perm.record_stream(cur)
+            else:
+                sidx, perm = sort_ids(self.idx_c.reshape(-1), self.rows)
+                done = None
+            self.out = (sidx, perm, done)
+        return self.out
+
+
+_pending: list = []
+# RTDC_SORT_AT_XENT=0: launch the sort right after the embedding (A/B)
+_SORT_AT_XENT = __import__("os").environ.get("RTDC_SORT_AT_XENT", "1") != "0"
+
+
+def launch_pending_sorts() -> None:
+    """Start the pending token sorts of this forward pass on the side stream (now)."""
+    while _pending:
+        _pending.pop().launch()
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, wte, wpe, presort=True):
@@ -50,16 +90,12 @@ class _Embedding(torch.autograd.Function):
         # stream, concurrently with the forward pass, instead of on the backward's critical path
         ctx.sorted = None
         if presort:
-            cur = torch.cuda.current_stream(idx.device)
-            side = _side_stream(idx.device)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                sidx, perm = sort_ids(idx_c.reshape(-1), wte.shape[0])
-                done = torch.cuda.Event()
-                done.record(side)
-            sidx.record_stream(cur)
-            perm.record_stream(cur)
-            ctx.sorted = (sidx, perm, done)
+            ctx.sorted = _PendingSort(idx_c, wte.shape[0])
+            if _SORT_AT_XENT:
+                del _pending[:-3]  # (forwards whose sorts never launched: no backward followed)
+                _pending.append(ctx.sorted)
+            else:
+                ctx.sorted.launch()
         ctx.save_for_backward(idx_c)
         ctx.shapes = (wte.shape, None if wpe is None else wpe.shape)
         ctx.params = (wte, wpe)
@@ -87,8 +123,11 @@ class _Embedding(torch.autograd.Function):
             elif T < wpe_shape[0]:
                 dwpe[T:].zero_()  # the kernel writes (not adds) positions [0, T)
         if ctx.sorted is not None:
-            sidx, perm, done = ctx.sorted
-            torch.cuda.current_stream(idx.device).wait_event(done)
+            if ctx.sorted in _pending:
+                _pending.remove(ctx.sorted)
+            sidx, perm, done = ctx.sorted.launch(side=False) if ctx.sorted.out is None else ctx.sorted.out
+            if done is not None:
+                torch.cuda.current_stream(idx.device).wait_event(done)
         else:
             sidx, perm = sort_ids(idx.reshape(-1), wte_shape[0])
         gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)

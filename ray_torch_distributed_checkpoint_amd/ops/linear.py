@@ -152,7 +152,7 @@ _GELU_SAVE_GRAD = os.environ.get("RTDC_GELU_SAVE_GRAD", "0") == "1"
 # next-tile loads and epilogue stores overlap MFMA work - 3 tile rounds at GPT-2 shapes).  The
 # forward writes a K-major bf16 image of W_proj (one transposing conversion from the fp32 master,
 # C x 4C) and the backward runs the dgrad on it.  Measured neutral on GPT-2-small (17.62 vs
-# 17.56 ms/step, alternating runs on one MI355X, profiles/dgrad_kmajor_colsum_defer_ab_r3.txt):
+# 17.56 ms/step, alternating runs on one MI355X, profiles/colsum_defer_pool_bn_ab_r3.txt):
 # opt-in, RTDC_DGRAD_KMAJOR=1.
 _DGRAD_KMAJOR = os.environ.get("RTDC_DGRAD_KMAJOR", "0") == "1"
 

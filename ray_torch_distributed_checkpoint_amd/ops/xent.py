@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext
+from .embedding import launch_pending_sorts
 from .gradbuf import grad_target
 from .shadow import shadow_of
 
@@ -113,6 +114,7 @@ class _LMHeadXent(torch.autograd.Function):
             # TF, profiles/gemm_bench_r3_4wave_v2.jsonl: ~0.2 ms/step); RTDC_LMHEAD_BLASLT=1
             # selects it for A/B runs only
             logits = torch.matmul(x2, ws.t()) if _LM_BLASLT else G.linear_fwd(x2, ws)
+            launch_pending_sorts()  # the embedding backward's token sort, under the xent kernel
             gpu_ext().xent(logits, logits, tgt, loss, None, None, M, vocab, Vp, scale, IGNORE_INDEX)
         else:
             # row chunks: each chunk's logits land in one reused buffer small enough to stay in
@@ -127,6 +129,7 @@ class _LMHeadXent(torch.autograd.Function):
                 G.gemm_bf16(x2[r0:r0 + n], ws, chunk, n, Vp, C, C, C, Vp, True, True)
                 gpu_ext().xent(chunk, logits[r0:r0 + n], tgt[r0:r0 + n], loss[r0:r0 + n], None, None, n, vocab,
                                Vp, scale, IGNORE_INDEX)
+        launch_pending_sorts()
         out = torch.empty(2, dtype=torch.float32, device=x.device)
         # out[0] = mean loss; out[1] = divisor (device count of non-ignored rows, or n_valid -
         # whose 1/n_valid the kernel already folded into the gradient)

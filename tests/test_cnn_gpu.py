@@ -375,3 +375,66 @@ def test_grad_join_matches_autograd_add(shortcut):
     ref, got = run(False), run(True)
     err = (got - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_backward_statistics_in_dgrad_epilogue(C, residual, monkeypatch):
+    """conv1 -> BN + ReLU -> conv2 (stride 1): with RTDC_BNB_FUSED the BatchNorm backward's
+    statistics come from conv2's dgrad epilogue (conv_gemm_bnb) instead of a pass over the
+    gradient - same gradients to rounding, against the unfused path and fp32 torch, including a
+    partial last row tile; run-to-run bitwise."""
+    import importlib
+
+    cnn = importlib.import_module("ray_torch_distributed_checkpoint_amd.ops.cnn")
+    torch.manual_seed(C)
+    B, H = 3, 13  # 507 pixels: partial last tile for 128- and 256-row tiles
+    x0 = torch.randn(B, H, H, C, device=DEV).bfloat16()
+    w1 = torch.randn(C, C, 3, 3, device=DEV) * 0.05
+    w2 = torch.randn(C, C, 3, 3, device=DEV) * 0.05
+    g0 = torch.randn(C, device=DEV)
+    b0 = torch.randn(C, device=DEV) * 0.5
+    dy = torch.randn(B, H, H, C, device=DEV).bfloat16()
+    taken = []
+    orig = cnn._take_bnb
+
+    def spy(g):
+        r = orig(g)
+        taken.append(r is not None)
+        return r
+
+    monkeypatch.setattr(cnn, "_take_bnb", spy)
+
+    def run(fused):
+        monkeypatch.setattr(cnn, "_BNB_FUSED", fused)
+        x = x0.clone().requires_grad_(True)
+        g, b = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        h = cnn.conv2d(x, w1, 1, 1)
+        # residual: relu(BN(h) + x) - the backward's mask comes from the output (bnb_y)
+        z = cnn.batch_norm(h, g, b, rm, rv, True, relu=True, residual=x if residual else None)
+        y = cnn.conv2d(z, w2, 1, 1)
+        y.backward(dy)
+        run.h = h.detach()
+        return [t.grad.float().clone() for t in (x, g, b)]
+
+    ref = run(False)
+    assert taken == [False]
+    got = run(True)
+    assert taken == [False, True]
+    again = run(True)
+    for n, a, r, a2 in zip(("dx", "dgamma", "dbeta"), got, ref, again):
+        _close(a, r, 1e-2 if n == "dx" else 1e-4, n)
+        assert torch.equal(a, a2), f"{n}: not run-to-run bitwise"
+    # fp32 torch from the same bf16 BatchNorm input (a conv output recomputed in fp32 would move
+    # elements across the ReLU boundary and change dbeta by whole gradient values)
+    gr, br = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+    hr = run.h.float().permute(0, 3, 1, 2)
+    zr = F.batch_norm(hr, None, None, gr, br, True)
+    if residual:
+        zr = zr + x0.float().permute(0, 3, 1, 2)
+    zr = torch.relu(zr)
+    yr = F.conv2d(zr, w2.bfloat16().float(), padding=1)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    _close(got[1], gr.grad, 3e-2, "dgamma vs torch")
+    _close(got[2], br.grad, 3e-2, "dbeta vs torch")
