@@ -740,35 +740,39 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
 template <int C>
 __device__ __forceinline__ void pool3s2_gather(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, int b,
                                                int h, int w, int c, int Ho, int Wo, float* g) {
-  int hos[2], khs[2], nh = 0, wos[2], kws[2], nw = 0;
-  if (h & 1) {
-    if ((h + 1) / 2 < Ho) { hos[nh] = (h + 1) / 2; khs[nh++] = 0; }
-    hos[nh] = (h - 1) / 2; khs[nh++] = 2;
-  } else {
-    if (h / 2 < Ho) { hos[nh] = h / 2; khs[nh++] = 1; }
-  }
-  if (w & 1) {
-    if ((w + 1) / 2 < Wo) { wos[nw] = (w + 1) / 2; kws[nw++] = 0; }
-    wos[nw] = (w - 1) / 2; kws[nw++] = 2;
-  } else {
-    if (w / 2 < Wo) { wos[nw] = w / 2; kws[nw++] = 1; }
+  // branch-free: input row h is covered by output row a = h >> 1 (tap 1 if h even, tap 2 if odd)
+  // and, for odd h, by a + 1 (tap 0) when it exists; same for columns.  All four candidate
+  // windows are loaded unconditionally (an absent one re-reads window (a, a') and is masked
+  // out), so every load of a thread is independent and issued together.
+  const int ah = h >> 1, aw = w >> 1;
+  const bool h1 = (h & 1) && ah + 1 < Ho, w1 = (w & 1) && aw + 1 < Wo;
+  const uint32_t th0 = (h & 1) ? 2u : 1u, tw0 = (w & 1) ? 2u : 1u;
+  const int hh[2] = {ah, h1 ? ah + 1 : ah}, ww[2] = {aw, w1 ? aw + 1 : aw};
+  const uint32_t th[2] = {th0, 0u}, tw[2] = {tw0, 0u};
+  const bool okh[2] = {true, h1}, okw[2] = {true, w1};
+  uint2 a8[4];
+  uint4 g4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t o = ((size_t)(b * Ho + hh[k >> 1]) * Wo + ww[k & 1]) * C + c;
+    a8[k] = *(const uint2*)(arg + o);
+    g4[k] = *(const uint4*)(dy + o);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) g[e] = 0.f;
-  for (int a = 0; a < nh; ++a)
-    for (int bb = 0; bb < nw; ++bb) {
-      const size_t o = ((size_t)(b * Ho + hos[a]) * Wo + wos[bb]) * C + c;
-      const uint2 a8 = *(const uint2*)(arg + o);
-      const uint4 g4 = *(const uint4*)(dy + o);
-      const uint32_t tap = khs[a] * 3 + kws[bb];
-      const uint32_t gw[4] = {g4.x, g4.y, g4.z, g4.w};
+  // summed in maxpool3s2_bwd_kernel's window order (row a+1 before a, column a'+1 before a')
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t ae = ((e < 4 ? a8.x : a8.y) >> (8 * (e & 3))) & 0xffu;
-        const float v = __uint_as_float((e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] << 16));
-        if (ae == tap) g[e] += v;
-      }
+  for (int k = 3; k >= 0; --k) {
+    const bool ok = okh[k >> 1] && okw[k & 1];
+    const uint32_t tap = ok ? th[k >> 1] * 3 + tw[k & 1] : 0xffu;  // 0xff: never an argmax tap
+    const uint32_t gw[4] = {g4[k].x, g4[k].y, g4[k].z, g4[k].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t ae = ((e < 4 ? a8[k].x : a8[k].y) >> (8 * (e & 3))) & 0xffu;
+      const float v = __uint_as_float((e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] << 16));
+      g[e] += ae == tap ? v : 0.f;
     }
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) g[e] = bf2f(f2bf(g[e]));  // the stored bf16 gradient
 }
@@ -797,6 +801,7 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_reduce_kernel(const bf16_t* _
     kb[e] = beta[c + e] - m8[e] * ka[e];
     s1[e] = s2[e] = 0.f;
   }
+#pragma unroll 2
   for (int i = i0; i < total; i += stride) {
     const int pix = i / CG;
     const int q = pix / W, w = pix - q * W;
@@ -859,6 +864,7 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(const bf16_t* __
     ka[e] = rstd[c + e] * gamma[c + e];
     kb[e] = beta[c + e] - mean[c + e] * ka[e];
   }
+#pragma unroll 2
   for (int i = i0; i < total; i += stride) {
     const int pix = i / CG;
     const int q = pix / W, w = pix - q * W;
