@@ -404,9 +404,13 @@ def stem_conv(x: torch.Tensor, w: torch.Tensor, bn_stats: bool = True) -> torch.
     return y
 
 
+# 16-B loads per thread and stream in the BatchNorm statistics pass (RTDC_BN_LOADS for A/B runs)
+_BN_LOADS = int(os.environ.get("RTDC_BN_LOADS", "32"))
+
+
 def _bn_blocks(N: int, C: int) -> int:
-    # ~32 16-B loads per thread in the statistics pass; bounded so the merge stays cheap
-    return max(1, min(2048, (N * C) // (256 * 8 * 32)))
+    # ~_BN_LOADS 16-B loads per thread in the statistics pass; bounded so the merge stays cheap
+    return max(1, min(4096, (N * C) // (256 * 8 * _BN_LOADS)))
 
 
 _BN_MASK_FROM_X = os.environ.get("RTDC_BN_MASK_FROM_X", "1") != "0"
