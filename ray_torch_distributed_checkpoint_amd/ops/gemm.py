@@ -136,7 +136,9 @@ def _round_split_rows(rows: int, cols: int, k: int, device) -> int:
 _GROUP_ON = os.environ.get("RTDC_WGRAD_GROUP", "1") != "0"
 _GROUP_MAX = 10       # products per launch (gemm8g_kernel G8_MAX_GROUP)
 _GROUP_TILES = 200    # products with fewer output tiles than this are deferred
-_ROUND = 256          # tiles per round (one 8-wave block per CU); groups are packed up to it
+# tiles per round (one 8-wave block per CU); groups are packed up to it (RTDC_WGRAD_ROUND: A/B of
+# smaller groups that leave CUs to the compute stream's kernels while a group runs)
+_ROUND = int(os.environ.get("RTDC_WGRAD_ROUND", "256"))
 # Grouped launches inside backward go to a side stream, so the next layer's backward kernels
 # can take the CUs a 216-tile group leaves idle (one 8-wave block fills a CU); the compute
 # stream joins it at the end of backward.  -0.17 ms/step on GPT-2-small
