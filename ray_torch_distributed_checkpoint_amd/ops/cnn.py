@@ -410,7 +410,7 @@ _BN_LOADS = int(os.environ.get("RTDC_BN_LOADS", "32"))
 
 def _bn_blocks(N: int, C: int) -> int:
     # ~_BN_LOADS 16-B loads per thread in the statistics pass; bounded so the merge stays cheap
-    return max(1, min(4096, (N * C) // (256 * 8 * _BN_LOADS)))
+    return max(1, min(2048, (N * C) // (256 * 8 * _BN_LOADS)))
 
 
 _BN_MASK_FROM_X = os.environ.get("RTDC_BN_MASK_FROM_X", "1") != "0"
