@@ -506,7 +506,10 @@ static void colsum_ws_reduce(const float* ws, int W, int D, float* tmp, OutPtrs 
                              hipStream_t st, int nz = 1, long long ws_z = 0) {
   int S = W / 32;
   S = S < 1 ? 1 : (S > 64 ? 64 : S);
-  if (S > 1 && W <= kWideMaxRows && colsum_wide_enabled()) {
+  // every W the wide kernel takes goes through it - also a handful of rows: the deferred form
+  // (colsum_multi_kernel) sums in its order, so a reduction's bits must not depend on whether
+  // its target was a deferrable gradient slot
+  if (W <= kWideMaxRows && colsum_wide_enabled()) {
     hipLaunchKernelGGL(colsum_wide_kernel, dim3((D + 63) / 64, 1, nz), dim3(1024), 0, st, ws, outs, W, D, accumulate,
                        ws_z);
   } else if (S > 1 && tmp) {

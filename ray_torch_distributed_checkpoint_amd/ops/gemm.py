@@ -149,7 +149,8 @@ _GROUP_SIDE = os.environ.get("RTDC_WGRAD_SIDE", "1") != "0"
 # reductions of a whole window run as ONE launch with the grouped weight gradients' flush
 # (norm.hip colsum_multi_kernel; same per-reduction order, so bitwise the immediate result).
 # ~4 reduction launches per GPT-2 layer otherwise.  RTDC_COLSUM_DEFER=0 reduces immediately.
-_DEFER_ON = os.environ.get("RTDC_COLSUM_DEFER", "1") != "0"
+_DEFER_ON = (os.environ.get("RTDC_COLSUM_DEFER", "1") != "0"
+             and os.environ.get("RTDC_COLSUM_WIDE", "1") != "0")  # (same summation order only then)
 _JOBS_MAX = 32  # reductions per launch (norm.hip kMultiJobs)
 
 
