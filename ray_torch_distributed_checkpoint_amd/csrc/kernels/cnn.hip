@@ -398,6 +398,47 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   }
 }
 
+// Split merge, stage 1: block (x, s) merges the per-row-block (mean, M2) partials of row-blocks
+// [s*per, min(nblk, (s+1)*per)) for channels 64x + lane.  Lanes run along the channels, so every
+// wave load is 256 coalesced bytes (bn_finalize_kernel alone - a block per channel whose loads
+// stride C floats - ran ~10 us per BatchNorm over the ~6k GEMM-tile partials of a 56x56 layer on
+// 64..512 blocks).  Same two-sum form as bn_finalize_kernel; the 4 waves' sums are added in wave
+// order (fixed).  Stage 2 is bn_finalize_kernel over the splits: split s is a row-block of
+// per*R rows.
+__global__ __launch_bounds__(256) void bn_merge_split_kernel(const float* __restrict__ pmean,
+                                                            const float* __restrict__ pm2, int nblk, long long N,
+                                                            int R, int C, int per, float* __restrict__ omean,
+                                                            float* __restrict__ om2) {
+  __shared__ float red[4][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l, s = blockIdx.y;
+  const int b0 = s * per, b1 = min(nblk, b0 + per);
+  const float ns = (float)max(0LL, min((long long)per * R, N - (long long)b0 * R));
+  float snm = 0.f;
+  if (c < C)
+    for (int b = b0 + w; b < b1; b += 4) {
+      const float nb = (float)max(0LL, min((long long)R, N - (long long)b * R));
+      snm += nb * pmean[(long long)b * C + c];
+    }
+  red[w][l] = snm;
+  __syncthreads();
+  const float mean = ns > 0.f ? ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l])) / ns : 0.f;
+  __syncthreads();
+  float sm2 = 0.f;
+  if (c < C)
+    for (int b = b0 + w; b < b1; b += 4) {
+      const float nb = (float)max(0LL, min((long long)R, N - (long long)b * R));
+      const float d = pmean[(long long)b * C + c] - mean;
+      sm2 += pm2[(long long)b * C + c] + nb * d * d;
+    }
+  red[w][l] = sm2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    omean[(long long)s * C + c] = mean;
+    om2[(long long)s * C + c] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  }
+}
+
 // y = act((x - mean) * rstd * gamma + beta (+ res)); 8 channels per thread (C % 8 == 0).
 // The grid stride (gridDim.x * 256 threads) is a multiple of C/8 whenever 256 % (C/8) == 0, so
 // each thread keeps ONE group of 8 channels for its whole grid-stride loop: the per-channel
@@ -1034,6 +1075,15 @@ extern "C" int rtdc_col2im(const void* dcols, void* dx, const void* addend, int 
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+static bool split_finalize_enabled() {
+  static int v = -1;  // RTDC_BN_SPLIT_FINALIZE=0: one block per channel over all partials (A/B)
+  if (v < 0) {
+    const char* e = getenv("RTDC_BN_SPLIT_FINALIZE");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // pmean/pm2 (optional): per-row-block statistics already computed by the producer (the
 // convolution GEMM epilogue, blocks of pR rows): the statistics pass over x is skipped.
 extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean, float* rstd, const float* gamma,
@@ -1042,8 +1092,22 @@ extern "C" int rtdc_bn_fwd(const void* x, const void* res, void* y, float* mean,
                            const float* pm2, int p_nblk, int p_R, long long* nbt, hipStream_t st) {
   if (C % 8 != 0 || N * C >= (1LL << 31)) return 1;
   if (training && pmean) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, pmean, pm2, p_nblk, N, p_R, C, eps, momentum, mean,
-                       rstd, running_mean, running_var, nbt);
+    // many producer partials: merged in splits over ~512 coalesced blocks first (ws holds the
+    // 2 x S split rows; S <= nblk, the caller's ws capacity), then finalized per channel
+    const int cg = (C + 63) / 64;
+    int S = std::min(std::min((512 + cg - 1) / cg, (p_nblk + 7) / 8), nblk);
+    if (S >= 4 && ws && split_finalize_enabled()) {
+      const int per = (p_nblk + S - 1) / S;
+      S = (p_nblk + per - 1) / per;
+      hipLaunchKernelGGL(bn_merge_split_kernel, dim3(cg, S), dim3(256), 0, st, pmean, pm2, p_nblk, N, p_R, C, per, ws,
+                         ws + (long long)S * C);
+      hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)ws,
+                         (const float*)(ws + (long long)S * C), S, N, per * p_R, C, eps, momentum, mean, rstd,
+                         running_mean, running_var, nbt);
+    } else {
+      hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, pmean, pm2, p_nblk, N, p_R, C, eps, momentum,
+                         mean, rstd, running_mean, running_var, nbt);
+    }
   } else if (training) {
     const int R = (int)((N + nblk - 1) / nblk);
     hipLaunchKernelGGL(bn_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)nullptr,
@@ -1102,26 +1166,34 @@ extern "C" int rtdc_bn_bwd(const void* dy, const void* y, const void* x, const f
 // dgrad operand of a stride-1 convolution: W'[c][kh'][kw'][co] = W[co][KH-1-kh'][KW-1-kw'][c]
 // from the forward's bf16 [Cout][KH][KW][Cin] matrix (one launch instead of ATen's flip +
 // permute + contiguous copy per conv per step).  Output-linear indexing: coalesced writes.
+// out[c][kh][kw][co] = w[co][KH-1-kh][KW-1-kw][c] (stride-1 dgrad operand): for each (kh, kw) a
+// [Cout][C] -> [C][Cout] transpose in 64x64 tiles through LDS, coalesced 128-B wave rows on both
+// sides and 32-bit index math (the element-wise form with 64-bit div/mod per element ran ~7 us
+// per ResNet conv).
 __global__ __launch_bounds__(256) void conv_w_flip_t_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
                                                            int Cout, int KH, int KW, int C) {
-  const long long n = (long long)Cout * KH * KW * C;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    long long t = i;
-    const int co = (int)(t % Cout); t /= Cout;
-    const int kw = (int)(t % KW); t /= KW;
-    const int kh = (int)(t % KH); t /= KH;
-    const int c = (int)t;
-    out[i] = w[(((long long)co * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * C + c];
+  __shared__ bf16_t tile[64][66];  // +2: the column reads hit distinct banks
+  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 64, khw = blockIdx.z;
+  const int kh = khw / KW, kw = khw - kh * KW;
+  const int src = (KH - 1 - kh) * KW + (KW - 1 - kw), taps = KH * KW;
+  const int l = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + 4 * i, co = co0 + r, c = c0 + l;
+    if (co < Cout && c < C) tile[r][l] = w[(co * taps + src) * C + c];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + 4 * i, c = c0 + r, co = co0 + l;
+    if (c < C && co < Cout) out[(c * taps + khw) * Cout + co] = tile[l][r];
   }
 }
 
 extern "C" int rtdc_conv_w_flip_t(const void* w, void* out, int Cout, int KH, int KW, int C, hipStream_t st) {
-  const long long n = (long long)Cout * KH * KW * C;
-  long long blocks = (n + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(conv_w_flip_t_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)w, (bf16_t*)out,
-                     Cout, KH, KW, C);
+  if (Cout < 1 || C < 1 || KH < 1 || KW < 1 || (long long)Cout * KH * KW * C >= (1LL << 31)) return 1;
+  hipLaunchKernelGGL(conv_w_flip_t_kernel, dim3((C + 63) / 64, (Cout + 63) / 64, KH * KW), dim3(256), 0, st,
+                     (const bf16_t*)w, (bf16_t*)out, Cout, KH, KW, C);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

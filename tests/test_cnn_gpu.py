@@ -322,9 +322,12 @@ def test_resnet18_matches_reference_and_trains():
     assert losses[-1] < 0.5 * losses[0], losses
 
 
-@pytest.mark.parametrize("B,H,C,Cout,s", [(4, 28, 64, 64, 1), (2, 14, 128, 256, 2), (2, 13, 64, 128, 1)])
+@pytest.mark.parametrize("B,H,C,Cout,s", [(4, 28, 64, 64, 1), (2, 14, 128, 256, 2), (2, 13, 64, 128, 1),
+                                             (16, 56, 64, 64, 1), (3, 30, 64, 128, 1)])
 def test_conv_fused_bn_statistics(B, H, C, Cout, s):
-    """BatchNorm statistics computed in the implicit-GEMM epilogue == the separate pass."""
+    """BatchNorm statistics computed in the implicit-GEMM epilogue == the separate pass (the
+    larger shapes merge hundreds of tile partials through the split merge, with a partial last
+    split)."""
     from ray_torch_distributed_checkpoint_amd.ops import cnn
 
     torch.manual_seed(B + H + Cout)
