@@ -741,6 +741,213 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// ---- 3x3 / stride-1 / pad-1 convolution weight gradient with input reuse ----------------
+// dW[co][kh][kw][ci] = sum over pixels p of dy[p][co] * x[p + (kh-1, kw-1)][ci] (NHWC bf16,
+// fp32 out).  The implicit GEMM (mode 2) gathers im2col(X) per 256-column tile: X is read once
+// per tap (9x) plus dY once per column tile - 1.24 GB for a 56x56x64 layer at batch 256, which
+// ran the Cout = 64 weight gradients at ~380 TF (156 us).  Here a block owns a 64(co) x 64(ci)
+// output tile for ALL nine taps and walks chunks of RC = 64 / W whole image rows: per chunk it
+// stages dY (64 pixels x 64 co) and the X halo the nine taps need ((RC+2) x (W+2) pixels x 64 ci,
+// zero rows / columns outside the image) once, and the taps are row offsets into that halo
+// (the transposing LDS read takes one row address per lane, so a shifted tap costs nothing).
+// 12 waves: wave (kh, quadrant) accumulates taps (kh, 0..2) of a 32x32 quadrant.  Staging is
+// global_load_lds into three LDS buffers (two chunks in flight under this chunk's MFMAs,
+// counted vmcnt, one barrier per chunk; the padding slots load from a zero line); the
+// transposing reads use the asm protocol of common.h (the builtin form drains vmcnt).  Blocks
+// split the chunks; fp32 partial slabs are summed by splitk_reduce_kernel (fixed order).
+namespace wg3 {
+constexpr int kThreads = 768, kDyBytes = 64 * 128, kMaxHalo = 192, kBuf = 3 * kThreads * 16;
+__device__ __forceinline__ int swz(int row) { return (row & 7) ^ (((row >> 3) & 1) << 2); }
+__device__ __forceinline__ int off(int row, int ch) {  // 128-B rows of 8 16-B chunks, swizzled
+  return row * 128 + ((ch ^ swz(row)) << 4);
+}
+struct Args {
+  const bf16_t* x;
+  const bf16_t* dy;
+  float* out;
+  int B, H, W, Cin, Cout, RC, cpi, nchunks, per, halo;
+  long long slab;
+};
+// 16 columns c0.. of rows r_lo / r_hi of an image as a 16x16x32 MFMA operand (lane l: column
+// c0 + (l&15), rows 8(l>>4) + j): two transposing reads, retired by the caller's lgkm wait
+__device__ __forceinline__ TrPair frag(const char* img, int r_lo, int r_hi, int c0, int lane) {
+  const int p = lane & 3, c = (c0 >> 3) + (p >> 1), b = (p & 1) << 3;
+  TrPair f;
+  f.lo = ds_tr16(img + off(r_lo, c) + b);
+  f.hi = ds_tr16(img + off(r_hi, c) + b);
+  return f;
+}
+}  // namespace wg3
+
+__global__ __launch_bounds__(768, 1) void conv3x3_wgrad_kernel(wg3::Args a) {
+  using namespace wg3;
+  __shared__ __attribute__((aligned(16))) char smem[3 * kBuf];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int kh = wv >> 2, quad = wv & 3, co_s = (quad >> 1) * 32, ci_s = (quad & 1) * 32;
+  const int ntc = a.Cin / 64;
+  const int co0 = (blockIdx.x / ntc) * 64, ci0 = (blockIdx.x % ntc) * 64;
+  const int c_begin = blockIdx.y * a.per, c_end = min(a.nchunks, c_begin + a.per);
+  const int W2 = a.W + 2, npieces = 512 + a.halo * 8, npx = a.RC * a.W;
+  // this lane's operand rows (chunk pixels k; chunk-invariant): dY row k, halo row of tap (kh, 0)
+  const int q4 = (lane & 15) >> 2, g = lane >> 4;
+  int kr[2][2], hb[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = ks * 32 + 8 * g + 4 * h + q4;
+      kr[ks][h] = k;
+      hb[ks][h] = k < npx ? (k / a.W + kh) * W2 + k % a.W : 0;  // (padding pixels: dY row is 0)
+    }
+  // this thread's three staging slots (slot i -> LDS byte 16 i of a buffer), chunk-invariant
+  // but for the image / row origin: source row offset from the chunk's first row, column,
+  // channel offset (logical chunk of the swizzled slot); dr = -2: padding (zero line)
+  int s_dr[3], s_w[3], s_c[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = tid + j * kThreads;
+    s_dr[j] = -2;
+    s_w[j] = 0;
+    s_c[j] = 0;
+    if (i < 512) {
+      const int r = i >> 3;
+      if (r < npx) {
+        s_dr[j] = r / a.W;
+        s_w[j] = r % a.W;
+        s_c[j] = ((i & 7) ^ swz(r)) * 8;
+      }
+    } else if (i < npieces) {
+      const int r = (i - 512) >> 3, hr = r / W2;
+      s_dr[j] = hr - 1;
+      s_w[j] = r - hr * W2 - 1;
+      s_c[j] = ((i & 7) ^ swz(r)) * 8;
+    }
+  }
+  auto issue = [&](int ch, char* buf) {
+    const int b = ch / a.cpi, h0 = (ch - b * a.cpi) * a.RC;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int i = tid + j * kThreads, hh = h0 + s_dr[j], ww = s_w[j];
+      const bool ok = s_dr[j] != -2 && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pix = (long long)(b * a.H + hh) * a.W + ww;
+      const bf16_t* src = !ok ? (const bf16_t*)g_conv_zero
+                          : i < 512 ? a.dy + pix * a.Cout + co0 + s_c[j]
+                                    : a.x + pix * a.Cin + ci0 + s_c[j];
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(buf + (j * kThreads + wv * 64) * 16), 16, 0, 0);
+    }
+  };
+  f32x4 acc[3][2][2];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int n = c_end - c_begin;
+  if (n > 0) issue(c_begin, smem);
+  if (n > 1) issue(c_begin + 1, smem + kBuf);
+  for (int t = 0; t < n; ++t) {
+    // this chunk's three loads are in; the next chunk's may still be in flight
+    if (t + 1 < n)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every thread's slots landed; buffer (t+2)%3 was last read in step t-1
+    if (t + 2 < n) issue(c_begin + t + 2, smem + ((t + 2) % 3) * kBuf);
+    const char* buf = smem + (t % 3) * kBuf;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      TrPair af[2], bfr[3][2];
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm) af[fm] = frag(buf, kr[ks][0], kr[ks][1], co_s + 16 * fm, lane);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn)
+          bfr[kw][fn] = frag(buf + kDyBytes, hb[ks][0] + kw, hb[ks][1] + kw, ci_s + 16 * fn, lane);
+      lgkm_wait0();
+      bf16x8 A[2], Bv[3][2];
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm) A[fm] = tr_use(af[fm]);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn) Bv[kw][fn] = tr_use(bfr[kw][fn]);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 2; ++fn)
+            acc[kw][fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[fm], Bv[kw][fn], acc[kw][fm][fn], 0, 0, 0);
+    }
+  }
+  // C[m = co][n = ci]: lane holds rows 4(l>>4) + r of column l & 15
+  float* out = a.out + (long long)blockIdx.y * a.slab;
+  const int K9 = 9 * a.Cin;
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + co_s + 16 * fm + 4 * g + r, ci = ci0 + ci_s + 16 * fn + (lane & 15);
+          out[(long long)co * K9 + (kh * 3 + kw) * a.Cin + ci] = acc[kw][fm][fn][r];
+        }
+}
+
+static bool conv3_wgrad_enabled() {
+  static int v = -1;  // RTDC_CONV3_WGRAD=0: the implicit-GEMM weight gradient (A/B)
+  if (v < 0) {
+    const char* e = getenv("RTDC_CONV3_WGRAD");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+// mode-2 arguments of a 3x3 / stride 1 / pad 1 weight gradient -> conv3x3_wgrad_kernel (+ the
+// split reduce); 1 = shape not taken (the caller runs the implicit GEMM)
+static int launch_conv3x3_wgrad(const GemmArgs& ga, hipStream_t st) {
+  const int H = ga.cv_H, W = ga.cv_W, Cin = ga.cv_C, Cout = ga.M;
+  if (Cin % 64 || Cout % 64 || W < 1 || W > 64 || H < 1 || ga.lda != Cout) return 1;
+  const int B = ga.cv_npix / (H * W);
+  int RC = 64 / W;
+  RC = RC < H ? RC : H;
+  const int halo = (RC + 2) * (W + 2);
+  if (halo > wg3::kMaxHalo || 512 + halo * 8 > 3 * wg3::kThreads) return 1;
+  wg3::Args a{};
+  a.x = (const bf16_t*)ga.B;
+  a.dy = (const bf16_t*)ga.A;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.RC = RC; a.halo = halo;
+  a.cpi = (H + RC - 1) / RC;
+  a.nchunks = B * a.cpi;
+  a.slab = (long long)Cout * 9 * Cin;
+  const int tiles = (Cout / 64) * (Cin / 64);
+  int S = 256 / tiles;
+  S = S < 1 ? 1 : S;
+  S = S < a.nchunks ? S : a.nchunks;
+  if (S > 1 && (!ga.ws || (long long)S * a.slab > ga.ws_elems))
+    S = ga.ws ? (int)(ga.ws_elems / a.slab) : 1;
+  S = S < 1 ? 1 : S;
+  a.per = (a.nchunks + S - 1) / S;
+  S = (a.nchunks + a.per - 1) / a.per;
+  a.out = S > 1 ? ga.ws : (float*)ga.C;
+  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(tiles, S), dim3(wg3::kThreads), 0, st, a);
+  if (S > 1) {
+    GemmArgs r = ga;
+    r.N = 9 * Cin;
+    r.ldc = 9 * Cin;
+    r.splitk = S;
+    r.Cin = nullptr;
+    r.beta = 0.f;
+    launch_splitk_reduce<float>(r, st);
+  }
+  return 0;
+}
+
 // Implicit-GEMM convolution products on the same MFMA kernel (see ConvStagerK / ConvStagerMN):
 //   mode 1: C[npix][N] (bf16) = im2col(X)[npix][K] . B[N][K]^T     conv forward / stride-1 dgrad
 //   mode 2: C[M][N]   (fp32) = A[K=npix][M]^T . im2col(X)[npix][N] weight gradient (split-K)
@@ -775,6 +982,9 @@ extern "C" int rtdc_conv_gemm(const GemmArgs* args, int mode, hipStream_t stream
     }
   } else if (mode == 2) {
     if (a.K < a.cv_npix || a.stats_mean) return 1;
+    if (conv3_wgrad_enabled() && a.cv_KW == 3 && a.N == 9 * a.cv_C && a.cv_stride == 1 && a.cv_pad == 1 &&
+        a.cv_Ho == a.cv_H && a.cv_Wo == a.cv_W && launch_conv3x3_wgrad(a, stream) == 0)
+      return hipGetLastError() == hipSuccess ? 0 : 2;
     const bool narrow = a.M <= 64;
     a.splitk = pick_splitk(a, narrow ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a), conv_stages() > 2 ? 256 : 512);
     if (narrow && conv64wg_w8()) launch_cfg<Cfg64x256w8, false, false, float, 2>(a, 1, stream);

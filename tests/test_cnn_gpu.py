@@ -33,6 +33,10 @@ def _nhwc(x):
         (2, 14, 128, 256, 3, 1, 1),  # implicit GEMM, 128x128 tiles
         (4, 28, 128, 64, 3, 1, 1),  # Cout = 64: 256x64 fwd tile, 64x256 wgrad tile
         (2, 9, 64, 64, 3, 2, 1),  # odd spatial size, strided
+        (3, 56, 64, 64, 3, 1, 1),  # 3x3/s1 weight gradient with input reuse: one row per chunk, split
+        (2, 9, 64, 64, 3, 1, 1),  # ... 7 rows per chunk, the second chunk of each image partial
+        (2, 7, 512, 256, 3, 1, 1),  # ... many output tiles, one chunk per image
+        (1, 64, 64, 64, 3, 1, 1),  # ... halo too large (W = 64): the implicit GEMM takes it
     ],
 )
 def test_conv2d(B, H, C, Cout, k, s, p):
