@@ -35,7 +35,9 @@ def _nhwc(x):
         (2, 9, 64, 64, 3, 2, 1),  # odd spatial size, strided
         (3, 56, 64, 64, 3, 1, 1),  # 3x3/s1 weight gradient with input reuse: one row per chunk, split
         (2, 9, 64, 64, 3, 1, 1),  # ... 7 rows per chunk, the second chunk of each image partial
-        (2, 7, 512, 256, 3, 1, 1),  # ... many output tiles, one chunk per image
+        (2, 7, 512, 256, 3, 1, 1),  # (many output tiles: the implicit GEMM)
+        (2, 28, 128, 128, 3, 1, 1),  # ... four output tiles, two rows per chunk
+        (1, 5, 64, 128, 3, 1, 1),  # ... one chunk per image (5 of 12 rows), two tiles
         (1, 64, 64, 64, 3, 1, 1),  # ... halo too large (W = 64): the implicit GEMM takes it
     ],
 )
