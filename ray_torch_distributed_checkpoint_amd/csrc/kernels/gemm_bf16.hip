@@ -756,7 +756,12 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
 // transposing reads use the asm protocol of common.h (the builtin form drains vmcnt).  Blocks
 // split the chunks; fp32 partial slabs are summed by splitk_reduce_kernel (fixed order).
 namespace wg3 {
-constexpr int kThreads = 768, kDyBytes = 64 * 128, kMaxHalo = 192, kBuf = 3 * kThreads * 16;
+constexpr int kThreads = 768;
+// KP pixels per chunk (64 or 128): NSL 16-B staging slots per thread, LDS bytes per buffer
+template <int KP> struct Cfg {
+  static constexpr int NSL = KP == 128 ? 4 : 3, kDyBytes = KP * 128, kBuf = NSL * kThreads * 16;
+  static constexpr int kMaxHalo = (NSL * kThreads - KP * 8) / 8;
+};
 __device__ __forceinline__ int swz(int row) { return (row & 7) ^ (((row >> 3) & 1) << 2); }
 __device__ __forceinline__ int off(int row, int ch) {  // 128-B rows of 8 16-B chunks, swizzled
   return row * 128 + ((ch ^ swz(row)) << 4);
@@ -779,20 +784,22 @@ __device__ __forceinline__ TrPair frag(const char* img, int r_lo, int r_hi, int 
 }
 }  // namespace wg3
 
+template <int KP>
 __global__ __launch_bounds__(768, 1) void conv3x3_wgrad_kernel(wg3::Args a) {
   using namespace wg3;
+  constexpr int NSL = Cfg<KP>::NSL, kDyBytes = Cfg<KP>::kDyBytes, kBuf = Cfg<KP>::kBuf, KS = KP / 32, NDY = KP * 8;
   __shared__ __attribute__((aligned(16))) char smem[3 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int kh = wv >> 2, quad = wv & 3, co_s = (quad >> 1) * 32, ci_s = (quad & 1) * 32;
   const int ntc = a.Cin / 64;
   const int co0 = (blockIdx.x / ntc) * 64, ci0 = (blockIdx.x % ntc) * 64;
   const int c_begin = blockIdx.y * a.per, c_end = min(a.nchunks, c_begin + a.per);
-  const int W2 = a.W + 2, npieces = 512 + a.halo * 8, npx = a.RC * a.W;
+  const int W2 = a.W + 2, npieces = NDY + a.halo * 8, npx = a.RC * a.W;
   // this lane's operand rows (chunk pixels k; chunk-invariant): dY row k, halo row of tap (kh, 0)
   const int q4 = (lane & 15) >> 2, g = lane >> 4;
-  int kr[2][2], hb[2][2];
+  int kr[KS][2], hb[KS][2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = ks * 32 + 8 * g + 4 * h + q4;
@@ -802,14 +809,14 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wgrad_kernel(wg3::Args a) {
   // this thread's three staging slots (slot i -> LDS byte 16 i of a buffer), chunk-invariant
   // but for the image / row origin: source row offset from the chunk's first row, column,
   // channel offset (logical chunk of the swizzled slot); dr = -2: padding (zero line)
-  int s_dr[3], s_w[3], s_c[3];
+  int s_dr[NSL], s_w[NSL], s_c[NSL];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
+  for (int j = 0; j < NSL; ++j) {
     const int i = tid + j * kThreads;
     s_dr[j] = -2;
     s_w[j] = 0;
     s_c[j] = 0;
-    if (i < 512) {
+    if (i < NDY) {
       const int r = i >> 3;
       if (r < npx) {
         s_dr[j] = r / a.W;
@@ -817,7 +824,7 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wgrad_kernel(wg3::Args a) {
         s_c[j] = ((i & 7) ^ swz(r)) * 8;
       }
     } else if (i < npieces) {
-      const int r = (i - 512) >> 3, hr = r / W2;
+      const int r = (i - NDY) >> 3, hr = r / W2;
       s_dr[j] = hr - 1;
       s_w[j] = r - hr * W2 - 1;
       s_c[j] = ((i & 7) ^ swz(r)) * 8;
@@ -826,12 +833,12 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wgrad_kernel(wg3::Args a) {
   auto issue = [&](int ch, char* buf) {
     const int b = ch / a.cpi, h0 = (ch - b * a.cpi) * a.RC;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NSL; ++j) {
       const int i = tid + j * kThreads, hh = h0 + s_dr[j], ww = s_w[j];
       const bool ok = s_dr[j] != -2 && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
       const long long pix = (long long)(b * a.H + hh) * a.W + ww;
       const bf16_t* src = !ok ? (const bf16_t*)g_conv_zero
-                          : i < 512 ? a.dy + pix * a.Cout + co0 + s_c[j]
+                          : i < NDY ? a.dy + pix * a.Cout + co0 + s_c[j]
                                     : a.x + pix * a.Cin + ci0 + s_c[j];
       __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(buf + (j * kThreads + wv * 64) * 16), 16, 0, 0);
     }
@@ -850,14 +857,14 @@ __global__ __launch_bounds__(768, 1) void conv3x3_wgrad_kernel(wg3::Args a) {
   for (int t = 0; t < n; ++t) {
     // this chunk's three loads are in; the next chunk's may still be in flight
     if (t + 1 < n)
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSL) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every thread's slots landed; buffer (t+2)%3 was last read in step t-1
     if (t + 2 < n) issue(c_begin + t + 2, smem + ((t + 2) % 3) * kBuf);
     const char* buf = smem + (t % 3) * kBuf;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       TrPair af[2], bfr[3][2];
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm) af[fm] = frag(buf, kr[ks][0], kr[ks][1], co_s + 16 * fm, lane);
@@ -914,10 +921,22 @@ static int launch_conv3x3_wgrad(const GemmArgs& ga, hipStream_t st) {
   const int H = ga.cv_H, W = ga.cv_W, Cin = ga.cv_C, Cout = ga.M;
   if (Cin % 64 || Cout % 64 || W < 1 || W > 64 || H < 1 || ga.lda != Cout) return 1;
   const int B = ga.cv_npix / (H * W);
-  int RC = 64 / W;
+  // 128-pixel chunks (half the barriers and staging rounds per pixel) when whole rows fill at
+  // least 3/4 of them and the halo fits; else 64
+  static int kp_env = -1;  // RTDC_CONV3_KP=128: 128-pixel chunks where they fit (A/B; default 64)
+  if (kp_env < 0) {
+    const char* e = getenv("RTDC_CONV3_KP");
+    kp_env = (e && e[0] == '1') ? 128 : 64;
+  }
+  int KP = 128, RC = 128 / W;
   RC = RC < H ? RC : H;
+  if (kp_env == 64 || RC * W * 4 < 3 * 128 || (RC + 2) * (W + 2) > wg3::Cfg<128>::kMaxHalo) {
+    KP = 64;
+    RC = 64 / W;
+    RC = RC < H ? RC : H;
+  }
   const int halo = (RC + 2) * (W + 2);
-  if (halo > wg3::kMaxHalo || 512 + halo * 8 > 3 * wg3::kThreads) return 1;
+  if (KP == 64 && halo > wg3::Cfg<64>::kMaxHalo) return 1;
   wg3::Args a{};
   a.x = (const bf16_t*)ga.B;
   a.dy = (const bf16_t*)ga.A;
@@ -939,7 +958,10 @@ static int launch_conv3x3_wgrad(const GemmArgs& ga, hipStream_t st) {
   a.per = (a.nchunks + S - 1) / S;
   S = (a.nchunks + a.per - 1) / a.per;
   a.out = S > 1 ? ga.ws : (float*)ga.C;
-  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(tiles, S), dim3(wg3::kThreads), 0, st, a);
+  if (KP == 128)
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, dim3(tiles, S), dim3(wg3::kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, dim3(tiles, S), dim3(wg3::kThreads), 0, st, a);
   if (S > 1) {
     GemmArgs r = ga;
     r.N = 9 * Cin;
