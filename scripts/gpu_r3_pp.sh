@@ -5,7 +5,7 @@ set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_cnn_gpu.py -x -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/pp_tests.log 2>&1
+RTDC_CONV3_KP=128 timeout -k 10 400 python -u -m pytest tests/test_cnn_gpu.py -x -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/pp_tests.log 2>&1
 rc=$?; echo "TESTS EXIT $rc"; tail -n 15 gpurun_out/pp_tests.log
 [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
