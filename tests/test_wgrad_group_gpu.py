@@ -147,6 +147,31 @@ def test_deferred_colsums_bitwise_equal_immediate():
             assert torch.equal(a[n], b[n]), n
 
 
+def test_deferred_small_reductions_bitwise_equal_unflattened():
+    """A handful of partial rows (128 tokens: LayerNorm backward with few blocks): the deferred
+    reduction into a flat-buffer slot and the immediate one into a plain tensor sum in the same
+    order - a gradient's bits must not depend on where it is written (the 1-rank RCCL DDP test
+    compares exactly that)."""
+    from ray_torch_distributed_checkpoint_amd.optim import FlatParamSpace
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(11)
+    data = torch.randint(0, 1024, (2, 65), generator=g).to(dev)
+
+    def run(flat):
+        model = _mlp_model(dev, 2)
+        if flat:
+            FlatParamSpace(list(reversed(list(model.parameters())))).zero_grad(set_to_none=True)
+        model(data[:, :-1], data[:, 1:]).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.dim() == 1}
+
+    a, b = run(True), run(False)
+    assert a.keys() == b.keys() and len(a) >= 8
+    for n in a:
+        assert torch.equal(a[n], b[n]), n
+
+
 def test_colsum_multi_matches_sum():
     from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
 
