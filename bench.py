@@ -60,8 +60,9 @@ def main():
                     help="gradient all-reduce dtype (fp32 = torch DDP semantics)")
     ap.add_argument("--p2p-kb", type=float, default=0.0,
                     help="buckets <= this many KiB use the one-shot hipIpc all-reduce (0 = all on RCCL)")
-    ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
-                    help="1: ZeRO-1 (reduce-scatter gradients, sharded optimizer step, all-gather parameters)")
+    ap.add_argument("--zero", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: ZeRO-1 (reduce-scatter gradients, sharded optimizer step, all-gather parameters); "
+                         "-1 (default): ZeRO-1 for llama* at world > 1 (workloads.default_zero_stage), else 0")
     ap.add_argument("--overlap-opt", type=int, default=0, choices=[0, 1],
                     help="1: each bucket's fused optimizer update runs on a side stream as soon as its gradients "
                          "are final (optim/overlap.py; bitwise the plain step's result).  Off by default: measured "
@@ -118,6 +119,10 @@ def main():
         ndev = max(1, torch.cuda.device_count())
         torch.cuda.set_device(local % ndev)
         dev = torch.device("cuda", local % ndev)
+    if args.zero < 0:
+        from ray_torch_distributed_checkpoint_amd.workloads import default_zero_stage
+
+        args.zero = default_zero_stage(args.model, world)
     if dist_on:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -448,9 +453,18 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
             raise ValueError("--simulate-world runs in a single process")
         sim = (args.simulate_world, args.simulate_rank)
     share = sim[0] if sim else max(world, 1)  # this rank writes ~1/share of the state
+    # --simulate-world W --zero 1: the optimizer state of rank r's ZeRO-1 shard (owner chunks of
+    # the W-rank layout, no all-gather) instead of the replicated dedup plan
+    zsim = bool(sim) and args.zero == 1
 
     def state():
-        msd, osd = get_state_dict(model, opt)
+        if zsim:
+            from ray_torch_distributed_checkpoint_amd.checkpoint.sharded import simulated_zero_optimizer_state
+
+            msd = get_state_dict(model, None)[0]
+            osd = simulated_zero_optimizer_state(model, opt, sim[0], sim[1], args.bucket_mb)
+        else:
+            msd, osd = get_state_dict(model, opt)
         return {"model": msd, "optim": osd, "step": 1} if scope == "full" else {"model": msd, "step": 1}
 
     def nbytes_of(sd):
@@ -517,7 +531,8 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
         t3 = time.perf_counter()
         sd = state()
         dcp.load(sd, path2, simulate=sim)
-        set_state_dict(model, opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
+        # (simulated ZeRO shards are read in place into the optimizer's own state buffers)
+        set_state_dict(model, None if zsim else opt, model_state_dict=sd["model"], optim_state_dict=sd.get("optim"))
         sync()
         if dist.is_initialized():
             dist.barrier()
@@ -562,6 +577,8 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
         out["ckpt_simulated"] = {"world": sim[0], "rank": sim[1], "note": "per-rank shard of a W-rank plan, "
                                  "written and restored by one process; other ranks' shards not written"}
         out["ckpt_format"] = f"torch.distributed.checkpoint (.metadata + __{sim[1]}_0.distcp of {sim[0]}), native engine"
+        if zsim:
+            out["ckpt_simulated"]["layout"] = "ZeRO-1 owner shards (optimizer state), dedup plan (parameters)"
     return out
 
 

@@ -1,6 +1,6 @@
 """LayerNorm forward at the GPT-2 shape (16384 x 768, bf16): the native row kernel vs ATen's,
 plus the HBM bandwidth it reaches (the backward is timed inside the model profile:
-scripts/gpu_prof_gpt2.sh).  python benchmarks/norm_bench.py"""
+scripts/gpu.sh prof).  python benchmarks/norm_bench.py"""
 from __future__ import annotations
 
 import json

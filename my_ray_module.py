@@ -174,6 +174,11 @@ def train_func_per_worker(config: Dict):
                     captured = CapturedStep(graph_step, warmup=0)
                 with phase("step"):
                     captured.replay()
+                if world > 1 and model.p2p.error():
+                    # no host code runs inside a replay: the poisoned step's update was skipped on
+                    # the device (kernels/optim.hip comm_poisoned); fail the attempt here
+                    raise RuntimeError("P2P all-reduce timed out waiting for a peer rank during a captured step "
+                                       "(gradients poisoned with NaN, update skipped)")
                 continue
             # before a capture, run the eager steps on a side stream (as CapturedStep's warm-up
             # does): autograd's AccumulateGrad nodes must not belong to the default stream

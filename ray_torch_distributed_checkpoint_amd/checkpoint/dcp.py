@@ -230,19 +230,20 @@ def write_metadata(checkpoint_id: str, md: Metadata):
     fsync_dir(checkpoint_id)
 
 
+SIMULATED_TAG = "rtdc:simulated"  # StorageMeta.modules marker of a simulated (one-rank) save
+
+
 def _simulated(simulate):
     """(world, rank) this process plays in a SIMULATED multi-rank save/load, or None.
-    `simulate=(W, r)` or env RTDC_DCP_SIMULATE="W:r": plan exactly as rank r of a W-rank
-    data-parallel job (owner plan, file layout, `.metadata` for all W ranks) but write / read
-    only rank r's share, with no collectives - how one GPU measures a per-rank shard of an
-    8-GPU job (e.g. Llama-3-8B's ~12 GB train-state shard).  The result on disk is one rank's
-    file plus the full metadata: a measurement artifact, not a restorable checkpoint."""
+    `simulate=(W, r)`: plan exactly as rank r of a W-rank data-parallel job (owner plan, file
+    layout, `.metadata` for all W ranks) but write / read only rank r's share, with no
+    collectives - how one GPU measures a per-rank shard of an 8-GPU job (e.g. Llama-3-8B's
+    ~12 GB train-state shard).  The result on disk is one rank's file plus the full metadata: a
+    measurement artifact, not a restorable checkpoint, so its metadata carries SIMULATED_TAG
+    and a non-simulated load refuses it.  Only the explicit argument enables this (an
+    environment switch could silently turn a trainer's real checkpoints into artifacts)."""
     if simulate is None:
-        env = os.environ.get("RTDC_DCP_SIMULATE")
-        if not env:
-            return None
-        w, _, r = env.partition(":")
-        simulate = (int(w), int(r or 0))
+        return None
     w, r = int(simulate[0]), int(simulate[1])
     if not (0 <= r < w):
         raise ValueError(f"simulate=({w}, {r}): rank out of range")
@@ -251,11 +252,48 @@ def _simulated(simulate):
     return w, r
 
 
+def _merge_rank_metadata(metadata: Metadata, parts: list) -> None:
+    """Fold the other ranks' metadata of a non-replicated save into rank 0's.  A key present on
+    several ranks (a FlatShardedTensor: one TensorStorageMetadata per rank, each listing that
+    rank's chunks) gets the union of their chunk lists, and its storage entries are re-indexed
+    to the merged list - a plain dict.update would keep only the last rank's chunks while the
+    storage entries of every rank survive, and a load would then miss chunk sizes."""
+    sd_md, storage = metadata.state_dict_metadata, metadata.storage_data
+    for p in parts:
+        for fqn, m in p.state_dict_metadata.items():
+            mine = sd_md.get(fqn)
+            if mine is None:
+                sd_md[fqn] = m
+                remap = {i: i for i in range(len(getattr(m, "chunks", []) or []))}
+            elif isinstance(m, TensorStorageMetadata) and isinstance(mine, TensorStorageMetadata):
+                if tuple(mine.size) != tuple(m.size):
+                    raise ValueError(f"{fqn}: ranks disagree on the global shape ({tuple(mine.size)} vs {tuple(m.size)})")
+                remap = {}
+                for i, c in enumerate(m.chunks):
+                    remap[i] = len(mine.chunks)
+                    mine.chunks.append(c)
+            else:
+                raise ValueError(f"{fqn}: saved by several ranks with replicated=False but is not a sharded tensor")
+            for idx, info in p.storage_data.items():
+                if idx.fqn != fqn:
+                    continue
+                i = remap.get(idx.index, idx.index) if idx.index is not None else None
+                storage[MetadataIndex(fqn, idx.offset, i)] = info
+        for idx, info in p.storage_data.items():
+            if idx.fqn not in p.state_dict_metadata:
+                storage[idx] = info
+        metadata.planner_data.update(p.planner_data)
+
+
 def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsync: bool = True,
                crc: bool = True, replicated: bool = True, simulate=None) -> AsyncSave:
     """Start a sharded save; returns once the HBM snapshot is enqueued (non-blocking).
     `simulate=(W, r)`: see `_simulated`."""
     t0 = time.perf_counter()
+    from ..parallel import health
+
+    # a timed-out P2P collective left NaN gradients behind: never snapshot that state
+    health.assert_healthy("checkpoint save")
     sim = _simulated(simulate)
     world, rank = sim if sim else _world(process_group)
     os.makedirs(checkpoint_id, exist_ok=True)
@@ -310,17 +348,15 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
                     sd_md[it.fqn] = BytesStorageMetadata()
                     storage[MetadataIndex(it.fqn)] = _StorageInfo(fname, base, size)
         metadata = Metadata(state_dict_metadata=sd_md, planner_data=mapping, storage_data=storage,
-                            storage_meta=StorageMeta(checkpoint_id=checkpoint_id, save_id=str(uuid.uuid4())),
+                            storage_meta=StorageMeta(checkpoint_id=checkpoint_id, save_id=str(uuid.uuid4()),
+                                                     modules=[SIMULATED_TAG] if sim else []),
                             version=DCP_VERSION)
         if not replicated and world > 1 and not sim:
             # gather per-rank metadata on rank 0 (CPU object collective)
             parts = [None] * world
             dist.all_gather_object(parts, metadata, group=process_group)
             if rank == 0:
-                for p in parts[1:]:
-                    metadata.state_dict_metadata.update(p.state_dict_metadata)
-                    metadata.storage_data.update(p.storage_data)
-                    metadata.planner_data.update(p.planner_data)
+                _merge_rank_metadata(metadata, parts[1:])
             else:
                 metadata = None
     elif not replicated and world > 1:
@@ -461,6 +497,15 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
     sim = _simulated(simulate)
     world, rank = sim if sim else _world(process_group)
     md = read_metadata(checkpoint_id)
+    sm = getattr(md, "storage_meta", None)
+    if not sim and sm is not None and SIMULATED_TAG in (getattr(sm, "modules", None) or []):
+        # a simulated save writes one rank's file: restorable only once every rank's file exists
+        missing_files = sorted({i.relative_path for i in md.storage_data.values()
+                                if not os.path.exists(os.path.join(checkpoint_id, i.relative_path))})
+        if missing_files:
+            raise ValueError(f"{checkpoint_id} is a simulated one-rank measurement artifact (saved with simulate=...): "
+                             f"{len(missing_files)} rank file(s) such as {missing_files[0]} were never written, so it "
+                             "cannot be restored")
     resolved = _resolve_stateful(state_dict)
     flat, mapping = flatten_state_dict(resolved)
     ext = _ext.ext()

@@ -214,7 +214,11 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
 
     async_=False: returns after the file is durable.  async_=True: takes an HBM/host snapshot
     (so the caller may keep mutating the tensors) and returns a SaveHandle immediately.
+    Refuses (parallel/health.py CommPoisonedError) after a timed-out P2P gradient collective.
     """
+    from ..parallel import health
+
+    health.assert_healthy("checkpoint save")
     pkl, tensors = pickle_state(obj)
     if snapshot is None:
         snapshot = async_

@@ -41,10 +41,10 @@ int rtdc_xent(const void* logits, void* dlogits, const int64_t* target, float* l
               hipStream_t st);
 int rtdc_adamw(const void* chunks, int nchunks, float* p, const float* g, float* m, float* v, void* shadow,
                float lr, float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt,
-               float grad_scale, hipStream_t st);
+               float grad_scale, const int* skip, hipStream_t st);
 int rtdc_sgd(const void* chunks, int nchunks, float* p, const float* g, float* buf, void* shadow, float lr,
              float momentum, float dampening, float wd, int nesterov, int first, float grad_scale,
-             hipStream_t st);
+             const int* skip, hipStream_t st);
 int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st);
 int rtdc_f32_to_bf16_t(const float* x, void* y, int R, int C, hipStream_t st);
 int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float* partial, hipStream_t st);
@@ -57,6 +57,7 @@ int rtdc_sort_ids(const int64_t* ids, int n, int nbits, uint32_t* ws, int64_t* s
                   hipStream_t st);
 int rtdc_synth_tokens(const int64_t* ids, int B, int T, long long vocab, unsigned long long seed_add, int64_t* inp,
                       int64_t* tgt, hipStream_t st);
+int rtdc_fill_f32(float* x, long long n, float v, hipStream_t st);
 int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const void* dout, float* dwte, float* dwpe, int B, int T,
                    int D, int accumulate_wpe, int accumulate_wte, hipStream_t st);
 int rtdc_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
@@ -367,20 +368,21 @@ static void check_chunks(const Tensor& chunks, int64_t nchunks, const char* op) 
 }
 static void adamw(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, Tensor m, Tensor v,
                   c10::optional<Tensor> shadow, double lr, double b1, double b2, double eps, double wd, double bc1,
-                  double bc2_sqrt, double grad_scale) {
+                  double bc2_sqrt, double grad_scale, int64_t skip_ptr) {
   check_chunks(chunks, nchunks, "adamw");
   check_rc(rtdc_adamw(chunks.data_ptr(), (int)nchunks, p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                       v.data_ptr<float>(), ptr_or_null(shadow), (float)lr, (float)b1, (float)b2, (float)eps,
-                      (float)wd, (float)bc1, (float)bc2_sqrt, (float)grad_scale, cur_stream()),
+                      (float)wd, (float)bc1, (float)bc2_sqrt, (float)grad_scale, (const int*)(uintptr_t)skip_ptr,
+                      cur_stream()),
            "adamw");
 }
 static void sgd(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, c10::optional<Tensor> buf,
                 c10::optional<Tensor> shadow, double lr, double momentum, double dampening, double wd,
-                bool nesterov, bool first, double grad_scale) {
+                bool nesterov, bool first, double grad_scale, int64_t skip_ptr) {
   check_chunks(chunks, nchunks, "sgd");
   check_rc(rtdc_sgd(chunks.data_ptr(), (int)nchunks, p.data_ptr<float>(), g.data_ptr<float>(),
                     (float*)ptr_or_null(buf), ptr_or_null(shadow), (float)lr, (float)momentum, (float)dampening,
-                    (float)wd, nesterov, first, (float)grad_scale, cur_stream()),
+                    (float)wd, nesterov, first, (float)grad_scale, (const int*)(uintptr_t)skip_ptr, cur_stream()),
            "sgd");
 }
 static void f32_to_bf16(Tensor x, Tensor y) {
@@ -445,6 +447,12 @@ static void synth_tokens(Tensor ids, Tensor inp, Tensor tgt, int64_t vocab, int6
            "synth_tokens");
 }
 // sidx / perm: stably sorted token ids and their original positions (deterministic backward)
+static void fill_f32(Tensor x, double v) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "fill_f32: contiguous fp32 CUDA tensor");
+  if (x.numel() == 0) return;
+  TORCH_CHECK(((uintptr_t)x.data_ptr() & 15) == 0, "fill_f32: 16-B aligned tensor");
+  check_rc(rtdc_fill_f32(x.data_ptr<float>(), (long long)x.numel(), (float)v, cur_stream()), "fill_f32");
+}
 static void embed_bwd(Tensor sidx, Tensor perm, Tensor dout, Tensor dwte, c10::optional<Tensor> dwpe, int64_t B,
                       int64_t T, bool accumulate_wpe, bool accumulate_wte) {
   const int D = (int)dwte.size(1);
@@ -929,6 +937,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("open", &rtdc_p2p::P2PComm::open)
       .def("allreduce_", &rtdc_p2p::P2PComm::allreduce_, py::arg("tensor"), py::arg("average") = true)
       .def("error", &rtdc_p2p::P2PComm::error)
+      .def("error_ptr", &rtdc_p2p::P2PComm::error_ptr)
       .def("capacity", &rtdc_p2p::P2PComm::capacity)
       .def("epoch", &rtdc_p2p::P2PComm::epoch)
       .def_property_readonly("world", &rtdc_p2p::P2PComm::world)
@@ -946,8 +955,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum_multi", &colsum_multi);
   m.def("colsum", &colsum);
   m.def("xent", &xent);
-  m.def("adamw", &adamw);
-  m.def("sgd", &sgd);
+  m.def("adamw", &adamw, py::arg("chunks"), py::arg("nchunks"), py::arg("p"), py::arg("g"), py::arg("m"),
+        py::arg("v"), py::arg("shadow"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
+        py::arg("bc1"), py::arg("bc2_sqrt"), py::arg("grad_scale"), py::arg("skip_ptr") = 0);
+  m.def("sgd", &sgd, py::arg("chunks"), py::arg("nchunks"), py::arg("p"), py::arg("g"), py::arg("buf"),
+        py::arg("shadow"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"),
+        py::arg("nesterov"), py::arg("first"), py::arg("grad_scale"), py::arg("skip_ptr") = 0);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("f32_to_bf16_t", &f32_to_bf16_t);
   m.def("sumsq", &sumsq);
@@ -956,6 +969,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("sort_ids", &sort_ids);
   m.def("synth_tokens", &synth_tokens);
+  m.def("fill_f32", &fill_f32, py::arg("x"), py::arg("value") = 0.0);
   m.def("embed_bwd", &embed_bwd, py::arg("sidx"), py::arg("perm"), py::arg("dout"), py::arg("dwte"), py::arg("dwpe"),
         py::arg("B"), py::arg("T"), py::arg("accumulate_wpe"), py::arg("accumulate_wte") = false);
   m.def("dropout", &dropout);

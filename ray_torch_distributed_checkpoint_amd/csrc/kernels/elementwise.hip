@@ -74,6 +74,15 @@ __global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __res
   }
 }
 
+// x[0, n) = v with 16-B stores (the embedding-gradient reset: a 2.1 GB fp32 table per Llama-3-8B
+// step, which ATen's FillFunctor did before; grid-stride, ~2 blocks per CU keep HBM busy)
+__global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ x, long long n, float v) {
+  const long long n4 = n >> 2;
+  const float4 q = make_float4(v, v, v, v);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) ((float4*)x)[i] = q;
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) x[(n4 << 2) + threadIdx.x] = v;
+}
+
 // dwpe[p, d] (+)= sum_b dout[b*T + p, d]   deterministic (fixed b order)
 __global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const bf16_t* __restrict__ dout, float* __restrict__ dwpe,
                                                            int B, int T, int D, int accumulate) {
@@ -177,6 +186,15 @@ extern "C" int rtdc_embed_bwd(const int64_t* sidx, const int64_t* perm, const vo
   if (dwpe)
     hipLaunchKernelGGL(embed_bwd_wpe_kernel, dim3(T, (D + 255) / 256), dim3(256), 0, st, (const bf16_t*)dout,
                        dwpe, B, T, D, accumulate_wpe);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_fill_f32(float* x, long long n, float v, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)x & 15) != 0) return 1;
+  long long blocks = (n / 4 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, v);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

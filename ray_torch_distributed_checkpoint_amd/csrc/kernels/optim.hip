@@ -14,9 +14,19 @@
 // state buffers hold only this rank's owned shards back to back (1/world of the bytes), so
 // `sstart` is the chunk's position in that compact buffer.
 // Semantics follow torch.optim.AdamW / SGD (decoupled weight decay; SGD first-step clone).
+//
+// `skip` (optional): a communicator health word (the one-shot P2P all-reduce's host-coherent
+// error flag, csrc/runtime/p2p_comm.cpp).  When a gradient collective earlier on this stream
+// timed out it poisoned its bucket with NaN and set the word; the update then becomes a no-op,
+// so a NaN gradient can never reach the parameters or the optimizer state - also inside a
+// replayed hipGraph, where no host code runs between the collective and the step.
 #include "common.h"
 
 namespace rtdc {
+
+__device__ __forceinline__ bool comm_poisoned(const int* skip) {
+  return skip != nullptr && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
 
 struct Chunk {
   long long start;   // offset into p / g / shadow
@@ -31,7 +41,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(const Chunk* __restrict__ ch
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ shadow, float lr, float b1,
                                                    float b2, float eps, float wd, float bc1,
-                                                   float bc2_sqrt, float grad_scale) {
+                                                   float bc2_sqrt, float grad_scale, const int* skip) {
+  if (comm_poisoned(skip)) return;
   const float step_size = lr / bc1;
   for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const Chunk c = chunks[ci];
@@ -78,7 +89,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(const Chunk* __restrict__ chun
                                                  float* __restrict__ p, const float* __restrict__ g,
                                                  float* __restrict__ buf, bf16_t* __restrict__ shadow,
                                                  float lr, float momentum, float dampening, float wd,
-                                                 int nesterov, int first, float grad_scale) {
+                                                 int nesterov, int first, float grad_scale, const int* skip) {
+  if (comm_poisoned(skip)) return;
   for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const Chunk c = chunks[ci];
     const float w = c.decay ? wd : 0.f;
@@ -216,20 +228,20 @@ static inline int grid_for(int nchunks) { return nchunks < 4096 ? nchunks : 4096
 
 extern "C" int rtdc_adamw(const void* chunks, int nchunks, float* p, const float* g, float* m,
                           float* v, void* shadow, float lr, float b1, float b2, float eps, float wd,
-                          float bc1, float bc2_sqrt, float grad_scale, hipStream_t st) {
+                          float bc1, float bc2_sqrt, float grad_scale, const int* skip, hipStream_t st) {
   if (nchunks <= 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
-                     nchunks, p, g, m, v, (bf16_t*)shadow, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale);
+                     nchunks, p, g, m, v, (bf16_t*)shadow, lr, b1, b2, eps, wd, bc1, bc2_sqrt, grad_scale, skip);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 extern "C" int rtdc_sgd(const void* chunks, int nchunks, float* p, const float* g, float* buf,
                         void* shadow, float lr, float momentum, float dampening, float wd,
-                        int nesterov, int first, float grad_scale, hipStream_t st) {
+                        int nesterov, int first, float grad_scale, const int* skip, hipStream_t st) {
   if (nchunks <= 0) return 0;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
                      nchunks, p, g, buf, (bf16_t*)shadow, lr, momentum, dampening, wd, nesterov, first,
-                     grad_scale);
+                     grad_scale, skip);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

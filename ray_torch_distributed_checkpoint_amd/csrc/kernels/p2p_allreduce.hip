@@ -21,6 +21,12 @@
 // The wait is BOUNDED (wall_clock64, 100 MHz): on timeout the kernel records an error in a
 // host-visible word, fills the bucket with NaN (never a silently un-reduced gradient) and
 // exits, so a missing peer can never leave waves spinning on the GPU.
+// The error is STICKY: once set, later calls on this rank neither stage nor publish - they
+// NaN-fill their bucket at once.  Restaging would break the reuse argument above (a rank that
+// timed out in call e+1 never passed its wait, so a late peer may still be reading call e's
+// slot of the parity that call e+2 would overwrite), and publishing would let a late peer
+// reduce against a rank that no longer participates.  A late peer therefore completes at most
+// the calls this rank published before its timeout, then times out itself on the next one.
 #include "common.h"
 
 namespace rtdc {
@@ -39,8 +45,13 @@ __device__ __forceinline__ unsigned load_flag(const unsigned* p) {
 }
 
 // T: float or bf16_t.  n elements (n * sizeof(T) a multiple of 16), 16-B vectors.
+__device__ __forceinline__ int sticky_error(const int* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void stage_kernel(const unsigned* __restrict__ epoch_dev, char* own, long long cap,
-                                                   const uint4* __restrict__ src, long long nv) {
+                                                   const uint4* __restrict__ src, long long nv, const int* err) {
+  if (sticky_error(err)) return;  // a timed-out rank never restages (see the header)
   const unsigned epoch = *epoch_dev + 1u;
   uint4* dst = (uint4*)(own + FLAG_BYTES + (long long)(epoch & 1u) * cap);
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) dst[i] = src[i];
@@ -57,9 +68,10 @@ __global__ __launch_bounds__(256) void oneshot_kernel(Peers peers, int world, in
   __shared__ int bad;
   const unsigned epoch = *epoch_dev + 1u;  // advanced by advance_kernel after this call
   if (threadIdx.x == 0) {
+    // sticky: after a timeout this rank neither publishes nor waits (see the header)
+    int timed_out = sticky_error(err);
     unsigned* mine = (unsigned*)peers.base[rank];
-    if (blockIdx.x == 0) __hip_atomic_store(mine, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    int timed_out = 0;
+    if (blockIdx.x == 0 && !timed_out) __hip_atomic_store(mine, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     const long long t0 = wall_clock64();
     for (int r = 0; r < world && !timed_out; ++r) {
       const unsigned* f = (const unsigned*)peers.base[r];
@@ -136,7 +148,7 @@ extern "C" int rtdc_p2p_oneshot(const void* const* bases, int world, int rank, u
   for (int r = 0; r < world; ++r) peers.base[r] = (const char*)bases[r];
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(p2p::stage_kernel, dim3(blocks), dim3(256), 0, st, (const unsigned*)epoch_dev,
-                     (char*)bases[rank], cap, (const uint4*)data, bytes / 16);
+                     (char*)bases[rank], cap, (const uint4*)data, bytes / 16, (const int*)err);
   if (is_bf16)
     hipLaunchKernelGGL(p2p::oneshot_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, peers, world, rank,
                        (const unsigned*)epoch_dev, cap, (bf16_t*)data, n, scale, err, timeout_ticks);

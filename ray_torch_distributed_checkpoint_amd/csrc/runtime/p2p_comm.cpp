@@ -92,6 +92,9 @@ class P2PComm {
   }
 
   int error() const { return *err_; }
+  // device-readable address of the error word (host-coherent): the fused optimizer kernels
+  // skip their update when it is set (kernels/optim.hip comm_poisoned)
+  int64_t error_ptr() const { return (int64_t)(uintptr_t)err_; }
   long long capacity() const { return cap_; }
   int world() const { return world_; }
   int rank() const { return rank_; }

@@ -78,6 +78,14 @@ def launch_pending_sorts() -> None:
         _pending.pop().launch()
 
 
+def _zero(ext, t: torch.Tensor) -> None:
+    """Native zero fill (kernels/elementwise.hip fill_f32_kernel) of a contiguous fp32 slice."""
+    if t.is_contiguous() and t.data_ptr() % 16 == 0:
+        ext.fill_f32(t, 0.0)
+    else:
+        t.zero_()
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, wte, wpe, presort=True):
@@ -113,15 +121,18 @@ class _Embedding(torch.autograd.Function):
             # tied table (GPT-2 LM head): add into the gradient the LM head already wrote
             dwte = claimed_target(wte)
             accumulate = dwte is not None
-        dwte = torch.zeros(wte_shape, dtype=torch.float32, device=idx.device) if dwte is None else \
-            (dwte if accumulate else dwte.zero_())
+        ext = gpu_ext()
+        if dwte is None:
+            dwte = torch.empty(wte_shape, dtype=torch.float32, device=idx.device)
+        if not accumulate:
+            _zero(ext, dwte)  # rows no token uses (the kernel writes only the used ones)
         dwpe = None
         if wpe_shape is not None:
             dwpe = grad_target(wpe)
             if dwpe is None:
-                dwpe = torch.zeros(wpe_shape, dtype=torch.float32, device=idx.device)
-            elif T < wpe_shape[0]:
-                dwpe[T:].zero_()  # the kernel writes (not adds) positions [0, T)
+                dwpe = torch.empty(wpe_shape, dtype=torch.float32, device=idx.device)
+            if T < wpe_shape[0]:
+                _zero(ext, dwpe[T:])  # the kernel writes (not adds) positions [0, T)
         if ctx.sorted is not None:
             if ctx.sorted in _pending:
                 _pending.remove(ctx.sorted)
@@ -130,7 +141,7 @@ class _Embedding(torch.autograd.Function):
                 torch.cuda.current_stream(idx.device).wait_event(done)
         else:
             sidx, perm = sort_ids(idx.reshape(-1), wte_shape[0])
-        gpu_ext().embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)
+        ext.embed_bwd(sidx, perm, dout.contiguous(), dwte, dwpe, B, T, False, accumulate)
         return None, (None if accumulate else dwte), dwpe, None
 
 

@@ -258,6 +258,10 @@ class _WgradGroup:
         items, self.items, self.tiles = self.items, [], 0
         jobs, self.jobs = self.jobs, []
         waiters, self.waiters = self.waiters, []
+        if join:
+            # a backward that raised never ran its queued _end_of_backward: re-arm on the next
+            # deferral instead of trusting a stale flag (a spare callback only flushes nothing)
+            self.cb_queued = False
         dev_t = items[0][0] if items else (jobs[0][0] if jobs else None)
         if (dev_t is not None and _GROUP_SIDE and not join and dev_t.is_cuda
                 and not torch.cuda.is_current_stream_capturing()):

@@ -9,6 +9,12 @@ memset of the buffer per step, and the DDP buckets / fused optimizer find the gr
 place.  A second contribution in the same step (tied weights) gets a fresh tensor and is
 added by autograd as usual; anything that ends up outside the buffer is folded back by the
 DDP hook / `FlatParamSpace.ensure_grad_views`.
+
+A first contribution may be a DEFERRED weight gradient (ops/gemm.py `_WgradGroup`): its slice
+is written only at the next flush, and the write overwrites.  Whenever a second contribution
+of the same step is about to read or add to that slice (a weight shared by two linears, whose
+second gradient autograd adds out of place; a linear head tied to an embedding, whose
+backward adds in place through `claimed_target`), the pending products are flushed first.
 """
 from __future__ import annotations
 
@@ -23,9 +29,19 @@ def grad_target(p: torch.Tensor | None) -> torch.Tensor | None:
     if sp is None or sp.grad is None or not sp.fresh or p.grad is not None:
         return None
     if getattr(p, "_rtdc_claim", -1) == sp.step_id:
-        return None  # already handed out this step (second use of a tied weight)
+        # already handed out this step (second use of a tied weight): autograd will add this
+        # contribution to the slice - which must hold the first one by then
+        _flush_if_pending(sp.grad_view(p))
+        return None
     p._rtdc_claim = sp.step_id
     return sp.grad_view(p)
+
+
+def _flush_if_pending(view: torch.Tensor) -> None:
+    from .gemm import _WG, flush_wgrads
+
+    if _WG.pending(view):
+        flush_wgrads()
 
 
 def claimed_target(p: torch.Tensor | None) -> torch.Tensor | None:
@@ -41,4 +57,6 @@ def claimed_target(p: torch.Tensor | None) -> torch.Tensor | None:
         return None
     if getattr(p, "_rtdc_claim", -1) != sp.step_id:
         return None
-    return sp.grad_view(p)
+    view = sp.grad_view(p)
+    _flush_if_pending(view)  # the in-place add must land on the first use's written gradient
+    return view

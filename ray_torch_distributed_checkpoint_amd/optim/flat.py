@@ -146,6 +146,9 @@ class FlatParamSpace:
             self.shadow = torch.empty(off, dtype=shadow_dtype, device=self.device)
             self.refresh_shadows()
         self.grad_scale = 1.0
+        # device address of a communicator error word (0: none); the fused optimizer kernels
+        # skip their update when it is set (parallel/health.py)
+        self.skip_ptr = 0
         self.zero: ZeroLayout | None = None
         self._offsets = None
         self._chunk_cache: dict = {}

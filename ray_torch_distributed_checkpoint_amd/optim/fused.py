@@ -366,7 +366,7 @@ class FusedAdamW(_FlatOptimizer):
             def fn(chunks, n, group=group, b1=b1, b2=b2, wd=wd, step=step):
                 ext.adamw(chunks, n, sp.data, sp.grad, self._bufs["exp_avg"], self._bufs["exp_avg_sq"],
                           sp.shadow, group["lr"], b1, b2, group["eps"], wd, 1 - b1 ** step,
-                          math.sqrt(1 - b2 ** step), sp.grad_scale)
+                          math.sqrt(1 - b2 ** step), sp.grad_scale, sp.skip_ptr)
 
             out.append((sub, [wd != 0.0] * len(sub), fn))
         return out
@@ -479,7 +479,7 @@ class FusedSGD(_FlatOptimizer):
             def fn(chunks, n, group=group, mom=mom, wd=wd, first=first):
                 ext.sgd(chunks, n, sp.data, sp.grad, self._bufs["momentum_buffer"] if mom != 0.0 else None,
                         sp.shadow, group["lr"], mom, group["dampening"], wd, group["nesterov"], first,
-                        sp.grad_scale)
+                        sp.grad_scale, sp.skip_ptr)
 
             out.append((sub, [wd != 0.0] * len(sub), fn))
         return out

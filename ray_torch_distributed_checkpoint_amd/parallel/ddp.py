@@ -267,6 +267,9 @@ class DistributedDataParallel(nn.Module):
                                 timeout_s=self._p2p_timeout_s)
         self.p2p_max_bytes = int(max_kb * 1024)
         self._engine.set_p2p(self.p2p.comm, self.p2p_max_bytes)
+        # a timed-out bucket is NaN-filled on the device: the fused optimizer kernels read the
+        # error word and skip the update, so no NaN ever reaches a parameter (parallel/health.py)
+        self.space.skip_ptr = self.p2p.error_ptr()
 
     def comm_plan(self) -> dict:
         """Self-description of the gradient all-reduce (what a multi-GPU bench reports)."""

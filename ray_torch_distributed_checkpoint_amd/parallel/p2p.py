@@ -35,6 +35,9 @@ class P2PAllReduce:
         dist.all_gather_object(handles, bytes(self.comm.handle()), group=group)
         self.comm.open(handles)
         self.device = dev
+        from . import health
+
+        health.register(self)  # checkpoints refuse to snapshot after a timeout (parallel/health.py)
 
     @property
     def capacity(self) -> int:
@@ -48,3 +51,7 @@ class P2PAllReduce:
 
     def error(self) -> int:
         return self.comm.error()
+
+    def error_ptr(self) -> int:
+        """Device-readable address of the error word (the fused optimizers' `skip_ptr`)."""
+        return self.comm.error_ptr()

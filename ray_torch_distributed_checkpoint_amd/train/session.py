@@ -193,6 +193,11 @@ class _Session:
     def report(self, metrics: dict, checkpoint: Checkpoint | None = None):
         if self._commit_err:
             raise self._commit_err
+        from ..parallel import health
+
+        # a rank whose gradient collective timed out (NaN-poisoned, update skipped) fails here,
+        # before the commit barrier: the attempt dies and nothing of this report is committed
+        health.assert_healthy("report")
         rank = self.ctx.world_rank
         n = self.n_reports
         key = f"s{self.ctx.attempt}/r{n}"

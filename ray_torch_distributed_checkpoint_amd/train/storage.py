@@ -20,6 +20,7 @@ import json
 import math
 import os
 import random
+import re
 import shutil
 import string
 import time
@@ -147,6 +148,9 @@ def latest_committed(trial_dir: str) -> str | None:
     return c[-1][1] if c else None
 
 
+REGISTRY_FN = ".checkpoints.json"
+
+
 class TrialLogger:
     """result.json (JSON lines) + progress.csv + checkpoint registry with retention (rank 0)."""
 
@@ -159,10 +163,17 @@ class TrialLogger:
         self.iteration = 0
         self.kept: list[tuple[int, str, dict]] = []  # (index, path, metrics)
         self._csv_fields = None
-        reg = os.path.join(trial_dir, ".checkpoints.json")
+        reg = os.path.join(trial_dir, REGISTRY_FN)
         if os.path.exists(reg):
-            with open(reg) as f:
-                self.kept = [tuple(x) for x in json.load(f)]
+            try:
+                with open(reg) as f:
+                    self.kept = [tuple(x) for x in json.load(f)]
+            except (ValueError, TypeError, OSError):
+                # unreadable registry (a crash of an older writer, a damaged disk): rebuild it
+                # from the committed checkpoint directories - the directories, not the registry,
+                # are the commit record (storage.commit renames them into place atomically)
+                self.kept = self._scan_committed()
+                self._write_registry()
             self.iteration = max([m.get("training_iteration", 0) for _, _, m in self.kept] + [0])
 
     def log(self, metrics: dict, checkpoint_index: int | None) -> dict:
@@ -219,9 +230,40 @@ class TrialLogger:
                     shutil.rmtree(k[1], ignore_errors=True)
                     deleted.append(k[1])
             self.kept = sorted(keep, key=lambda x: x[0])
-        with open(os.path.join(self.trial_dir, ".checkpoints.json"), "w") as f:
-            json.dump([list(k) for k in self.kept], f, default=str)
+        self._write_registry()
         return deleted
+
+    def _write_registry(self) -> None:
+        """tmp + fsync + rename: a crash leaves the old or the new registry, never a torn one."""
+        reg = os.path.join(self.trial_dir, REGISTRY_FN)
+        tmp = f"{reg}.tmp.{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump([list(k) for k in self.kept], f, default=str)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, reg)
+        fsync_dir(self.trial_dir)
+
+    def _scan_committed(self) -> list:
+        """(index, path, metrics) of every committed checkpoint directory, metrics from result.json."""
+        rows = {}
+        try:
+            with open(os.path.join(self.trial_dir, "result.json")) as f:
+                for line in f:
+                    try:
+                        r = json.loads(line)
+                    except ValueError:
+                        continue  # a torn last line
+                    if r.get("checkpoint_dir_name"):
+                        rows[r["checkpoint_dir_name"]] = r
+        except OSError:
+            pass
+        out = []
+        for name in sorted(os.listdir(self.trial_dir)):
+            m = re.fullmatch(r"checkpoint_(\d{6})", name)
+            if m and os.path.isdir(os.path.join(self.trial_dir, name)):
+                out.append((int(m.group(1)), os.path.join(self.trial_dir, name), rows.get(name, {})))
+        return out
 
     def best_checkpoints(self):
         return list(self.kept)

@@ -177,3 +177,39 @@ def test_zero1_checkpoint_model_part_loads_with_stock_torch_dcp(tmp_path):
     md = tdcp.FileSystemReader(path).read_metadata()
     m = md.state_dict_metadata["optim.state.a.weight.exp_avg"]
     assert tuple(m.size) == (129, 37) and len(m.chunks) >= 2
+
+
+def _per_rank_sharded_save(rank, world, path):
+    """replicated=False: every rank writes its own items; one key is a FlatShardedTensor whose
+    chunks are spread over both ranks, another a per-rank tensor with a rank-unique name."""
+    import torch
+
+    from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
+    from ray_torch_distributed_checkpoint_amd.checkpoint.sharded import FlatShardedTensor
+
+    full = torch.arange(6 * 10, dtype=torch.float32).view(6, 10)
+    ranges = [[(0, 25)], [(25, 60)]]
+    flat = full.reshape(-1)
+    local = [(a, flat[a:b].clone()) for a, b in ranges[rank]]
+    sd = {"w": FlatShardedTensor((6, 10), torch.float32, local, ranges, rank),
+          f"own_{rank}": torch.full((3,), float(rank))}
+    dcp.save(sd, path, replicated=False)
+    return True
+
+
+def test_per_rank_metadata_merge_keeps_every_ranks_chunks(tmp_path):
+    """Rank 0 merges the per-rank metadata of a replicated=False save: a key sharded over both
+    ranks keeps the union of their chunk lists (dict.update kept only the last rank's)."""
+    import torch
+
+    from tests.mp_util import run
+    from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
+
+    path = str(tmp_path / "ck")
+    run(_per_rank_sharded_save, 2, path)
+    md = dcp.read_metadata(path)
+    assert len(md.state_dict_metadata["w"].chunks) >= 2
+    sd = {"w": torch.zeros(6, 10), "own_0": torch.zeros(3), "own_1": torch.zeros(3)}
+    dcp.load(sd, path)
+    assert torch.equal(sd["w"], torch.arange(60, dtype=torch.float32).view(6, 10))
+    assert torch.equal(sd["own_1"], torch.ones(3)) and torch.equal(sd["own_0"], torch.zeros(3))

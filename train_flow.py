@@ -48,7 +48,12 @@ class RayTorchTrain(FlowSpec):
     report_every_n_steps = Parameter("report_every_n_steps", default=0,
                                      help="metrics rows between checkpoints (0: one row per checkpoint)")
     grad_comm_dtype = Parameter("grad_comm_dtype", default="fp32", help="fp32 | bf16 gradient all-reduce")
-    zero_stage = Parameter("zero_stage", default=0, help="1: ZeRO-1 sharded optimizer step (bf16 workloads)")
+    zero_stage = Parameter("zero_stage", default=-1,
+                           help="1: ZeRO-1 sharded optimizer step, 0: replicated; -1 (default): ZeRO-1 for llama* "
+                                "at more than one worker (bf16 workloads)")
+    batch_size_per_worker = Parameter("batch_size_per_worker", default=0,
+                                      help="bf16 workloads: samples per worker per step (0: the model's default). "
+                                           "--batch_size is the reference MLP's global batch")
 
     @step
     def start(self):
@@ -99,8 +104,8 @@ class RayTorchTrain(FlowSpec):
             mode = "exact" if self.resume_mode == "exact" else "weights"
             self.result = train_workload(
                 model=self.model, steps=int(self.steps), num_workers=n, use_gpu=use_gpu,
-                batch_size_per_worker=max(1, int(self.global_batch_size) // n) if int(self.global_batch_size) != 32
-                else None, lr=None, ckpt_every_n_steps=int(self.ckpt_every_n_steps),
+                batch_size_per_worker=int(self.batch_size_per_worker) or None,
+                lr=None, ckpt_every_n_steps=int(self.ckpt_every_n_steps),
                 checkpoint_storage_path=current.ray_storage_path, checkpoint=args.get("checkpoint"),
                 resume_mode=mode, max_failures=int(self.max_failures), grad_comm_dtype=self.grad_comm_dtype,
                 zero_stage=int(self.zero_stage),
