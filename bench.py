@@ -347,11 +347,12 @@ def comm_sweep(args, model, opt, net, cur, step, world, sync) -> list:
             w = DistributedDataParallel(model, bucket_cap_mb=cap, defer_tail_to_optimizer=True, grad_comm_dtype=dtype,
                                         force_collectives=args.force_dist)
             cur["net"] = w
-            step(0)
+            for i in range(2):  # warm: lazy workspaces, the engine's first bucket plan
+                step(i)
             sync()
             dist.barrier()
             t0 = time.perf_counter()
-            n = 3
+            n = 10
             for i in range(n):
                 step(i)
             sync()

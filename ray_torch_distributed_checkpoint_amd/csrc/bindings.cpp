@@ -101,7 +101,8 @@ int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, in
                  int K, int s, int p, int backward, hipStream_t st);
 int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st);
 int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
-                   int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws, hipStream_t st);
+                   int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws, float* part, int qs,
+                   hipStream_t st);
 }
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -487,15 +488,22 @@ static void flash_fwd(Tensor qkv, Tensor out, Tensor lse, int64_t B, int64_t T, 
 }
 // cs_ws (optional fp32 [B*T/16][W], W = (H + 2 Hkv) Dh): per 16-row group column sums of dqkv
 static void flash_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, Tensor dqkv, int64_t B, int64_t T,
-                      int64_t H, int64_t Hkv, int64_t Dh, double scale, c10::optional<Tensor> cs_ws) {
+                      int64_t H, int64_t Hkv, int64_t Dh, double scale, c10::optional<Tensor> cs_ws,
+                      c10::optional<Tensor> part, int64_t qs) {
   TORCH_CHECK(dout.is_contiguous() && dqkv.is_contiguous(), "flash_bwd: contiguous tensors expected");
+  TORCH_CHECK(qs >= 1 && (H / Hkv) % qs == 0, "flash_bwd: qs must divide the GQA group size");
+  if (qs > 1)
+    TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= qs * B * T * Hkv * 2 * Dh,
+                "flash_bwd: part fp32 [qs][B*T][Hkv][2*Dh] workspace");
   if (cs_ws.has_value())
     TORCH_CHECK(cs_ws->is_cuda() && cs_ws->scalar_type() == at::kFloat && cs_ws->is_contiguous() &&
                     cs_ws->numel() >= B * T / 16 * (H + 2 * Hkv) * Dh,
                 "flash_bwd: cs_ws fp32 [B*T/16][W]");
   check_rc(rtdc_flash_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                           delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)T, (int)H, (int)Hkv, (int)Dh,
-                          (float)scale, cs_ws.has_value() ? cs_ws->data_ptr<float>() : nullptr, cur_stream()),
+                          (float)scale, cs_ws.has_value() ? cs_ws->data_ptr<float>() : nullptr,
+                          qs > 1 ? part->data_ptr<float>() : nullptr, (int)qs, cur_stream()),
            "flash_bwd");
 }
 
@@ -924,6 +932,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("can_stream_wait", &rtdc_ddp::GradBucketEngine::can_stream_wait)
       .def("stream_wait_bucket", &rtdc_ddp::GradBucketEngine::stream_wait_bucket)
       .def("tail_start", &rtdc_ddp::GradBucketEngine::tail_start)
+      .def("set_tail_split", &rtdc_ddp::GradBucketEngine::set_tail_split, py::arg("max_elems"))
+      .def("tail_piece_starts", &rtdc_ddp::GradBucketEngine::tail_piece_starts)
+      .def("wait_tail_piece", &rtdc_ddp::GradBucketEngine::wait_tail_piece, py::arg("i"))
       .def("num_buckets", &rtdc_ddp::GradBucketEngine::num_buckets)
       .def("launched", &rtdc_ddp::GradBucketEngine::launched)
       .def("steps", &rtdc_ddp::GradBucketEngine::steps)
@@ -975,7 +986,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout", &dropout);
   m.def("relu_dropout", &relu_dropout);
   m.def("flash_fwd", &flash_fwd);
-  m.def("flash_bwd", &flash_bwd);
+  m.def("flash_bwd", &flash_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("delta"),
+        py::arg("dqkv"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("Hkv"), py::arg("Dh"), py::arg("scale"),
+        py::arg("cs_ws") = py::none(), py::arg("part") = py::none(), py::arg("qs") = 1);
   m.def("rope", &rope);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);

@@ -63,6 +63,11 @@ struct Args {
   // the backward kernels store (the qkv projection's bias gradient, reduced later without
   // re-reading dqkv: ops/gemm.py offer_colsum_partials)
   float* cs_ws;
+  // GQA head split of dK/dV (qs > 1): block (key block, kv-head, qsub) covers q-heads
+  // qsub*grp/qs .. +grp/qs of the group and writes its fp32 partial dK|dV rows to
+  // part [qs][B*T][Hkv][2*Dh]; dkdv_reduce_kernel sums them in qsub order (deterministic)
+  float* part;
+  int qs;
 };
 
 // column sums over a wave's 16 rows of its stored fragment values v (lane = row (lane & 15) x
@@ -552,10 +557,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   const int nkb = a.T / BKV;
-  int kb, bk;
-  grid_pos(a, kb, bk);  // key block, (batch, kv-head)
+  int kb, bkq;
+  grid_pos(a, kb, bkq);  // key block, (batch, kv-head, q-head subset)
+  const int qs = a.qs, bk = bkq / qs, qsub = bkq - bk * qs;
   const int b = bk / a.Hkv, kvh = bk % a.Hkv;
-  const int grp = a.H / a.Hkv;
+  const int grp = a.H / a.Hkv, gper = grp / qs;  // q-heads of the group this block covers
   const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
   const bf16_t* base = a.qkv + (long long)b * a.T * W;
   const bf16_t* dob = a.dout + (long long)b * a.T * C;
@@ -566,15 +572,15 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
   uint32_t troff[DH / 16];
   tr_lane_offsets<DH>(troff, lane);
 
-  const int nq = nkb - kb;     // q blocks at/after the diagonal
-  const int total = nq * grp;  // steps over (q-head in group, q block)
+  const int nq = nkb - kb;      // q blocks at/after the diagonal
+  const int total = nq * gper;  // steps over (q-head of this subset, q block)
   const float* rowsrc = wave < 2 ? (const float*)a.lse : a.delta;
   const int rowoff = 32 * (wave & 1) + 4 * (lane & 7);
   const int rowdst = 2 * TILE + 256 * (wave >> 1) + 128 * (wave & 1);
   auto issue = [&](int it) {
     char* st = smem + (it % NS) * STG;
     const int gi = it / nq, qb = kb + it % nq;
-    const int h = kvh * grp + gi;
+    const int h = kvh * grp + qsub * gper + gi;
     stage<DH>(base, W, qb * BQ, h * DH, st, wave, lane);
     stage<DH>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
     const float* src = rowsrc + ((long long)b * a.H + h) * a.T + qb * BQ + rowoff;
@@ -665,6 +671,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
     if (it + 1 < total && !(a.diag & 1)) wait_vm_upto(PER * (min(it + NS - 1, total - 1) - it - 1));
     step_barrier();
   }
+  if (qs > 1) {  // fp32 partial of this q-head subset; dkdv_reduce_kernel finishes the rows
+    float* prow = a.part + (((long long)qsub * a.B * a.T + (long long)b * a.T + mykey) * a.Hkv + kvh) * (2 * DH);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      *(f32x4*)(prow + 16 * d + 4 * g) = f32x4{dk[d][0] * a.scale, dk[d][1] * a.scale, dk[d][2] * a.scale,
+                                               dk[d][3] * a.scale};
+      *(f32x4*)(prow + DH + 16 * d + 4 * g) = dv[d];
+    }
+    return;
+  }
   bf16_t* krow = a.dqkv + ((long long)b * a.T + mykey) * W;
 #pragma unroll
   for (int d = 0; d < DT; ++d) {
@@ -677,6 +693,38 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
     wave_colsum16<DT>(dk, a.scale, crow + kcol, lane);
     wave_colsum16<DT>(dv, 1.f, crow + vcol, lane);
   }
+}
+
+// dK | dV rows from the qs fp32 partials of a head-split dK/dV pass: dqkv[b, t, K|V cols] =
+// bf16(sum over qsub in order).  Block = 16 rows x 1024 columns of the [Hkv][2*Dh] partial row
+// (blockIdx.y picks the column half when Hkv*2*Dh = 2048); thread = 4 columns, 16-B loads.  With
+// cs_ws it also writes the 16-row column sums of the stored bf16 values (the qkv bias gradient
+// partials, as the unsplit kernel's wave_colsum16 does).
+template <int DH>
+__global__ __launch_bounds__(256) void dkdv_reduce_kernel(Args a) {
+  const int KV = a.Hkv * 2 * DH;
+  const int col = (blockIdx.y * 256 + threadIdx.x) * 4;  // column in the [Hkv][2][DH] row
+  if (col >= KV) return;
+  const long long rows = (long long)a.B * a.T, r0 = (long long)blockIdx.x * 16;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const int kvh = col / (2 * DH), rem = col % (2 * DH);
+  const int dcol = rem < DH ? C + kvh * DH + rem : C + a.Hkv * DH + kvh * DH + (rem - DH);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 16; ++i) {
+    const long long r = r0 + i;
+    f32x4 acc = *(const f32x4*)(a.part + r * KV + col);
+    for (int q = 1; q < a.qs; ++q) {
+      const f32x4 v = *(const f32x4*)(a.part + ((long long)q * rows + r) * KV + col);
+      acc[0] += v[0]; acc[1] += v[1]; acc[2] += v[2]; acc[3] += v[3];
+    }
+    const uint2 o = make_uint2(pack_bf2(acc[0], acc[1]), pack_bf2(acc[2], acc[3]));
+    *(uint2*)(a.dqkv + r * W + dcol) = o;
+    if (a.cs_ws) {
+      cs[0] += __uint_as_float(o.x << 16); cs[1] += __uint_as_float(o.x & 0xffff0000u);
+      cs[2] += __uint_as_float(o.y << 16); cs[3] += __uint_as_float(o.y & 0xffff0000u);
+    }
+  }
+  if (a.cs_ws) *(f32x4*)(a.cs_ws + (r0 >> 4) * W + dcol) = f32x4{cs[0], cs[1], cs[2], cs[3]};
 }
 
 // ------------------------------------------------------------------------------ dQ
@@ -872,8 +920,9 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
 
 extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
                               void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws,
-                              hipStream_t st) {
+                              float* part, int qs, hipStream_t st) {
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
+  if (qs < 1 || (H / Hkv) % qs != 0 || (qs > 1 && part == nullptr) || ((Hkv * 2 * Dh) % 4) != 0) return 1;
   // dQ first: it also computes the row terms delta = rowsum(dO * O) that dK/dV read
   fa::Args a{};
   a.qkv = (const bf16_t*)qkv; a.out = (bf16_t*)out; a.dout = (const bf16_t*)dout; a.lse = (float*)lse;
@@ -881,7 +930,8 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   a.dqkv = (bf16_t*)dqkv;
   a.cs_ws = cs_ws;
   a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd(); a.diag = fa_diag();
-  dim3 g1(T / 64, B * Hkv), g2(T / 64, B * H);
+  a.part = part; a.qs = qs;
+  dim3 g1(T / 64, B * Hkv * qs), g2(T / 64, B * H);
   const int ns = fa_ns(Dh);
   if (Dh == 64) {
     FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
@@ -889,6 +939,12 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   } else {
     FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
     FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
+  }
+  if (qs > 1) {
+    const int KV = Hkv * 2 * Dh;
+    dim3 gr((unsigned)((long long)B * T / 16), (unsigned)((KV / 4 + 255) / 256));
+    if (Dh == 64) hipLaunchKernelGGL(fa::dkdv_reduce_kernel<64>, gr, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(fa::dkdv_reduce_kernel<128>, gr, dim3(256), 0, st, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -102,6 +102,8 @@ class GradBucketEngine {
       if (e) hipEventDestroy(e);
     for (auto e : p2p_done_)
       if (e) hipEventDestroy(e);
+    for (auto e : piece_events_)
+      if (e) hipEventDestroy(e);
   }
 
   void finalize(bool defer_last = false) {
@@ -112,8 +114,11 @@ class GradBucketEngine {
     for (size_t i = 0; i < marked_.size(); ++i)
       if (!marked_[i]) flat_.slice(0, seg_[i].first, seg_[i].first + seg_[i].second).zero_();
     while (next_ < works_.size()) launch(next_++);
-    const bool defer = defer_last && works_.size() > 1 && !is_p2p(works_.size() - 1);
+    const size_t last_b = works_.size() - 1;
+    const bool defer = defer_last && works_.size() > 1 && !is_p2p(last_b);
     const size_t nwait = works_.size() - (defer ? 1 : 0);
+    // the last bucket as pieces (set_tail_split), not deferred: its pieces complete here
+    const bool pieces_now = !defer && !pieces_.empty();
     if (p2p_) {
       hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
       for (size_t b = 0; b < nwait; ++b)
@@ -121,22 +126,43 @@ class GradBucketEngine {
     }
     if (side_) {
       // the widened fp32 slices are final once the side stream passed each bucket's event
+      // (a piece-split last bucket: its last piece's event - the side stream is in order)
       hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
       size_t last = nwait;
       while (last > 0 && is_p2p(last - 1)) --last;  // the side stream handled buckets < last
-      if (last > 0) TORCH_CHECK(hipStreamWaitEvent(cur, events_[last - 1], 0) == hipSuccess, "hipStreamWaitEvent");
+      if (last > 0) {
+        hipEvent_t ev = (pieces_now && last - 1 == last_b) ? piece_events_[pieces_.size() - 1] : events_[last - 1];
+        TORCH_CHECK(hipStreamWaitEvent(cur, ev, 0) == hipSuccess, "hipStreamWaitEvent");
+      }
     } else {
       {
         pybind11::gil_scoped_release nogil;
         for (size_t b = 0; b < nwait; ++b)
           if (works_[b]) works_[b]->wait();
+        if (pieces_now)
+          for (auto& w : piece_works_) w->wait();
       }
-      if (lp_.defined())  // CPU (gloo): widen in place after the blocking wait
-        for (size_t b = 0; b < nwait; ++b) widen(b);
-      else if (!use_avg_ && post_scale_ != 1.0)
+      if (lp_.defined()) {  // CPU (gloo): widen in place after the blocking wait
+        for (size_t b = 0; b < nwait; ++b)
+          if (!(pieces_now && b == last_b)) widen(b);
+        if (pieces_now)
+          for (size_t i = 0; i < pieces_.size(); ++i) widen_range(pieces_[i].first, pieces_[i].second);
+      } else if (!use_avg_ && post_scale_ != 1.0) {
         flat_.slice(0, 0, bounds_[nwait]).mul_(post_scale_);
+      }
     }
-    if (defer) tail_ = works_.back();
+    if (pieces_now) {
+      pieces_.clear();
+      piece_works_.clear();
+    }
+    if (defer) {
+      if (!pieces_.empty()) {
+        tail_piece_next_ = 0;  // pieces stay in flight: wait_tail_piece(i) / wait_tail()
+        tail_pieces_pending_ = true;
+      } else {
+        tail_ = works_.back();
+      }
+    }
     for (size_t b = 0; b < nwait; ++b) works_[b].reset();
     pending_ = expected_;
     std::fill(launched_.begin(), launched_.end(), false);
@@ -147,6 +173,10 @@ class GradBucketEngine {
 
   // stream-order the last bucket's all-reduce before later work (no-op when none is pending)
   void wait_tail() {
+    if (tail_pieces_pending_) {
+      while (tail_piece_next_ < pieces_.size()) wait_tail_piece((int64_t)tail_piece_next_);
+      return;
+    }
     if (!tail_) return;
     const size_t last = works_.size() - 1;
     if (side_) {
@@ -163,6 +193,50 @@ class GradBucketEngine {
     tail_.reset();
     works_[last].reset();
   }
+  // ---- the last bucket as several collectives (set_tail_split) -------------------------
+  // GPT-2's tied token table is one 154 MB gradient that completes at the very end of
+  // backward: as ONE deferred collective the fused optimizer can only update it after all of
+  // it landed.  Split into pieces of at most `max_elems`, the optimizer waits for piece i and
+  // updates its slice while pieces i+1.. are still on the wire (optim/fused.py _launch_split).
+  // All pieces launch together in order on every rank (same collective sequence everywhere).
+  void set_tail_split(int64_t max_elems) {
+    TORCH_CHECK(max_elems >= 0, "set_tail_split: max_elems >= 0");
+    tail_max_ = max_elems;
+  }
+  // flat offsets where the pieces of a deferred tail start (empty: no piece-split tail pending)
+  std::vector<int64_t> tail_piece_starts() const {
+    std::vector<int64_t> out;
+    if (tail_pieces_pending_)
+      for (auto& pr : pieces_) out.push_back(pr.first);
+    return out;
+  }
+  // make the current stream (CPU: the host) wait until piece i of the deferred tail is final
+  void wait_tail_piece(int64_t i) {
+    if (!tail_pieces_pending_) return;
+    TORCH_CHECK(i >= 0 && (size_t)i < pieces_.size(), "wait_tail_piece: bad piece");
+    while (tail_piece_next_ <= (size_t)i) {
+      const size_t k = tail_piece_next_++;
+      if (side_) {
+        hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+        TORCH_CHECK(hipStreamWaitEvent(cur, piece_events_[k], 0) == hipSuccess, "hipStreamWaitEvent");
+      } else {
+        {
+          pybind11::gil_scoped_release nogil;
+          piece_works_[k]->wait();
+        }
+        if (lp_.defined()) widen_range(pieces_[k].first, pieces_[k].second);
+        else if (!use_avg_ && post_scale_ != 1.0)
+          flat_.slice(0, pieces_[k].first, pieces_[k].second).mul_(post_scale_);
+      }
+    }
+    if (tail_piece_next_ >= pieces_.size()) {
+      tail_pieces_pending_ = false;
+      pieces_.clear();
+      piece_works_.clear();
+      works_.back().reset();
+    }
+  }
+
   // Route buckets of at most max_bytes (communicated bytes) through the one-shot hipIpc
   // all-reduce (runtime/p2p_comm.cpp) on a dedicated stream instead of RCCL; the rest stay on
   // the process group.  Collective order is unchanged (bucket order), so every rank routes the
@@ -203,6 +277,14 @@ class GradBucketEngine {
     TORCH_CHECK(can_stream_wait(), "stream_wait_bucket: needs a device buffer, no ZeRO, and AVG or bf16 comm");
     TORCH_CHECK(b >= 0 && (size_t)b < works_.size() && launched_[b], "stream_wait_bucket: bucket not launched");
     hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+    if ((size_t)b + 1 == works_.size() && !pieces_.empty()) {  // a piece-split last bucket: all pieces
+      if (side_) {
+        TORCH_CHECK(hipStreamWaitEvent(cur, piece_events_[pieces_.size() - 1], 0) == hipSuccess, "hipStreamWaitEvent");
+      } else {
+        for (auto& w : piece_works_) w->wait();
+      }
+      return;
+    }
     if (is_p2p(b)) {
       TORCH_CHECK(hipStreamWaitEvent(cur, p2p_done_[b], 0) == hipSuccess, "hipStreamWaitEvent");
     } else if (side_) {
@@ -212,7 +294,7 @@ class GradBucketEngine {
       works_[b]->wait();
     }
   }
-  bool tail_pending() const { return (bool)tail_; }
+  bool tail_pending() const { return (bool)tail_ || tail_pieces_pending_; }
   int64_t tail_start() const { return bounds_[bounds_.size() - 2]; }
 
   int64_t num_buckets() const { return (int64_t)works_.size(); }
@@ -263,6 +345,11 @@ class GradBucketEngine {
       launched_[b] = true;
       return;
     }
+    if (b + 1 == works_.size() && tail_max_ > 0 && hi - lo > tail_max_ && !zero_world_) {
+      launch_pieces(lo, hi);
+      launched_[b] = true;
+      return;
+    }
     if (lp_.defined()) {
       at::Tensor dst = lp_.slice(0, lo, hi);
       if (flat_.is_cuda()) {
@@ -294,6 +381,62 @@ class GradBucketEngine {
       works_[b]->wait();
       widen(b);
       TORCH_CHECK(hipEventRecord(events_[b], side_->stream()) == hipSuccess, "hipEventRecord");
+    }
+  }
+
+  // the last bucket [lo, hi) as pieces of <= tail_max_ elements (64-aligned), each its own
+  // all-reduce (+ bf16 narrow / side-stream widen and a per-piece event)
+  void launch_pieces(int64_t lo, int64_t hi) {
+    pieces_.clear();
+    piece_works_.clear();
+    const int64_t n = (hi - lo + tail_max_ - 1) / tail_max_;
+    const int64_t step = ((hi - lo + n - 1) / n + 63) / 64 * 64;
+    for (int64_t a = lo; a < hi; a += step) pieces_.emplace_back(a, std::min(hi, a + step));
+    if (side_)
+      while (piece_events_.size() < pieces_.size()) {
+        hipEvent_t e;
+        TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
+        piece_events_.push_back(e);
+      }
+    c10d::AllreduceOptions opts;
+    opts.reduceOp = use_avg_ ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
+    for (size_t i = 0; i < pieces_.size(); ++i) {
+      const auto [a, e] = pieces_[i];
+      at::Tensor t = flat_.slice(0, a, e);
+      if (lp_.defined()) {
+        at::Tensor dst = lp_.slice(0, a, e);
+        if (flat_.is_cuda()) {
+          hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+          TORCH_CHECK(rtdc_f32_to_bf16(t.data_ptr<float>(), dst.data_ptr(), e - a, cur) == 0, "f32->bf16");
+        } else {
+          dst.copy_(t);
+        }
+        t = dst;
+      }
+      std::vector<at::Tensor> tv{t};
+      piece_works_.push_back(pg_->allreduce(tv, opts));
+    }
+    if (side_) {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*side_);
+      for (size_t i = 0; i < pieces_.size(); ++i) {
+        piece_works_[i]->wait();
+        widen_range(pieces_[i].first, pieces_[i].second);
+        TORCH_CHECK(hipEventRecord(piece_events_[i], side_->stream()) == hipSuccess, "hipEventRecord");
+      }
+    }
+  }
+
+  void widen_range(int64_t lo, int64_t hi) {
+    const float scale = use_avg_ ? 1.f : (float)post_scale_;
+    if (flat_.is_cuda()) {
+      hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+      TORCH_CHECK(rtdc_bf16_to_f32(lp_.slice(0, lo, hi).data_ptr(), flat_.slice(0, lo, hi).data_ptr<float>(), hi - lo,
+                                   scale, st) == 0,
+                  "bf16->f32");
+    } else {
+      at::Tensor f = flat_.slice(0, lo, hi);
+      f.copy_(lp_.slice(0, lo, hi));
+      if (scale != 1.f) f.mul_(scale);
     }
   }
 
@@ -332,6 +475,12 @@ class GradBucketEngine {
   std::vector<hipEvent_t> p2p_ready_, p2p_done_;
   size_t next_ = 0;
   int64_t steps_ = 0;
+  int64_t tail_max_ = 0;                                  // set_tail_split (0: one collective)
+  std::vector<std::pair<int64_t, int64_t>> pieces_;       // the last bucket's pieces this step
+  std::vector<c10::intrusive_ptr<c10d::Work>> piece_works_;
+  std::vector<hipEvent_t> piece_events_;
+  bool tail_pieces_pending_ = false;
+  size_t tail_piece_next_ = 0;
 };
 
 }  // namespace rtdc_ddp

@@ -133,10 +133,32 @@ class _FlashAttention(torch.autograd.Function):
         # written by the kernels on the way out, offered to that projection's colsum()
         Wd = qkv.shape[-1]
         cs = torch.empty((B * T // 16, Wd), dtype=torch.float32, device=qkv.device) if G.partials_wanted() else None
-        gpu_ext().flash_bwd(qkv, out, dout.contiguous(), lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs)
+        qs = _dkdv_head_split(B, T, H, Hkv, qkv.device)
+        part = torch.empty(qs * B * T * Hkv * 2 * Dh, dtype=torch.float32, device=qkv.device) if qs > 1 else None
+        gpu_ext().flash_bwd(qkv, out, dout.contiguous(), lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs, part, qs)
         if cs is not None:
             G.offer_colsum_partials(dqkv, cs)
         return dqkv, None, None, None, None, None
+
+
+def _dkdv_head_split(B: int, T: int, H: int, Hkv: int, device) -> int:
+    """q-head subsets per GQA group for the dK/dV pass.  One dK/dV block owns 64 keys of one
+    kv-head and loops over every q-head of its group, so a short batch (Llama-3-8B at B=1,
+    T=2048: 8 kv-heads x 32 key blocks = 256 blocks, the heaviest with 4x32 steps) fills one
+    block per CU with a 2:1 load imbalance.  Splitting the group over `qs` blocks multiplies the
+    block count (partials summed in a fixed order by dkdv_reduce_kernel: deterministic) and lets
+    the heavy-first order balance them.  RTDC_FA_QS forces a value (1 = no split)."""
+    grp = H // Hkv
+    forced = int(os.environ.get("RTDC_FA_QS", "0"))
+    if forced:
+        return forced if grp % forced == 0 else 1
+    from .gemm import _num_cus
+
+    blocks, cus = B * Hkv * (T // 64), _num_cus(device)
+    qs = 1
+    while grp % (qs * 2) == 0 and blocks * qs < 4 * cus:
+        qs *= 2
+    return qs
 
 
 def flash_supported(T: int, Dh: int) -> bool:

@@ -152,16 +152,18 @@ class FlatParamSpace:
         self.zero: ZeroLayout | None = None
         self._offsets = None
         self._chunk_cache: dict = {}
-        # (flat offset, wait fn) of a gradient slice whose all-reduce is still in flight
-        # (DistributedDataParallel(defer_tail_to_optimizer=True)); everything below the offset
-        # is final
+        # [(flat offset, wait fn)] of gradient pieces whose all-reduce is still in flight
+        # (DistributedDataParallel(defer_tail_to_optimizer=True)), ascending: everything below
+        # the first offset is final, piece i spans [offset_i, offset_i+1) and is final after
+        # its wait fn (which also waits for the pieces before it)
         self.pending_tail = None
 
     def wait_pending_tail(self) -> None:
         t = self.pending_tail
         if t is not None:
             self.pending_tail = None
-            t[1]()
+            for _, wait in t:
+                wait()
 
     @staticmethod
     def view(buf: torch.Tensor, s: Segment) -> torch.Tensor:
@@ -297,6 +299,31 @@ class FlatParamSpace:
             (lo if s.offset < split else hi).extend(self._chunks(s, d))
         out = tuple((torch.tensor(r if r else [(0, 0, 0)], dtype=torch.int64).to(self.device), len(r))
                     for r in (lo, hi))
+        self._chunk_cache[key] = out
+        return out
+
+    def chunk_table_splits(self, params_subset, decay_flags, splits):
+        """len(splits)+1 chunk tables: elements below flat offset splits[0], in
+        [splits[i], splits[i+1]), ..., and from splits[-1] on.  A chunk that straddles a
+        split is cut there (pieces of a deferred collective need not align to chunks)."""
+        splits = tuple(int(x) for x in splits)
+        key = ("splits", tuple(id(p) for p in params_subset), tuple(decay_flags), splits)
+        hit = self._chunk_cache.get(key)
+        if hit is not None:
+            return hit
+        import bisect
+
+        parts = [[] for _ in range(len(splits) + 1)]
+        for p, d in zip(params_subset, decay_flags):
+            for start, lend, so in self._chunks(self.segment_of(p), d):
+                n, flag = lend & 0xFFFFFFFF, lend & ~0xFFFFFFFF
+                a, e = start, start + n
+                while a < e:
+                    k = bisect.bisect_right(splits, a)
+                    cut = min(e, splits[k]) if k < len(splits) else e
+                    parts[k].append((a, (cut - a) | flag, so + (a - start)))
+                    a = cut
+        out = tuple((torch.tensor(r if r else [(0, 0, 0)], dtype=torch.int64).to(self.device), len(r)) for r in parts)
         self._chunk_cache[key] = out
         return out
 

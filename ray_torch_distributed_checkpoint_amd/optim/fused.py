@@ -314,15 +314,17 @@ class _FlatOptimizer(torch.optim.Optimizer):
             for ps, flags, fn in launches:
                 fn(*sp.chunk_table(ps, flags))
             return
-        split = tail[0]
-        parts = [(sp.chunk_table_split(ps, flags, split), fn) for ps, flags, fn in launches]
-        for (lo, _hi), fn in parts:
-            if lo[1]:
-                fn(*lo)
-        sp.wait_pending_tail()
-        for (_lo, hi), fn in parts:
-            if hi[1]:
-                fn(*hi)
+        sp.pending_tail = None
+        starts = [off for off, _ in tail]
+        parts = [(sp.chunk_table_splits(ps, flags, starts), fn) for ps, flags, fn in launches]
+        for tables, fn in parts:  # everything below the first in-flight piece
+            if tables[0][1]:
+                fn(*tables[0])
+        for i, (_, wait) in enumerate(tail):  # piece i: wait for its collective, then update it
+            wait()
+            for tables, fn in parts:
+                if tables[i + 1][1]:
+                    fn(*tables[i + 1])
 
     def _use_native(self):
         ps = self._all_params()

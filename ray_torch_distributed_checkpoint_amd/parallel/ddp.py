@@ -26,7 +26,10 @@ MI355X:
 * With `defer_tail_to_optimizer`, backward returns with the LAST bucket's all-reduce still in
   flight (on RCCL): the fused optimizer steps every other parameter first and stream-waits for
   it only before the last slice, hiding the step's exposed collective tail (GPT-2: the tied
-  154 MB token table, whose gradient completes at the very end of backward).
+  154 MB token table, whose gradient completes at the very end of backward).  That bucket is
+  issued as collectives of <= `tail_piece_mb` (32 MB: >= 4 MB per xGMI link at 8 ranks), and
+  the optimizer waits for and updates them piece by piece, so only the first piece's transfer
+  and the last piece's update stay exposed.
 * `zero_stage=1` (ZeRO-1) shards the optimizer work: every bucket is padded to a multiple of
   64 x world elements and REDUCE-SCATTERED in place (rank r receives the averaged shard r), the
   fused optimizer updates only this rank's shards (1/world of the AdamW traffic - 40 of 150 ms
@@ -68,7 +71,8 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: float = 2.0, broadcast_buffers: bool = True, device_ids=None,
                  output_device=None, find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  defer_tail_to_optimizer: bool = False, grad_comm_dtype: str = "fp32", p2p_max_kb: float = 0.0,
-                 zero_stage: int = 0, p2p_timeout_s: float = 30.0, force_collectives: bool = False):
+                 zero_stage: int = 0, p2p_timeout_s: float = 30.0, force_collectives: bool = False,
+                 tail_piece_mb: float = 32.0):
         super().__init__()
         if grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
@@ -177,6 +181,11 @@ class DistributedDataParallel(nn.Module):
         if self._collective:
             self._verify_plan_across_ranks()
             self._engine = self._native_engine(process_group)
+            if self._engine is not None and self.defer_tail and tail_piece_mb > 0:
+                # the deferred last bucket (GPT-2: the 154 MB tied token table) as collectives of
+                # <= tail_piece_mb communicated bytes: the optimizer updates piece i while pieces
+                # i+1.. are still on the wire (see FlatParamSpace.pending_tail)
+                self._engine.set_tail_split(int(tail_piece_mb * (1 << 20) / esz))
             self._attach_p2p(process_group, p2p_max_kb)
             for p in self.space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
@@ -376,7 +385,12 @@ class DistributedDataParallel(nn.Module):
                                    f"p2p_timeout_s={self._p2p_timeout_s}")
             self._engine.finalize(self.defer_tail)
             if self._engine.tail_pending():
-                self.space.pending_tail = (self._engine.tail_start(), self._engine.wait_tail)
+                starts = self._engine.tail_piece_starts()
+                if starts:
+                    eng = self._engine
+                    self.space.pending_tail = [(s, (lambda i=i: eng.wait_tail_piece(i))) for i, s in enumerate(starts)]
+                else:
+                    self.space.pending_tail = [(self._engine.tail_start(), self._engine.wait_tail)]
             if self._check:  # RTDC_COLLECTIVE_CHECK=1: desync detector (one tiny all-reduce per step)
                 self._agree(self._steps * 1000003 + self._engine.launched() + len(self.buckets), "step sequence")
             if self.zero and not self._zero_checked:

@@ -47,7 +47,7 @@ def test_ddp_python_engine_matches_torch_ddp():
     assert max(out) < 1e-5, out
 
 
-def _ddp_deferred_tail(rank, world, opt_kind):
+def _ddp_deferred_tail(rank, world, opt_kind, piece_mb=32.0, comm="fp32"):
     """defer_tail_to_optimizer: backward returns with the last bucket's all-reduce pending; the
     fused optimizer steps the rest first and waits for it before the last slice - the same
     parameters as torch DDP + torch optimizer after several steps."""
@@ -60,7 +60,8 @@ def _ddp_deferred_tail(rank, world, opt_kind):
     base = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64), torch.nn.ReLU(),
                                torch.nn.Linear(64, 5))
     ours_m, ref_m = copy.deepcopy(base), copy.deepcopy(base)
-    ours = DistributedDataParallel(ours_m, bucket_cap_mb=0.01, first_bucket_mb=0.005, defer_tail_to_optimizer=True)
+    ours = DistributedDataParallel(ours_m, bucket_cap_mb=0.01, first_bucket_mb=0.005, defer_tail_to_optimizer=True,
+                                   tail_piece_mb=piece_mb, grad_comm_dtype=comm)
     ref = torch.nn.parallel.DistributedDataParallel(ref_m)
     assert len(ours.buckets) > 1
     if opt_kind == "adamw":
@@ -78,17 +79,31 @@ def _ddp_deferred_tail(rank, world, opt_kind):
             opt.zero_grad()
             torch.nn.functional.cross_entropy(m(x), y).backward()
             if m is ours:
-                pending.append(ours.space.pending_tail is not None)
+                pending.append(len(ours.space.pending_tail) if ours.space.pending_tail else 0)
             opt.step()
         assert ours.space.pending_tail is None
     assert all(pending), pending
-    return max(float((a - b).abs().max()) for a, b in zip(ours_m.parameters(), ref_m.parameters()))
+    err = max(float((a - b).abs().max()) for a, b in zip(ours_m.parameters(), ref_m.parameters()))
+    return err, max(pending)
 
 
 def test_ddp_deferred_tail_matches_torch():
     for kind in ("sgd", "adamw"):
         out = mp_util.run(_ddp_deferred_tail, 2, kind)
-        assert max(out) < 1e-5, (kind, out)
+        assert max(e for e, _ in out) < 1e-5, (kind, out)
+        assert all(n == 1 for _, n in out)  # the small tail: one collective
+
+
+def test_ddp_tail_pieces_pipelined_into_optimizer_match_torch():
+    """The deferred last bucket as several collectives (tail_piece_mb): the optimizer waits for
+    and updates piece by piece (chunks cut at piece boundaries) - same parameters as torch DDP;
+    with bf16 communication the same up to the bf16 rounding of the gradients."""
+    for kind in ("sgd", "adamw"):
+        out = mp_util.run(_ddp_deferred_tail, 2, kind, 0.002)
+        assert max(e for e, _ in out) < 1e-5, (kind, out)
+        assert all(n >= 3 for _, n in out), out
+    out = mp_util.run(_ddp_deferred_tail, 2, "sgd", 0.002, "bf16")
+    assert max(e for e, _ in out) < 5e-3 and all(n >= 2 for _, n in out), out
 
 
 def _ddp_unused(rank, world):

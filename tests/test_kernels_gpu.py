@@ -755,3 +755,41 @@ def test_gemm4w_splitk_weight_gradient(a_k, b_k):
     dw = torch.empty(N, K, device=DEV, dtype=torch.float32)
     G.gemm_bf16(A, x, dw, N, K, Mt, A.shape[1], K, K, a_k, b_k, tile_cfg=10)
     _close(dw, dy.float().t() @ x.float(), 1e-5)
+
+
+@pytest.mark.parametrize("Dh,qs", [(128, 2), (128, 4), (64, 4)])
+def test_flash_dkdv_head_split_matches_unsplit_and_reference(monkeypatch, Dh, qs):
+    """GQA dK/dV with the group's q-heads split over `qs` blocks (fp32 partials summed in a
+    fixed order by dkdv_reduce_kernel): same gradients as the unsplit kernel (to fp32 rounding)
+    and the fp32 reference, bitwise run to run, and the offered colsum partials match dqkv."""
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+    from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref
+
+    torch.manual_seed(Dh + qs)
+    Bn, T, H, Hkv = 1, 512, 8, 2
+    W = (H + 2 * Hkv) * Dh
+    qkv0 = _bf(Bn, T, W)
+    g = _bf(Bn, T, H * Dh)
+
+    def grads(split):
+        monkeypatch.setenv("RTDC_FA_QS", str(split))
+        qkv = qkv0.clone().requires_grad_(True)
+        causal_attention(qkv, H, Hkv).backward(g)
+        d2 = qkv.grad.view(-1, W)
+        cs = G.colsum(d2)  # the kernels' offered 16-row partials
+        torch.cuda.synchronize()
+        return qkv.grad.clone(), cs.clone()
+
+    a, cs_a = grads(qs)
+    a2, _ = grads(qs)
+    b, _ = grads(1)
+    assert torch.equal(a, a2), "head-split backward is not deterministic"
+    C = H * Dh
+    _close(a[..., C:], b[..., C:], 1e-2)      # dK | dV: split vs unsplit (bf16 rounding of each)
+    assert torch.equal(a[..., :C], b[..., :C])  # dQ untouched by the split
+    qr = qkv0.float().requires_grad_(True)
+    causal_attention_ref(qr, Bn, T, H, Hkv, Dh).backward(g.float())
+    _close(a[..., C:C + Hkv * Dh], qr.grad[..., C:C + Hkv * Dh], 3e-2)
+    _close(a[..., C + Hkv * Dh:], qr.grad[..., C + Hkv * Dh:], 3e-2)
+    _close(cs_a, a.view(-1, W).float().sum(0), 1e-5)
