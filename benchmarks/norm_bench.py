@@ -47,6 +47,33 @@ def main():
     r["aten_fwd_us"] = round(timeit(aten_fwd), 1)
     print(json.dumps(r), flush=True)
 
+    # backward at the GPT-2 form (residual-stream gradient added in the kernel, column sums of
+    # dx for the residual projection's bias, dgamma / dbeta partial rows) and the Llama RMSNorm
+    # form; bytes = read x, dy, dres + write dx
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+    from ray_torch_distributed_checkpoint_amd.ops.norm import _bwd_waves, _bwd_ws_elems
+
+    ext = gpu_ext()
+    for name, M2, D2, rms in (("gpt2_ln", 16384, 768, False), ("llama_rms", 2048, 4096, True)):
+        x2 = torch.randn(M2, D2, device=dev).bfloat16()
+        dy = torch.randn(M2, D2, device=dev).bfloat16()
+        dres = torch.randn(M2, D2, device=dev).bfloat16()
+        g2 = torch.ones(D2, device=dev).bfloat16()
+        mean = torch.zeros(M2, device=dev)
+        rstd = torch.ones(M2, device=dev)
+        dx = torch.empty_like(x2)
+        nw = _bwd_waves(M2)
+        ws = torch.empty(_bwd_ws_elems(nw, D2), device=dev)
+        dg, db, dxs = (torch.empty(D2, device=dev) for _ in range(3))
+        if rms:
+            fn = lambda: ext.rmsnorm_bwd(dy, x2, g2, rstd, dres, dx, ws, dg, None, nw, False)  # noqa: E731
+        else:
+            fn = lambda: ext.layernorm_bwd(dy, x2, g2, mean, rstd, dres, dx, ws, dg, db, dxs, nw, False,  # noqa: E731
+                                           False)
+        us = timeit(fn)
+        print(json.dumps({"bwd": name, "M": M2, "D": D2, "us": round(us, 1),
+                          "TBps": round(4 * M2 * D2 * 2 / us / 1e6, 2)}), flush=True)
+
 
 if __name__ == "__main__":
     main()

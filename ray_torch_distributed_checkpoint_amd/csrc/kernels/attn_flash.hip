@@ -695,6 +695,196 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
   }
 }
 
+// dK / dV with 32 keys per wave (block = 128 keys, two 16-key groups per wave): every Q / dO
+// fragment and row constant read from LDS feeds both key groups' S / dP MFMAs, and every
+// transposed dO / Q fragment both groups' dV / dK MFMAs - half the LDS traffic per MFMA of
+// bwd_dkdv_kernel, whose Dh = 64 loop is LDS-bound (per step and wave 24 ds_read_b128 + 32
+// ds_read_b64_tr_b16 = 160 LDS-array cycles for 32 MFMAs, 12 waves per CU; MI355X_MICROARCH.md
+// §LDS).  Same ring, row-constant DMA and output contract (incl. the GQA head split).
+template <int DH, int NS>
+__global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, DB = 2, TILE = 64 * DH * 2, KG = 2, BK2 = 128;
+  constexpr int STG = 2 * TILE + 512, PER = DH / 16 + 1;
+  __shared__ __attribute__((aligned(16))) char smem[NS * STG];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = a.T / BQ;
+  int kb, bkq;
+  grid_pos(a, kb, bkq);  // 128-key block, (batch, kv-head, q-head subset)
+  const int qs = a.qs, bk = bkq / qs, qsub = bkq - bk * qs;
+  const int b = bk / a.Hkv, kvh = bk % a.Hkv;
+  const int grp = a.H / a.Hkv, gper = grp / qs;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const bf16_t* dob = a.dout + (long long)b * a.T * C;
+  const int kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int k0w = kb * BK2 + wave * 32;  // this wave's keys [k0w, k0w + 32)
+  int mykey[KG];
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) mykey[kg] = k0w + 16 * kg + (lane & 15);
+  const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
+
+  const int qb0 = kb * (BK2 / BQ);  // first q block that meets the block's keys
+  const int nq = nqb - qb0;
+  const int total = nq * gper;
+  const float* rowsrc = wave < 2 ? (const float*)a.lse : a.delta;
+  const int rowoff = 32 * (wave & 1) + 4 * (lane & 7);
+  const int rowdst = 2 * TILE + 256 * (wave >> 1) + 128 * (wave & 1);
+  auto issue = [&](int it) {
+    char* st = smem + (it % NS) * STG;
+    const int gi = it / nq, qb = qb0 + it % nq;
+    const int h = kvh * grp + qsub * gper + gi;
+    stage<DH>(base, W, qb * BQ, h * DH, st, wave, lane);
+    stage<DH>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
+    const float* src = rowsrc + ((long long)b * a.H + h) * a.T + qb * BQ + rowoff;
+    if (lane < 8) __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(st + rowdst), 16, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < total) issue(s);
+
+  bf16x8 kf[KG][KS], vf[KG][KS];
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[kg][ks] = gload8(base + (long long)mykey[kg] * W + kcol + ks * 32 + g * 8);
+      vf[kg][ks] = gload8(base + (long long)mykey[kg] * W + vcol + ks * 32 + g * 8);
+    }
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      settle(kf[kg][ks]);
+      settle(vf[kg][ks]);
+    }
+  step_barrier();
+
+  f32x4 dk[KG][DT], dv[KG][DT];
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dk[kg][d] = dv[kg][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int it = 0; it < total; ++it) {
+    if (it + NS - 1 < total) issue(it + NS - 1);
+    const char* st = smem + (it % NS) * STG;
+    const int qb = qb0 + it % nq;
+    // (wave-uniform) the tile's last query row is before this wave's first key: nothing to add
+    if (qb * BQ + BQ - 1 >= k0w) {
+      const char* qt = st;
+      const char* ot = st + TILE;
+      const uint32_t qbase = lds_addr(qt), obase = lds_addr(ot);
+      const float* lse_s = (const float*)(st + 2 * TILE);
+      const float* del_s = lse_s + 64;
+      const bool diag = qb * BQ < k0w + 32;
+      f32x4 p[KG][4], ds[KG][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x4 sacc[KG], dpacc[KG];
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) sacc[kg] = dpacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 qa = frag_rows<DH>(qt, 16 * t, ks, lane), oa = frag_rows<DH>(ot, 16 * t, ks, lane);
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            sacc[kg] = mfma(qa, kf[kg][ks], sacc[kg]);    // D[q][key]
+            dpacc[kg] = mfma(oa, vf[kg][ks], dpacc[kg]);  // D[q][key]
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * t + 4 * g + r;
+          const float lv = lse_s[ql], dl = del_s[ql];
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            p[kg][t][r] = fexp2(fmaf(sacc[kg][r], c, -lv));
+            ds[kg][t][r] = dpacc[kg][r] - dl;
+          }
+        }
+      }
+      if (diag) {  // causal mask where the tile meets this wave's keys (wave-uniform branch)
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (qb * BQ + 16 * t + 4 * g + r < mykey[kg]) p[kg][t][r] = 0.f;
+      }
+      bf16x8 p0[KG], p1[KG], d0[KG], d1[KG];
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ds[kg][t][r] *= p[kg][t][r];
+        p0[kg] = pack_pair(p[kg][0], p[kg][1]);
+        p1[kg] = pack_pair(p[kg][2], p[kg][3]);
+        d0[kg] = pack_pair(ds[kg][0], ds[kg][1]);
+        d1[kg] = pack_pair(ds[kg][2], ds[kg][3]);
+      }
+#pragma unroll
+      for (int e0 = 0; e0 < DT; e0 += DB) {
+        TrPair fo[DB][2], fq[DB][2];
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const uint32_t lo = obase + troff[e0 + d], lq = qbase + troff[e0 + d];
+          fo[d][0] = frag_cols_at<DH, 0>(lo);
+          fo[d][1] = frag_cols_at<DH, 32>(lo);
+          fq[d][0] = frag_cols_at<DH, 0>(lq);
+          fq[d][1] = frag_cols_at<DH, 32>(lq);
+        }
+        lgkm_wait0();
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const bf16x8 o0 = tr_use(fo[d][0]), o1 = tr_use(fo[d][1]);
+          const bf16x8 q0 = tr_use(fq[d][0]), q1 = tr_use(fq[d][1]);
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            dv[kg][e0 + d] = mfma(o0, p0[kg], dv[kg][e0 + d]);
+            dv[kg][e0 + d] = mfma(o1, p1[kg], dv[kg][e0 + d]);
+            dk[kg][e0 + d] = mfma(q0, d0[kg], dk[kg][e0 + d]);
+            dk[kg][e0 + d] = mfma(q1, d1[kg], dk[kg][e0 + d]);
+          }
+        }
+      }
+    }
+    if (it + 1 < total && !(a.diag & 1)) wait_vm_upto(PER * (min(it + NS - 1, total - 1) - it - 1));
+    step_barrier();
+  }
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    if (qs > 1) {
+      float* prow = a.part + (((long long)qsub * a.B * a.T + (long long)b * a.T + mykey[kg]) * a.Hkv + kvh) * (2 * DH);
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        *(f32x4*)(prow + 16 * d + 4 * g) = f32x4{dk[kg][d][0] * a.scale, dk[kg][d][1] * a.scale,
+                                                 dk[kg][d][2] * a.scale, dk[kg][d][3] * a.scale};
+        *(f32x4*)(prow + DH + 16 * d + 4 * g) = dv[kg][d];
+      }
+      continue;
+    }
+    bf16_t* krow = a.dqkv + ((long long)b * a.T + mykey[kg]) * W;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      *(uint2*)(krow + kcol + 16 * d + 4 * g) = make_uint2(pack_bf2(dk[kg][d][0] * a.scale, dk[kg][d][1] * a.scale),
+                                                           pack_bf2(dk[kg][d][2] * a.scale, dk[kg][d][3] * a.scale));
+      *(uint2*)(krow + vcol + 16 * d + 4 * g) =
+          make_uint2(pack_bf2(dv[kg][d][0], dv[kg][d][1]), pack_bf2(dv[kg][d][2], dv[kg][d][3]));
+    }
+    if (a.cs_ws) {
+      float* crow = a.cs_ws + (((long long)b * a.T + k0w + 16 * kg) >> 4) * W;
+      wave_colsum16<DT>(dk[kg], a.scale, crow + kcol, lane);
+      wave_colsum16<DT>(dv[kg], 1.f, crow + vcol, lane);
+    }
+  }
+}
+
 // dK | dV rows from the qs fp32 partials of a head-split dK/dV pass: dqkv[b, t, K|V cols] =
 // bf16(sum over qsub in order).  Block = 16 rows x 1024 columns of the [Hkv][2*Dh] partial row
 // (blockIdx.y picks the column half when Hkv*2*Dh = 2048); thread = 4 columns, 16-B loads.  With
@@ -933,9 +1123,17 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   a.part = part; a.qs = qs;
   dim3 g1(T / 64, B * Hkv * qs), g2(T / 64, B * H);
   const int ns = fa_ns(Dh);
+  // dK/dV at Dh = 64: 32 keys per wave (bwd_dkdv2_kernel) unless RTDC_FA_DKDV=1 (16 keys per wave)
+  const char* dkdv_env = getenv("RTDC_FA_DKDV");  // (read per call: tests A/B it in one process)
+  const int dkdv_v = dkdv_env ? atoi(dkdv_env) : 2;
   if (Dh == 64) {
     FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
-    FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
+    if (dkdv_v == 2 && T % 128 == 0) {
+      dim3 g3(T / 128, B * Hkv * qs);
+      FA_DISPATCH(fa::bwd_dkdv2_kernel, 64, ns, g3, a);
+    } else {
+      FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
+    }
   } else {
     FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
     FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);

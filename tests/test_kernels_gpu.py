@@ -793,3 +793,28 @@ def test_flash_dkdv_head_split_matches_unsplit_and_reference(monkeypatch, Dh, qs
     _close(a[..., C:C + Hkv * Dh], qr.grad[..., C:C + Hkv * Dh], 3e-2)
     _close(a[..., C + Hkv * Dh:], qr.grad[..., C + Hkv * Dh:], 3e-2)
     _close(cs_a, a.view(-1, W).float().sum(0), 1e-5)
+
+
+@pytest.mark.parametrize("H,Hkv,T", [(4, 4, 256), (4, 2, 512), (2, 2, 1024)])
+def test_flash_dkdv_32_keys_per_wave_equals_16(monkeypatch, H, Hkv, T):
+    """The Dh = 64 dK/dV kernel with two 16-key groups per wave (bwd_dkdv2_kernel) computes
+    every key's dK / dV with the same MFMA sequence as the 16-keys-per-wave kernel (the extra
+    fully-masked q block adds exact zeros): bitwise equal gradients, colsum partials included."""
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(T + H)
+    Dh, Bn = 64, 2
+    W = (H + 2 * Hkv) * Dh
+    qkv0 = _bf(Bn, T, W)
+    g = _bf(Bn, T, H * Dh)
+    out = {}
+    for v in ("1", "2"):
+        monkeypatch.setenv("RTDC_FA_DKDV", v)
+        qkv = qkv0.clone().requires_grad_(True)
+        causal_attention(qkv, H, Hkv).backward(g)
+        cs = G.colsum(qkv.grad.view(-1, W))
+        torch.cuda.synchronize()
+        out[v] = (qkv.grad.clone(), cs.clone())
+    assert torch.equal(out["1"][0], out["2"][0])
+    _close(out["1"][1], out["2"][1], 1e-6)

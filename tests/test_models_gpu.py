@@ -22,9 +22,9 @@ def test_gpt2_tiny_matches_reference_and_trains():
     loss.backward()
     assert abs(loss.item() - loss_ref.item()) < 0.02 * loss_ref.item()
     for (n, p), (_, q) in zip(ref.named_parameters(), gpu.named_parameters()):
-        err = (p.grad - q.grad.cpu()).abs().max().item()
-        mag = p.grad.abs().max().item() + 1e-8
-        assert err < 0.08 * mag, f"{n}: grad err {err} vs {mag}"
+        # relative-norm error of the whole gradient (bf16 activations vs the fp32 CPU path)
+        err = ((p.grad - q.grad.cpu()).norm() / (p.grad.norm() + 1e-12)).item()
+        assert err < 0.02, f"{n}: relative grad error {err:.3e}"
     opt = FusedAdamW(gpu.parameters(), lr=3e-3, weight_decay=0.0)
     data = torch.randint(0, cfg.vocab_size, (4, 129), device="cuda")
     losses = []
@@ -58,8 +58,8 @@ def test_gpt2_tied_embedding_grad_in_flat_space():
         gpu(idx.cuda(), idx.roll(-1, 1).cuda()).backward()
         g, r = gpu.wte.grad.cpu(), ref.wte.grad
         assert gpu.wte.grad.data_ptr() == opt.flat_space.grad_view(gpu.wte).data_ptr()
-        err = (g - r).abs().max().item()
-        assert err < 0.08 * r.abs().max().item(), err
+        err = ((g - r).norm() / r.norm()).item()
+        assert err < 0.02, err
 
 
 def test_toy_mlp_native_fp32():
@@ -134,9 +134,9 @@ def test_llama_tiny_matches_reference_and_trains():
     loss.backward()
     assert abs(loss.item() - loss_ref.item()) < 0.02 * loss_ref.item()
     for (n, p), (_, q) in zip(ref.named_parameters(), gpu.named_parameters()):
-        err = (p.grad - q.grad.cpu()).abs().max().item()
-        mag = p.grad.abs().max().item() + 1e-8
-        assert err < 0.08 * mag, f"{n}: grad err {err} vs {mag}"
+        # relative-norm error of the whole gradient (bf16 activations vs the fp32 CPU path)
+        err = ((p.grad - q.grad.cpu()).norm() / (p.grad.norm() + 1e-12)).item()
+        assert err < 0.02, f"{n}: relative grad error {err:.3e}"
     opt = FusedAdamW(gpu.parameters(), lr=3e-3, weight_decay=0.0)
     data = torch.randint(0, cfg.vocab_size, (2, 129), device="cuda")
     losses = []
