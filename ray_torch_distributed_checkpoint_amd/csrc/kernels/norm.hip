@@ -365,123 +365,6 @@ __global__ __launch_bounds__(256) void norm_bwd4_kernel(
   }
 }
 
-// norm_bwd4_kernel with RB rows in flight per wave: a wave issues the loads of RB consecutive
-// rows at once, then reduces and writes them in order.  The 1-row software pipeline above
-// keeps ~1 row per wave in flight at ~3 waves per SIMD - a latency-bound stream (GPT-2's
-// 16384 x 768 LayerNorm backward moved 100 MB in ~50 us, half of what the forward streams);
-// RB rows per wave multiply the bytes in flight at the same occupancy.  Same math, the same
-// per-block partial rows (block-ordered, deterministic) as norm_bwd4_kernel.
-template <int CPL, bool RMS, bool CS, int RB>
-__global__ __launch_bounds__(256) void norm_bwd4g_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
-    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ ws_dg,
-    float* __restrict__ ws_db, float* __restrict__ ws_cs, int M, int D) {
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int nw = gridDim.x * 4;
-  const int nch = D >> 2;
-  float adg[CPL][4], adb[CPL][4], acs[CS ? CPL : 1][4];
-#pragma unroll
-  for (int i = 0; i < CPL; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) adg[i][e] = adb[i][e] = 0.f;
-#pragma unroll
-  for (int i = 0; i < (CS ? CPL : 1); ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acs[i][e] = 0.f;
-  float gg[CPL][4];
-#pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) ld4b(g + c * 4, gg[i]);
-  }
-  for (int r0 = gw * RB; r0 < M; r0 += nw * RB) {
-    uint2 cx[RB][CPL], cd[RB][CPL], cr[RB][CPL];
-    float mean[RB], rstd[RB];
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int row = min(r0 + j, M - 1);  // (a clamped row is loaded but never written)
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nch) {
-          cx[j][i] = *(const uint2*)(x + (long long)row * D + c * 4);
-          cd[j][i] = *(const uint2*)(dy + (long long)row * D + c * 4);
-          if (dres) cr[j][i] = *(const uint2*)(dres + (long long)row * D + c * 4);
-        }
-      }
-      mean[j] = RMS ? 0.f : mean_in[row];
-      rstd[j] = rstd_in[row];
-    }
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int row = r0 + j;
-      if (row >= M) break;  // (wave-uniform)
-      float xh[CPL][4], dxh[CPL][4];
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nch) {
-          float xv[4], dv[4];
-          unpack4(cx[j][i], xv);
-          unpack4(cd[j][i], dv);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            xh[i][e] = (xv[e] - mean[j]) * rstd[j];
-            dxh[i][e] = dv[e] * gg[i][e];
-            s1 += dxh[i][e];
-            s2 += dxh[i][e] * xh[i][e];
-            adg[i][e] += dv[e] * xh[i][e];
-            adb[i][e] += dv[e];
-          }
-        }
-      }
-      const float m1 = RMS ? 0.f : wave_sum(s1) / D;
-      const float m2 = wave_sum(s2) / D;
-      bf16_t* dxr = dx + (long long)row * D;
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nch) {
-          float o[4], r[4];
-          if (dres) unpack4(cr[j][i], r);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            o[e] = rstd[j] * (dxh[i][e] - m1 - xh[i][e] * m2);
-            if (dres) o[e] += r[e];
-            if constexpr (CS) acs[i][e] += o[e];
-          }
-          *(uint2*)(dxr + c * 4) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
-        }
-      }
-    }
-  }
-  extern __shared__ float red[];
-  constexpr int KCS = RMS ? 1 : 2;
-  const int wv = threadIdx.x >> 6;
-  for (int w = 0; w < 4; ++w) {
-    if (wv == w) {
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nch) {
-          red_acc4(red, c, adg[i], w);
-          if (!RMS) red_acc4(red, D / 4 + c, adb[i], w);
-          if constexpr (CS) red_acc4(red, KCS * D / 4 + c, acs[i], w);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  for (int d = threadIdx.x; d < D; d += 256) {
-    ws_dg[(long long)blockIdx.x * D + d] = red[d];
-    if (!RMS) ws_db[(long long)blockIdx.x * D + d] = red[D + d];
-    if constexpr (CS) ws_cs[(long long)blockIdx.x * D + d] = red[KCS * D + d];
-  }
-}
-
 // out[d] (+)= sum_w ws[w][d], fixed summation order.  A block owns 64 columns; its 4 waves
 // stride over the W partial rows (coalesced 256-B rows per wave) and combine through LDS,
 // so a 1024 x 768 workspace is 12 blocks x 256 loads per lane instead of 768 serial chains.
@@ -733,12 +616,10 @@ static int resident_blocks(size_t lds) {
 }
 
 template <bool RMS, bool CS>
-static int resident_blocks4(size_t lds, int cpl4, bool grouped = false) {
+static int resident_blocks4(size_t lds, int cpl4) {
   static int cus = 0;
   static int occ[5] = {0, 0, 0, 0, 0};
   static size_t occ_lds[5] = {~(size_t)0, ~(size_t)0, ~(size_t)0, ~(size_t)0, ~(size_t)0};
-  static int occ_g = 0;
-  static size_t occ_g_lds = ~(size_t)0;
   if (cus == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -746,15 +627,6 @@ static int resident_blocks4(size_t lds, int cpl4, bool grouped = false) {
       cus = 256;
   }
   if (cpl4 < 1 || cpl4 > 4) return cus;
-  if (grouped && cpl4 == 3) {  // norm_bwd4g_kernel (more registers: fewer blocks per CU)
-    if (lds != occ_g_lds) {
-      int o = 0;
-      const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, norm_bwd4g_kernel<3, RMS, CS, 4>, 256, lds);
-      occ_g = (e != hipSuccess || o <= 0) ? 1 : o;
-      occ_g_lds = lds;
-    }
-    return cus * occ_g;
-  }
   if (lds != occ_lds[cpl4]) {
     hipError_t e = hipErrorInvalidValue;
     int o = 0;
@@ -790,14 +662,7 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
   // (GPT-2: 1024 blocks on 768 slots ran 0.94 ms/step of LayerNorm backward, 768 blocks 0.67)
 #define RB(C) (cs ? resident_blocks<C, RMS, true>(lds) : resident_blocks<C, RMS, false>(lds))
   const int cpl4 = (D / 4) / 64;
-  static int rb_env = -1;  // RTDC_NORM_BWD_RB: rows in flight per wave (4: norm_bwd4g_kernel, 0: 1-row pipeline)
-  if (rb_env < 0) {
-    const char* e = getenv("RTDC_NORM_BWD_RB");
-    rb_env = e ? atoi(e) : 4;
-  }
-  const bool grouped = vw4 && rb_env == 4 && cpl4 == 3;
-  const int slots = vw4 ? (cs ? resident_blocks4<RMS, true>(lds, cpl4, grouped)
-                              : resident_blocks4<RMS, false>(lds, cpl4, grouped))
+  const int slots = vw4 ? (cs ? resident_blocks4<RMS, true>(lds, cpl4) : resident_blocks4<RMS, false>(lds, cpl4))
                         : cpl <= 1 ? RB(1) : cpl <= 2 ? RB(2) : cpl <= 4 ? RB(4) : RB(8);
 #undef RB
   const int nblk = nwaves / 4 < slots ? nwaves / 4 : slots;
@@ -817,13 +682,7 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
   hipLaunchKernelGGL((norm_bwd4_kernel<C, RMS, CS>), grid, block, lds, st, (const bf16_t*)dy,  \
                      (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \
                      (bf16_t*)dx, ws_dg, ws_db, ws_cs, M, D)
-#define L4G(C, CS)                                                                            \
-  hipLaunchKernelGGL((norm_bwd4g_kernel<C, RMS, CS, 4>), grid, block, lds, st, (const bf16_t*)dy, \
-                     (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,     \
-                     (bf16_t*)dx, ws_dg, ws_db, ws_cs, M, D)
-  if (grouped) {
-    if (cs) L4G(3, true); else L4G(3, false);
-  } else if (vw4) {
+  if (vw4) {
     if (cpl4 == 1) { if (cs) L4(1, true); else L4(1, false); }
     else if (cpl4 == 2) { if (cs) L4(2, true); else L4(2, false); }
     else if (cpl4 == 3) { if (cs) L4(3, true); else L4(3, false); }
@@ -836,7 +695,6 @@ static int launch_norm_bwd(const void* dy, const void* x, const void* g, const f
 #undef LC
 #undef L
 #undef L4
-#undef L4G
   if (nblk_out) {  // deferred: the caller reduces the [nz][nblk][D] partials (rtdc_colsum_multi)
     *nblk_out = nblk;
     return hipGetLastError() == hipSuccess ? 0 : 2;

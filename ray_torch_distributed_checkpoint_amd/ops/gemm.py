@@ -233,6 +233,11 @@ class _WgradGroup:
     def pending(self, t) -> bool:
         return t is not None and bool(self.ptrs) and t.data_ptr() in self.ptrs
 
+    def pending_product(self, t) -> bool:
+        """t is the output of a deferred weight-gradient PRODUCT (not a column-sum job: a
+        second claim of a bias slot is the LayerNorm-offer protocol, see colsum())."""
+        return t is not None and any(it[2].data_ptr() == t.data_ptr() for it in self.items)
+
     def _launch(self, items):
         for i in range(0, len(items), _GROUP_MAX):
             chunk = items[i:i + _GROUP_MAX]

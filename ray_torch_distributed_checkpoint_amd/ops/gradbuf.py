@@ -40,7 +40,10 @@ def grad_target(p: torch.Tensor | None) -> torch.Tensor | None:
 def _flush_if_pending(view: torch.Tensor) -> None:
     from .gemm import _WG, flush_wgrads
 
-    if _WG.pending(view):
+    # only a deferred PRODUCT overwrites its slice at the flush; a pending column-sum job into a
+    # bias slot claimed twice is the LayerNorm offer protocol (ops/gemm.py colsum), which
+    # retargets the job instead of reading the slot
+    if _WG.pending_product(view):
         flush_wgrads()
 
 
