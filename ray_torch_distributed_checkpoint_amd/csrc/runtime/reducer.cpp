@@ -272,7 +272,9 @@ class GradBucketEngine {
   // widen event (bf16 communication), the P2P done event, or - averaging backends - the
   // collective itself (Work::wait on a CUDA-like backend orders the current stream after it).
   // Backends that need the finalize() post-scale (SUM without a widen pass) cannot do this.
-  bool can_stream_wait() const { return flat_.is_cuda() && !zero_world_ && (use_avg_ || side_.has_value()); }
+  bool can_stream_wait() const {
+    return flat_.is_cuda() && !zero_world_ && (use_avg_ || side_.has_value() || post_scale_ == 1.0);
+  }
   void stream_wait_bucket(int64_t b) {
     TORCH_CHECK(can_stream_wait(), "stream_wait_bucket: needs a device buffer, no ZeRO, and AVG or bf16 comm");
     TORCH_CHECK(b >= 0 && (size_t)b < works_.size() && launched_[b], "stream_wait_bucket: bucket not launched");

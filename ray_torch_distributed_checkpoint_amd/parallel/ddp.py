@@ -117,7 +117,11 @@ class DistributedDataParallel(nn.Module):
             self.space = FlatParamSpace(order, align_after=align)
         dev = self.space.device
         backend = dist.get_backend(process_group) if dist.is_initialized() else "gloo"
-        self._use_avg = backend == "nccl"
+        # RCCL averages inside the collective (ReduceOp.AVG = PreMulSum).  On a 1-rank group
+        # (force_collectives rehearsal) the average is the identity, but RCCL still runs its
+        # oneRankReduce<PreMulSum> pass over every bucket (measured 0.87 ms per GPT-2 step in
+        # bf16, profiles/comm_bf16_1rank_r4.txt): SUM there, which RCCL treats as in-place no-op.
+        self._use_avg = backend == "nccl" and self.world_size > 1
         # one flat broadcast of all parameters from rank 0
         if self._collective:
             dist.broadcast(self.space.data, src=0, group=process_group)
@@ -411,7 +415,7 @@ class DistributedDataParallel(nn.Module):
             b.work = None
             b.launched = False
             b.pending = len(b.params)
-        if not self._use_avg:
+        if not self._use_avg and self.world_size > 1:
             with torch.no_grad():
                 self.space.grad.mul_(1.0 / self.world_size)
         self.space.attach_grad_views()

@@ -303,8 +303,8 @@ def _shared_grads(group_on: bool, x, tied_head: bool):
         sp = FlatParamSpace([w2, w])
         sp.zero_grad(set_to_none=True)
         if tied_head:
-            ids = (x[:, 0].abs() * 1000).long() % 1024
-            h = ops.embedding(ids, w) if hasattr(ops, "embedding") else torch.nn.functional.embedding(ids, w)
+            ids = ((x[:, 0].float().abs() * 1000).long() % 1024).view(4, 1024)  # [B, T] token ids
+            h = ops.embedding(ids, w)
             h = ops.linear(h.bfloat16(), w2)
             y = ops.linear(h, w)  # head tied to the embedding table
         else:
