@@ -21,6 +21,7 @@ the restore wall-clock (sharded read + RCCL broadcast into the live model/optimi
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import shutil
@@ -342,27 +343,34 @@ def comm_sweep(args, model, opt, net, cur, step, world, sync) -> list:
 
     out = []
     net.detach()
-    for dtype in ("fp32", "bf16"):
-        for cap in (16.0, 32.0, 64.0, 128.0):
-            w = DistributedDataParallel(model, bucket_cap_mb=cap, defer_tail_to_optimizer=True, grad_comm_dtype=dtype,
-                                        force_collectives=args.force_dist)
-            cur["net"] = w
-            for i in range(2):  # warm: lazy workspaces, the engine's first bucket plan
-                step(i)
+    cells = [(d, c) for d in ("fp32", "bf16") for c in (16.0, 32.0, 64.0, 128.0)]
+    if os.environ.get("RTDC_SWEEP_CELLS"):  # e.g. "bf16:32,fp32:64" (A/B of single cells)
+        cells = [(d, float(c)) for d, c in (x.split(":") for x in os.environ["RTDC_SWEEP_CELLS"].split(","))]
+    for dtype, cap in cells:
+        w = DistributedDataParallel(model, bucket_cap_mb=cap, defer_tail_to_optimizer=True, grad_comm_dtype=dtype,
+                                    force_collectives=args.force_dist)
+        cur["net"] = w
+        for i in range(2):  # warm: lazy workspaces, the engine's first bucket plan
+            step(i)
+        # three windows of 5 steps, the fastest one reported (plus the mean): one host hiccup
+        # inside a single short window would otherwise move a whole cell
+        gc.collect()
+        times = []
+        for rep in range(3):
             sync()
             dist.barrier()
             t0 = time.perf_counter()
-            n = 10
+            n = 5
             for i in range(n):
                 step(i)
             sync()
             dist.barrier()
-            dt = (time.perf_counter() - t0) / n
-            tt = torch.tensor([dt], device=sp_device(model))
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            out.append({"bucket_cap_mb": cap, "grad_comm_dtype": dtype, "buckets": len(w.buckets),
-                        "ms_per_step": round(tt.item() * 1e3, 3)})
-            w.detach()
+            times.append((time.perf_counter() - t0) / n)
+        tt = torch.tensor([min(times), sum(times) / len(times)], device=sp_device(model))
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        out.append({"bucket_cap_mb": cap, "grad_comm_dtype": dtype, "buckets": len(w.buckets),
+                    "ms_per_step": round(tt[0].item() * 1e3, 3), "ms_per_step_mean": round(tt[1].item() * 1e3, 3)})
+        w.detach()
     cur["net"] = net
     return out
 

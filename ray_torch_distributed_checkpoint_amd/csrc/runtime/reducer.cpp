@@ -28,6 +28,7 @@
 #include <torch/csrc/distributed/c10d/Work.hpp>
 
 #include <memory>
+#include <mutex>
 
 #include "p2p_comm.cpp"
 
@@ -37,6 +38,22 @@ int rtdc_bf16_to_f32(const void* x, float* y, long long n, float scale, hipStrea
 }
 
 namespace rtdc_ddp {
+
+// One widen stream and one P2P stream per device for the whole process, shared by every
+// engine.  A pool stream per engine made each re-wrap (bench.py's bucket sweep) create a new
+// HIP stream; past GPU_MAX_HW_QUEUES (4) streams share hardware queues round-robin, and a
+// widen stream that lands on the compute stream's queue parks the compute kernels behind its
+// wait on the all-reduce: +2..8 ms/step on the 2nd..4th bf16 wrap of GPT-2 (r4 sweep).
+enum SharedStream { kWiden = 0, kP2P = 1 };
+inline c10::hip::HIPStreamMasqueradingAsCUDA shared_stream(SharedStream kind, int dev) {
+  static std::mutex mu;
+  static std::vector<c10::optional<c10::hip::HIPStreamMasqueradingAsCUDA>> streams[2];
+  std::lock_guard<std::mutex> lock(mu);
+  auto& v = streams[kind];
+  if ((int)v.size() <= dev) v.resize(dev + 1);
+  if (!v[dev]) v[dev].emplace(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true, dev));
+  return *v[dev];
+}
 
 class GradBucketEngine {
  public:
@@ -57,8 +74,7 @@ class GradBucketEngine {
                       lp_.device() == flat_.device() && lp_.is_contiguous(),
                   "comm buffer: contiguous bf16 twin of the flat gradient buffer");
       if (flat_.is_cuda()) {
-        side_.emplace(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true,
-                                                                      flat_.device().index()));
+        side_.emplace(shared_stream(kWiden, flat_.device().index()));
         events_.resize(nb, nullptr);
         for (auto& e : events_) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
                                             "hipEventCreate");
@@ -247,7 +263,7 @@ class GradBucketEngine {
     p2p_max_bytes_ = max_bytes;
     const size_t nb = works_.size();
     if (!p2p_stream_)
-      p2p_stream_.emplace(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true, flat_.device().index()));
+      p2p_stream_.emplace(shared_stream(kP2P, flat_.device().index()));
     if (p2p_ready_.empty()) {
       p2p_ready_.resize(nb, nullptr);
       p2p_done_.resize(nb, nullptr);
