@@ -25,6 +25,20 @@ SHAPES = [  # (name, M tokens, in K, out N)
     ("lm_head", 16384, 768, 50304),
     ("sq4096", 4096, 4096, 4096),
 ]
+LLAMA_SHAPES = [  # Llama-3-8B decoder layer at 1 x 2048 tokens (GQA 32/8 heads, SwiGLU 14336)
+    ("l_qkv", 2048, 4096, 6144),
+    ("l_o", 2048, 4096, 4096),
+    ("l_gate_up", 2048, 4096, 28672),
+    ("l_down", 2048, 14336, 4096),
+]
+
+
+def _mm_f32(a, b):
+    """hipBLASLt bf16 x bf16 -> fp32 output (what our weight-gradient kernels write)."""
+    try:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    except (RuntimeError, TypeError):
+        return (a @ b).float()
 
 
 def timeit(fn, reps):
@@ -56,13 +70,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--set", default="gpt2", choices=["gpt2", "llama", "all"])
     ap.add_argument("--sweep", action="store_true", help="also time forced tile configurations (all layouts)")
     ap.add_argument("--cfgs", default="0,6,7", help="tile configurations for --sweep")
     args = ap.parse_args()
     torch.manual_seed(0)
     warm_up_clocks()
     res = []
-    for name, M, K, N in SHAPES:
+    shapes = {"gpt2": SHAPES, "llama": LLAMA_SHAPES, "all": SHAPES + LLAMA_SHAPES}[args.set]
+    for name, M, K, N in shapes:
         if args.only and args.only != name:
             continue
         xs = float(os.environ.get("GEMM_BENCH_XSCALE", "1"))  # e.g. 0.05: model-like magnitudes
@@ -87,6 +103,8 @@ def main():
             ("dgrad_gelu", lambda: G.linear_dgrad(dy, w, G.ACT_GELU_BWD, aux_in=x), lambda: dy @ w),
             ("dgrad", lambda: G.linear_dgrad(dy, w), lambda: dy @ w),
             ("wgrad", lambda: G.linear_wgrad(dy, x), lambda: (dy.t() @ x)),
+            # same product, hipBLASLt writing fp32 like our kernel does
+            ("wgrad_f32out", lambda: G.linear_wgrad(dy, x), lambda: _mm_f32(dy.t(), x)),
         ]:
             # interleaved rounds, best of each: neither side is always timed first
             t_o = t_r = float("inf")

@@ -295,9 +295,25 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& a, f32x4 (&acc)[2]
 // outstanding glds instructions allowed (wave-uniform): counted waits are immediates
 __device__ __forceinline__ void wait_vm(int allowed) {
   if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (allowed >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (allowed >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (allowed == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if (allowed == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (allowed == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (allowed == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (allowed == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// glds instructions per wave of events first..last (event kinds e & 3: 0 A-lo, 1 B-lo, 2 B-hi,
+// 3 A-hi): an A half is 16 KiB = 2 per wave, a B half CB (64-row halves of the 256x128 tile: 1)
+template <int CB>
+__device__ __forceinline__ int ev_loads(int first, int last) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int x = first + i;
+    if (x <= last) n += ((x & 3) == 1 || (x & 3) == 2) ? CB : 2;
+  }
+  return n;
 }
 
 // The kernel body over one (tile, K-slice): `bid` = the product's flat tile id, `ks` = the split-K
@@ -305,8 +321,11 @@ __device__ __forceinline__ void wait_vm(int allowed) {
 // group of independent products in one launch.
 template <bool AK, bool BKM, typename OutT, int BN>
 __device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, const int ks) {
-  // BN = 256: waves 2 (A) x 4 (B), quadrant 64x32; BN = 192: waves 4 x 2, quadrant 32x48
+  // BN = 256: waves 2 (A) x 4 (B), quadrant 64x32; BN = 192: waves 4 x 2, quadrant 32x48;
+  // BN = 128: waves 4 x 2, quadrant 32x32 (M = 2048 products with N = 4096: 8 x 32 = 256
+  // tiles, one full round of the chip where 256x256 tiles leave half of it idle)
   constexpr int BH = BN / 2, WA = BN == 256 ? 2 : 4, WB = 8 / WA;
+  constexpr int CB = BN == 128 ? 1 : 2;  // glds per wave of one B half
   constexpr int SA = 128 / WA, SB = BH / WB, TMQ = SA / 16, TNQ = SB / 16;
   constexpr int BHALF = BH * 128, BUF = 2 * HALF + 2 * BHALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024];  // [buf][A-lo, A-hi, B-lo, B-hi] + junk
@@ -332,7 +351,7 @@ __device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, con
   const int total_ev = 4 * nt;
 
   Stager<AK, 128, 8> sa0, sa1;
-  using SBT = std::conditional_t<BN == 256, Stager<BKM, 128, 8>, Half96Stager<BKM>>;
+  using SBT = std::conditional_t<BN == 192, Half96Stager<BKM>, Stager<BKM, BH, 8>>;
   SBT sb0, sb1;
   sa0.init(a.A, a.lda, a.M, m0, wave, lane);
   sa1.init(a.A, a.lda, a.M, m0 + 128, wave, lane);
@@ -347,9 +366,9 @@ __device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, con
     char* base = smem + (j & 1) * BUF;
     if (kind == 0) sa0.issue(k0, base, wave);
     else if (kind == 3) sa1.issue(k0, base + HALF, wave);
-    else if constexpr (BN == 256) {
+    else if constexpr (BN != 192) {
       if (kind == 1) sb0.issue(k0, base + 2 * HALF, wave);
-      else sb1.issue(k0, base + 3 * HALF, wave);
+      else sb1.issue(k0, base + 2 * HALF + BHALF, wave);
     } else {
       if (kind == 1) sb0.issue(k0, base + 2 * HALF, junk);
       else sb1.issue(k0, base + 2 * HALF + BHALF, junk);
@@ -370,7 +389,7 @@ __device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, con
     // prologue: A-lo(0) B-lo(0) B-hi(0) A-hi(0) A-lo(1); phase (0,1) needs events 0 and 1
 #pragma unroll
     for (int e = 0; e < 5; ++e) issue(e);
-    wait_vm(2 * (min(5, total_ev) - 2));
+    wait_vm(ev_loads<CB>(2, min(4, total_ev - 1)));
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -399,7 +418,7 @@ __device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, con
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int j = 0; j < TNQ; ++j) {
-            if constexpr (BN == 256) rb[j][ks] = load_fragx<BKM, 128>(bh, SB * wb + 16 * j, ks, lane);
+            if constexpr (BN != 192) rb[j][ks] = load_fragx<BKM, BH>(bh, SB * wb + 16 * j, ks, lane);
             else rb[j][ks] = load_frag96<BKM>(bh, SB * wb + 16 * j, ks, lane);
           }
       }
@@ -409,7 +428,7 @@ __device__ __forceinline__ void gemm8_body(const GemmArgs& a, const int bid, con
       // 3. retire what the next phase reads (p3 -> p4 reads nothing new)
       if (p != 3 && (p != 4 || t + 1 < nt) && !(RTDC_G8_DIAG & 1)) {
         const int need = p == 1 ? 4 * t + 2 : (p == 2 ? 4 * t + 3 : 4 * t + 5);
-        wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
+        wait_vm(ev_loads<CB>(need + 1, min(e, total_ev - 1)));
       }
       asm volatile("" ::: "memory");
       if (!(RTDC_G8_DIAG & 4)) __builtin_amdgcn_s_barrier();
@@ -543,7 +562,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
   if (total_kt == 0) return;
 
   Stager<AK, 128, 8> sa0, sa1;
-  using SBT = std::conditional_t<BN == 256, Stager<BKM, 128, 8>, Half96Stager<BKM>>;
+  using SBT = std::conditional_t<BN == 192, Half96Stager<BKM>, Stager<BKM, BH, 8>>;
   SBT sb0, sb1;
   auto stage_tile = [&](int s) {
     int tm, tn;
@@ -561,9 +580,9 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
     char* base = smem + ((e >> 2) & 1) * BUF;
     if (kind == 0) sa0.issue(k0, base, wave);
     else if (kind == 3) sa1.issue(k0, base + HALF, wave);
-    else if constexpr (BN == 256) {
+    else if constexpr (BN != 192) {
       if (kind == 1) sb0.issue(k0, base + 2 * HALF, wave);
-      else sb1.issue(k0, base + 3 * HALF, wave);
+      else sb1.issue(k0, base + 2 * HALF + BHALF, wave);
     } else {
       if (kind == 1) sb0.issue(k0, base + 2 * HALF, junk);
       else sb1.issue(k0, base + 2 * HALF + BHALF, junk);
@@ -1010,12 +1029,18 @@ using namespace rtdc;
 
 #ifndef RTDC_G4_ONLY  // (-DRTDC_G4_ONLY: a quick build of the 4-wave kernel alone for ISA inspection)
 // Launch the 8-phase kernel (batch 1, no causal modes).  a->splitk is honoured as set.
-// bn: 256 or 192 (output tile columns)
+// bn: 256, 192 or 128 (output tile columns; 128: bf16 output, K-major A only - else returns 1)
 extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
                                  hipStream_t st) {
   const GemmArgs& a = *args;
   const unsigned tiles = (unsigned)(((a.M + 255) / 256) * ((a.N + bn - 1) / bn));
   dim3 grid(tiles, a.splitk > 1 ? a.splitk : 1, 1), block(512);
+  if (bn == 128) {
+    if (out_fp32 || !a_kmajor) return 1;
+    if (b_kmajor) hipLaunchKernelGGL((g8::gemm8_kernel<true, true, bf16_t, 128>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((g8::gemm8_kernel<true, false, bf16_t, 128>), grid, block, 0, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
 #define G8(AK, BKM, T)                                                                      \
   do {                                                                                      \
     if (bn == 192) hipLaunchKernelGGL((g8::gemm8_kernel<AK, BKM, T, 192>), grid, block, 0, st, a); \

@@ -622,6 +622,16 @@ static bool gemm4w_enabled() {
   return v == 1;
 }
 
+// RTDC_GEMM_FEW_ROWS=0 keeps pick_cfg's choice for M <= 4096 products (A/B of pick_cfg_few_rows).
+static bool few_rows_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTDC_GEMM_FEW_ROWS");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // Persistent 8-wave kernel (gemm_8ph.hip gemm8p_kernel) for plain-K (no split-K) products with
 // more tiles than CUs: the next tile's loads and this tile's epilogue overlap MFMA work instead
 // of costing a prologue/epilogue bubble per tile (K = 768 GPT-2 products: 12 K-tiles per tile).
@@ -663,6 +673,37 @@ static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, doub
   return best;
 }
 
+// Few-row-tile products (M <= 4096: Llama-3-8B at 2048 tokens per GPU) with a K-major A and a
+// bf16 output: choose among the 8-wave tiles by a wave-quantised time model instead of the
+// M = 16384 rules of pick_cfg.  At M = 2048 an N = 4096 output is only 128 tiles of 256x256 -
+// half of the 256 CUs idle - and the right answer differs per product: 256x128 tiles (one full
+// round), 256x256 tiles with two K slices, or 256x192.  Per-K-tile block times (us) from
+// benchmarks/gemm_bench.py --set llama --sweep (profiles/gemm_llama_sweep_r4.jsonl):
+//   256x256  1.74 (1.58 persistent, > 256 tiles)   256x192  1.42 fwd / 1.37 dgrad
+//   256x128  1.10 fwd / 1.16 dgrad
+// Returns the cfg (6 / 7 / 11), or -1 when the product is outside this regime.
+static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
+  const int kt = a.K / gemm::BK, tm = (a.M + 255) / 256;
+  const double slab_us = (double)a.M * a.N * 8.0 / 4.0e6;
+  auto est = [&](int bn, double t_k) {
+    const long long tiles = (long long)tm * ((a.N + bn - 1) / bn);
+    double best = 1e30;
+    for (int s = 1; s <= (can_split ? 8 : 1); ++s) {
+      if (s > 1 && (kt / s < 8 || tiles >= 200 || (long long)s * a.M * a.N > a.ws_elems)) break;
+      const long long waves = (tiles * s + 255) / 256;
+      const double t = (double)waves * ((kt + s - 1) / s) * t_k + (s > 1 ? s * slab_us : 0.0);
+      best = t < best ? t : best;
+    }
+    return best;
+  };
+  const long long t6 = (long long)tm * ((a.N + 255) / 256);
+  const double e6 = est(256, b_kmajor && t6 > 256 ? 1.58 : 1.74);
+  const double e7 = (b_kmajor || a.K <= 4096) ? est(192, b_kmajor ? 1.42 : 1.37) : 1e30;
+  const double e11 = est(128, b_kmajor ? 1.10 : 1.16);
+  if (e11 < e6 && e11 < e7) return 11;
+  return e7 < e6 ? 7 : 6;
+}
+
 // cs_rows_out (optional): with cs_ws set and cs_out null the column sums are DEFERRED - the
 // 8-wave gelu-backward epilogue leaves its partial rows in cs_ws, *cs_rows_out = their count
 // (0: this kernel choice wrote none; the caller reduces C itself).
@@ -672,34 +713,41 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   GemmArgs a = *args;
   if (a.K % gemm::BK != 0 || a.M % 8 != 0 || a.N % 8 != 0) return 1;
   int cfg = pick_cfg(a, batch, a_kmajor, b_kmajor);
+  if (a.tile_cfg < 0 && few_rows_enabled() && batch == 1 && a.causal == 0 && a_kmajor && !out_fp32 &&
+      a.M >= 256 && a.M <= 4096 && a.N >= 128 && a.K >= 8 * gemm::BK) {
+    const bool plain = a.act == 0 && a.bias_type == 0 && !a.cs_out && !a.cs_ws;
+    cfg = pick_cfg_few_rows(a, b_kmajor, plain && a.ws != nullptr);
+  }
   if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4w_enabled()) cfg = 10;
   // the 8-wave kernels write bf16 outputs 16 B at a time through tile-relative 32-bit buffer
   // offsets (gemm_8ph.hip tile_epilogue)
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
                        (uintptr_t)a.bias;
-  if (cfg >= 6 && cfg <= 10 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
+  if (cfg >= 6 && cfg <= 11 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
   long long tiles = cfg == 3 ? ntiles<Cfg256x256>(a) : cfg == 1 ? ntiles<Cfg256x128>(a)
                   : cfg == 2 ? ntiles<Cfg128x256>(a) : cfg == 4 ? ntiles<Cfg256x64>(a)
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
-  const bool big = cfg >= 6 && cfg <= 10;  // counted-vmcnt pipelines (gemm_8ph.hip)
-  const int bn = (cfg == 7 || cfg == 9) ? 192 : 256;
+  // cfg 11: the 8-wave kernel on 256x128 tiles (bf16 output, K-major A)
+  if (cfg == 11 && (out_fp32 || !a_kmajor)) cfg = 6;
+  const bool big = cfg >= 6 && cfg <= 11;  // counted-vmcnt pipelines (gemm_8ph.hip)
+  const int bn = (cfg == 7 || cfg == 9) ? 192 : cfg == 11 ? 128 : 256;
   if (big) {
     if (batch != 1 || a.causal != 0) return 1;
     tiles = (long long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
   }
   // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
-  if (plain && (cfg <= 7 || cfg == 10))
-    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : 1.8) : pick_splitk(a, tiles);
+  if (plain && (cfg <= 7 || cfg == 10 || cfg == 11))
+    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : cfg == 11 ? 1.0 : 1.8) : pick_splitk(a, tiles);
   if (cfg == 10) {
     const int rc = rtdc_gemm4_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
     if (rc) return rc;
   } else if (big) {
     // cfg 8 / 9 force the persistent form; 6 / 7 take it automatically where it applies
-    const bool persist = cfg >= 8 || (persist_enabled() && a.splitk == 1 && a_kmajor && b_kmajor &&
-                                      tiles > 256 && a.K >= 2 * gemm::BK);
+    const bool persist = (cfg == 8 || cfg == 9) || (cfg != 11 && persist_enabled() && a.splitk == 1 && a_kmajor &&
+                                                    b_kmajor && tiles > 256 && a.K >= 2 * gemm::BK);
     const int rc = persist ? rtdc_gemm8p_launch(&a, a_kmajor, b_kmajor, out_fp32, bn, stream)
                            : rtdc_gemm8_launch(&a, a_kmajor, b_kmajor, out_fp32, bn, stream);
     if (rc) return rc;

@@ -16,9 +16,6 @@ from .gradbuf import claimed_target, grad_target
 from .shadow import shadow_of
 
 
-_side: dict = {}
-
-
 def sort_ids(ids: torch.Tensor, num_rows: int):
     """(sorted ids, original positions) of a 1-D int64 GPU tensor of ids in [0, num_rows):
     stable, deterministic, one native kernel launch."""
@@ -31,11 +28,9 @@ def sort_ids(ids: torch.Tensor, num_rows: int):
 
 
 def _side_stream(device) -> torch.cuda.Stream:
-    s = _side.get(device)
-    if s is None:
-        s = torch.cuda.Stream(device=device)
-        _side[device] = s
-    return s
+    from .streams import side_stream
+
+    return side_stream(device)
 
 
 class _PendingSort:

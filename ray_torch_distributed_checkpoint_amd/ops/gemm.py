@@ -272,7 +272,9 @@ class _WgradGroup:
                 and not torch.cuda.is_current_stream_capturing()):
             cur = torch.cuda.current_stream(dev_t.device)
             if self.side is None:
-                self.side = torch.cuda.Stream(device=dev_t.device)
+                from .streams import side_stream
+
+                self.side = side_stream(dev_t.device)
             self.side.wait_stream(cur)  # operands written
             with torch.cuda.stream(self.side):
                 if items:
