@@ -30,7 +30,7 @@ def sort_ids(ids: torch.Tensor, num_rows: int):
 def _side_stream(device) -> torch.cuda.Stream:
     from .streams import side_stream
 
-    return side_stream(device)
+    return side_stream(device, "sort")
 
 
 class _PendingSort:

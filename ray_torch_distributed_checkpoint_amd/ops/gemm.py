@@ -136,6 +136,7 @@ def _round_split_rows(rows: int, cols: int, k: int, device) -> int:
 _GROUP_ON = os.environ.get("RTDC_WGRAD_GROUP", "1") != "0"
 _GROUP_MAX = 10       # products per launch (gemm8g_kernel G8_MAX_GROUP)
 _GROUP_TILES = 200    # products with fewer output tiles than this are deferred
+_BIG_TILES = 4096     # ... and, over a short K (< 4096 tokens), products of up to this many
 # tiles per round (one 8-wave block per CU); groups are packed up to it (RTDC_WGRAD_ROUND: A/B of
 # smaller groups that leave CUs to the compute stream's kernels while a group runs)
 _ROUND = int(os.environ.get("RTDC_WGRAD_ROUND", "256"))
@@ -144,6 +145,9 @@ _ROUND = int(os.environ.get("RTDC_WGRAD_ROUND", "256"))
 # stream joins it at the end of backward.  -0.17 ms/step on GPT-2-small
 # (profiles/wgrad_group_ab_r3.txt); RTDC_WGRAD_SIDE=0 keeps them on the compute stream.
 _GROUP_SIDE = os.environ.get("RTDC_WGRAD_SIDE", "1") != "0"
+# Short-K multi-round weight gradients packed into whole rounds (see _groupable);
+# RTDC_WGRAD_GROUP_BIG=0 launches them one by one.
+_GROUP_BIG = os.environ.get("RTDC_WGRAD_GROUP_BIG", "1") != "0"
 # Deferred column sums: the bias / LayerNorm-parameter gradients are reductions of per-block
 # partial rows; inside backward each leaves its partial rows in a buffer of its own and the
 # reductions of a whole window run as ONE launch with the grouped weight gradients' flush
@@ -201,17 +205,29 @@ class _WgradGroup:
                 return j
         return None
 
-    def add(self, dy, x2d, out, tiles) -> bool:
+    def add(self, dy, x2d, out, tiles, whole_rounds=False) -> bool:
         if not self._arm():
             return False
         # keep an alias, not `out` itself: AccumulateGrad adopts the returned tensor as p.grad
         # without a copy only while nothing else references it (otherwise it clones the still
         # unwritten buffer)
+        if whole_rounds:
+            # multi-round products (see _groupable): pack until the group is a whole number
+            # of rounds - Llama-3-8B's four products of a layer at 2048 tokens are 896 + 1792
+            # + 256 + 384 = 3328 tiles = 13 rounds, 14 when launched one by one
+            if self.items and (len(self.items) >= _GROUP_MAX or not self.items[-1][4]):
+                self.flush()
+            self.items.append((dy, x2d, out.view(out.shape), tiles, True))
+            self.tiles += tiles
+            self.ptrs.add(out.data_ptr())
+            if self.tiles % _ROUND == 0 or self.tiles > _BIG_TILES:
+                self.flush()
+            return True
         # greedy packing into rounds of the chip: launch the pending group first when this
         # product would not fit the round any more (GPT-2: 252-tile groups of 9 products)
-        if self.items and (self.tiles + tiles > _ROUND or len(self.items) >= _GROUP_MAX):
+        if self.items and (self.tiles + tiles > _ROUND or len(self.items) >= _GROUP_MAX or self.items[-1][4]):
             self.flush()
-        self.items.append((dy, x2d, out.view(out.shape), tiles))
+        self.items.append((dy, x2d, out.view(out.shape), tiles, False))
         self.tiles += tiles
         self.ptrs.add(out.data_ptr())
         if self.tiles >= _ROUND:
@@ -225,7 +241,7 @@ class _WgradGroup:
     def _launch_split(self, items):
         """A remainder far below a round (the last layer's products): each product on its own
         with split-K slabs, which spreads it over the chip."""
-        for dy, x2d, out, _ in items:
+        for dy, x2d, out, _, _ in items:
             M, N = dy.shape
             K = x2d.shape[1]
             gemm_bf16(dy, x2d, out, N, K, M, N, K, K, False, False)
@@ -242,7 +258,7 @@ class _WgradGroup:
         for i in range(0, len(items), _GROUP_MAX):
             chunk = items[i:i + _GROUP_MAX]
             dims = []
-            for dy, x2d, out, _ in chunk:
+            for dy, x2d, out, _, _ in chunk:
                 M, N = dy.shape
                 K = x2d.shape[1]
                 dims += [N, K, M, N, K, K]
@@ -274,14 +290,14 @@ class _WgradGroup:
             if self.side is None:
                 from .streams import side_stream
 
-                self.side = side_stream(dev_t.device)
+                self.side = side_stream(dev_t.device, "wgrad")
             self.side.wait_stream(cur)  # operands written
             with torch.cuda.stream(self.side):
                 if items:
                     self._launch(items)
                 if jobs:
                     self._launch_jobs(jobs)
-                for dy, x2d, _, _ in items:  # the compute stream may recycle them before the kernel ran
+                for dy, x2d, _, _, _ in items:  # the compute stream may recycle them before the kernel ran
                     dy.record_stream(self.side)
                     x2d.record_stream(self.side)
                 for j in jobs:
@@ -294,7 +310,7 @@ class _WgradGroup:
                     fn()
             return
         if items:
-            if join and sum(it[3] for it in items) * 2 < _ROUND:
+            if join and sum(it[3] for it in items) * 2 < _ROUND and not any(it[4] for it in items):
                 self._launch_split(items)
             else:
                 self._launch(items)
@@ -335,7 +351,9 @@ def when_grad_ready(p: torch.Tensor, fn) -> None:
 
 def _groupable(dy, x2d, out, accumulate, alpha, alpha_dev) -> int:
     """Tiles of a weight gradient that may be deferred into a grouped launch, else 0: plain
-    products that would otherwise split K (fewer than 200 output tiles, long K)."""
+    products that would otherwise split K (fewer than 200 output tiles, long K), or - over a
+    short K (M < 4096 tokens: Llama-3-8B at 2048 per GPU) - multi-round products that are
+    packed into whole rounds of the chip (returned negative)."""
     if not (_GROUP_ON and dy.is_cuda and out is not None and not accumulate and alpha == 1.0 and alpha_dev is None
             and out.dtype == torch.float32 and out.is_contiguous() and dy.is_contiguous() and x2d.is_contiguous()
             and dy.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16):
@@ -343,12 +361,14 @@ def _groupable(dy, x2d, out, accumulate, alpha, alpha_dev) -> int:
     M, N = dy.shape
     K = x2d.shape[1]
     tiles = ((N + 255) // 256) * ((K + 255) // 256)
-    if M % 64 or N % 8 or K % 8 or M < 64 * 64 or tiles >= _GROUP_TILES or N < 256 or K < 256:
+    if M % 64 or N % 8 or K % 8 or N < 256 or K < 256:
         return 0
     for t in (dy, x2d, out):
         if t.data_ptr() % 16:
             return 0
-    return tiles
+    if M < 64 * 64:
+        return -tiles if _GROUP_BIG and M >= 1024 and 256 <= tiles <= _BIG_TILES else 0
+    return tiles if tiles < _GROUP_TILES else 0
 
 
 def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False, alpha=1.0, alpha_dev=None):
@@ -358,7 +378,7 @@ def linear_wgrad(dy: torch.Tensor, x2d: torch.Tensor, out=None, accumulate=False
     M, N = dy.shape
     K = x2d.shape[1]
     tiles = _groupable(dy, x2d, out, accumulate, alpha, alpha_dev)
-    if tiles and _WG.add(dy, x2d, out, tiles):
+    if tiles and _WG.add(dy, x2d, out, abs(tiles), whole_rounds=tiles < 0):
         return out
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)

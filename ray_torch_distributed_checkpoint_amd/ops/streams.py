@@ -1,28 +1,34 @@
-"""Process-wide side streams.
+"""Process-wide side streams, one per user and device, created once.
 
 A MI355X process gets GPU_MAX_HW_QUEUES (4) hardware queues; HIP streams beyond that share
 queues round-robin, and a side stream that lands on the compute stream's queue serialises
-with it (its event waits park the compute kernels queued behind them).  A data-parallel
-GPT-2 step already uses the compute stream, RCCL's stream and the DDP widen stream
-(csrc/runtime/reducer.cpp `shared_stream`), so the framework's own side work - the grouped
-weight-gradient GEMMs (ops/gemm.py) and the embedding backward's token sort
-(ops/embedding.py) - shares ONE stream per device instead of one each: four queues, four
-streams.  The sort runs under the cross-entropy kernel, long before the first grouped
-weight-gradient flush, so in-order sharing costs nothing.
+with it.  Every side stream of the framework's compute path is made here (the DDP widen / P2P
+streams in csrc/runtime/reducer.cpp `shared_stream`), once per process, so re-wrapping a model
+or re-running a step never adds streams.
+
+Users: "wgrad" (the grouped weight-gradient GEMMs, ops/gemm.py) and "sort" (the embedding
+backward's token sort, ops/embedding.py).  RTDC_SHARED_SIDE=1 gives both one stream: neutral
+on one GPU (17.22 vs 17.24 ms GPT-2 step) but +0.7 ms under DDP (18.35 / 18.27 vs 17.51 /
+17.68 ms, 1-rank RCCL, r4; the bucket collectives are launched from the wgrad stream's
+gradient-ready callbacks - which ordering costs the time was not isolated).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 _side: dict = {}
+_SHARED = os.environ.get("RTDC_SHARED_SIDE", "0") == "1"  # 1: one stream for all users (A/B)
 
 
-def side_stream(device) -> torch.cuda.Stream:
+def side_stream(device, user: str = "") -> torch.cuda.Stream:
     """The device's compute side stream (created once)."""
     device = torch.device(device)
-    key = device.index if device.index is not None else torch.cuda.current_device()
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, "" if _SHARED else user)
     s = _side.get(key)
     if s is None:
-        s = torch.cuda.Stream(device=torch.device("cuda", key))
+        s = torch.cuda.Stream(device=torch.device("cuda", idx))
         _side[key] = s
     return s

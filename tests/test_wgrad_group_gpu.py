@@ -333,3 +333,53 @@ def test_shared_weight_gradients_with_deferral_equal_immediate(tied_head):
         assert torch.isfinite(a).all()
         err = (a - b).norm() / b.norm()
         assert err < 1e-5, f"deferred vs immediate: {err:.3e}"
+
+
+def test_short_k_multi_round_products_pack_whole_rounds():
+    """Llama-3-8B at 2048 tokens/GPU: weight gradients of >= 256 tiles over a short K are packed
+    until the group is a whole number of rounds (ops/gemm.py `_groupable` whole_rounds).  A chain
+    of 6144x4096, 4096x6144 and 4096x4096 weights gives 384 + 384 + 256 tiles: the last layer's
+    256 tiles flush alone, the other two as one 768-tile (3-round) launch - bitwise the
+    one-by-one 256x256 launches (same tiles, same MFMA order)."""
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+    from ray_torch_distributed_checkpoint_amd.optim import FlatParamSpace
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(21)
+    x0 = (torch.randn(2048, 4096, device=dev) * 0.5).bfloat16()
+    ws0 = [torch.randn(6144, 4096, device=dev) * 0.02, torch.randn(4096, 6144, device=dev) * 0.02,
+           torch.randn(4096, 4096, device=dev) * 0.02]
+
+    def run(big):
+        old = G._GROUP_BIG
+        G._GROUP_BIG = big
+        sizes = []
+        orig = G._WgradGroup.flush
+
+        def spy(self, *a, **k):
+            if self.items:
+                sizes.append(sum(it[3] for it in self.items))
+            return orig(self, *a, **k)
+
+        G._WgradGroup.flush = spy
+        try:
+            ws = [torch.nn.Parameter(w.clone()) for w in ws0]
+            sp = FlatParamSpace(list(reversed(ws)))
+            sp.zero_grad(set_to_none=True)
+            h = x0
+            for w in ws:
+                h = ops.linear(h, w)
+            h.float().square().mean().backward()
+            torch.cuda.synchronize()
+            assert not G._WG.items and not G._WG.waiters
+            return [w.grad.detach().clone() for w in ws], sizes
+        finally:
+            G._WgradGroup.flush = orig
+            G._GROUP_BIG = old
+
+    (ga, sa), (gb, sb) = run(True), run(False)
+    assert sa == [256, 768], sa
+    assert sb == [], sb
+    for a, b in zip(ga, gb):
+        assert torch.isfinite(a).all() and torch.equal(a, b)
