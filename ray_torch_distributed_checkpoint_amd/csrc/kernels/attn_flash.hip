@@ -451,23 +451,30 @@ __global__ __launch_bounds__(256, 2) void fwd2_kernel(Args a) {
             mx = fmaxf(mx, v);
           }
         mx = max_rows4(mx);
-        const float mn = fmaxf(m[qg], mx * c);
-        const float alpha = fexp2(m[qg] - mn);
-        m[qg] = mn;
+        // lazy rescale (as fwd_kernel): the running max moves - and O, l are rescaled - only when
+        // some row of the wave would otherwise see probabilities above 2^8 (wave-uniform branch;
+        // a fully masked row keeps mx = -inf and never triggers it)
+        if (__any(mx * c > m[qg] + 8.f)) {
+          const float mn = fmaxf(m[qg], mx * c);
+          const float alpha = fexp2(m[qg] - mn);
+          m[qg] = mn;
+          l[qg] *= alpha;
+#pragma unroll
+          for (int d = 0; d < DT; ++d)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[qg][d][r] *= alpha;
+        }
+        const float mq = m[qg];
         float ps = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float pv = fexp2(fmaf(sc[qg][t][r], c, -mn));
+            const float pv = fexp2(fmaf(sc[qg][t][r], c, -mq));
             sc[qg][t][r] = pv;
             ps += pv;
           }
-        l[qg] = l[qg] * alpha + ps;
-#pragma unroll
-        for (int d = 0; d < DT; ++d)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[qg][d][r] *= alpha;
+        l[qg] += ps;
         pp[qg][0] = pack_pair(sc[qg][0], sc[qg][1]);
         pp[qg][1] = pack_pair(sc[qg][2], sc[qg][3]);
       }

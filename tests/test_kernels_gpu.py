@@ -715,6 +715,38 @@ def test_attention_impls(monkeypatch, impl, H, Hkv, Dh, T):
     _close(qkv.grad[..., C + Hkv * Dh:], qr.grad[..., C + Hkv * Dh:], 3e-2)    # dV
 
 
+@pytest.mark.parametrize("Dh,H,Hkv", [(64, 2, 2), (128, 2, 1)])
+def test_flash_forward_lazy_rescale_branch(Dh, H, Hkv):
+    """The forward kernels rescale O and l only when a row's running max grows by more than 2^8
+    (a rare, data-dependent, wave-uniform branch): spike Q.K scores at LATER key blocks so the
+    branch fires mid-row (twice, at key blocks 3 and 4 for query 300, once at block 6 for query
+    450), and compare the whole output and the gradients against the fp32 reference
+    (cdna_hip_programming.md §5.4 rule 26).  Dh 64 runs fwd_kernel, Dh 128 fwd2_kernel."""
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref
+
+    torch.manual_seed(7)
+    Bn, T = 1, 512
+    C = H * Dh
+    qkv = _bf(Bn, T, (H + 2 * Hkv) * Dh, scale=0.5)
+    for q, k, v in [(300, 200, 1.5), (300, 290, 2.0), (450, 420, 2.0)]:
+        for h in range(H):
+            qkv[0, q, h * Dh:(h + 1) * Dh] = v
+        for kh in range(Hkv):
+            qkv[0, k, C + kh * Dh:C + (kh + 1) * Dh] = v
+    qkv.requires_grad_(True)
+    out = causal_attention(qkv, H, Hkv)
+    g = _bf(Bn, T, C)
+    out.backward(g)
+    qr = qkv.detach().float().requires_grad_(True)
+    ref = causal_attention_ref(qr, Bn, T, H, Hkv, Dh)
+    ref.backward(g.float())
+    _close(out, ref, 2e-2)
+    _close(out[0, 300], ref[0, 300], 2e-2)  # the spiked rows themselves
+    _close(out[0, 450], ref[0, 450], 2e-2)
+    _close(qkv.grad, qr.grad, 3e-2)
+
+
 def test_flash_attention_deterministic():
     from ray_torch_distributed_checkpoint_amd.ops import causal_attention
 
