@@ -108,3 +108,45 @@ class CardRegistry(dict):
 
     def append(self, comp):  # default card
         self["default"].append(comp)
+
+
+def error_analysis_components(predictions, misclassified, labels_map: dict, n_samples: int = 50,
+                              image_shape=(28, 28)) -> list:
+    """The eval flow's error-analysis card (R/eval_flow.py:96-139) as card components: a
+    "Misclassifications X out of Y" heading and a table of up to `n_samples` misclassified rows
+    (deterministic sample) with the input image, true / predicted label and a logits bar chart.
+    `predictions` / `misclassified` are DataFrames with features, labels, predicted_values and
+    logits columns.  Renders with matplotlib's Agg backend (no display needed)."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    total, wrong = predictions.shape[0], misclassified.shape[0]
+    picked = misclassified.sample(min(n_samples, wrong), random_state=0) if wrong else misclassified
+    names = list(labels_map.values())
+
+    def image_of(features):
+        fig, ax = plt.subplots()
+        ax.imshow(features.reshape(*image_shape), cmap="gray")
+        ax.axis("off")
+        img = Image.from_matplotlib(fig)
+        plt.close(fig)
+        return img
+
+    def logits_chart(logits):
+        fig, ax = plt.subplots(figsize=(6, 4))
+        bars = ax.barh(names, logits)
+        ax.set(title="Logits", xlabel="Value", ylabel="Category")
+        ax.spines[["right", "top"]].set_visible(False)
+        for bar, v in zip(bars, logits):
+            ax.text(v, bar.get_y() + bar.get_height() / 2, f"{v:.2f}", va="center")
+        fig.tight_layout()
+        img = Image.from_matplotlib(fig)
+        plt.close(fig)
+        return img
+
+    rows = [[image_of(r.features), labels_map[int(r.labels)], labels_map[int(r.predicted_values)], logits_chart(r.logits)]
+            for _, r in picked.iterrows()]
+    return [Markdown(f"### Misclassifications {wrong} out of {total}"),
+            Table(headers=["Image", "True label", "Predicted label", "Logits"], data=rows)]

@@ -14,8 +14,8 @@ trainer / storage layout / --from-run path:
     python train_flow.py run --model gpt2-small --steps 400 --from-run RayTorchTrain/<id> --resume_mode exact
 (--model resnet18 | llama3-8b | *-tiny; sharded DCP checkpoints every N steps, async.)
 """
-from ray_torch_distributed_checkpoint_amd.flow import (FlowSpec, Parameter, Run, Task, current, gpu_profile,
-                                                       kubernetes, metaflow_ray, pypi, retry, schedule, step)
+from ray_torch_distributed_checkpoint_amd.flow import (FlowSpec, Parameter, current, gpu_profile, kubernetes,
+                                                       metaflow_ray, pypi, retry, schedule, step, upstream_checkpoint)
 
 N_PARALLEL = 2
 N_GPU_PER_WORKER = 1
@@ -89,12 +89,9 @@ class RayTorchTrain(FlowSpec):
             max_failures=int(self.max_failures),
             **hyperparameters,
         )
-        if self.upstream_task_pathspec is not None and self.upstream_task_pathspec != "null":
-            t = Task(self.upstream_task_pathspec)
-            args["checkpoint"] = t.data.result.checkpoint
-        elif self.upstream_run_pathspec is not None and self.upstream_run_pathspec != "null":
-            r = Run(self.upstream_run_pathspec)
-            args["checkpoint"] = r.data.result.checkpoint
+        warm = upstream_checkpoint(self.upstream_task_pathspec, self.upstream_run_pathspec, required=False)
+        if warm is not None:  # --from-task wins over --from-run (flow/upstream.py)
+            args["checkpoint"] = warm
         else:
             print("Training from newly initialized")
 
