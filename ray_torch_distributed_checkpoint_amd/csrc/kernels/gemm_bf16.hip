@@ -610,6 +610,38 @@ extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajo
 extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, int bn,
                                   hipStream_t st);
 extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
+extern "C" int rtdc_gemm4b_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
+
+// cfg 12: the one-barrier-per-K-tile 4-wave kernel (gemm4b.hip), any operand layout.  Chosen
+// automatically for K-major x K-major products with K >= 2048 (where it beats the 8-wave kernels,
+// profiles/gemm_4wave_one_barrier_r4.txt; RTDC_GEMM4B_AUTO=0 turns that off);
+// RTDC_GEMM4B=1 routes every 8-wave 256x256 choice (cfg 6 / 8) to it (A/B of the routing).
+static int g_gemm4b_auto = -1;
+static bool gemm4b_auto() {
+  if (g_gemm4b_auto < 0) {
+    const char* e = getenv("RTDC_GEMM4B_AUTO");
+    g_gemm4b_auto = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_gemm4b_auto == 1;
+}
+extern "C" int rtdc_gemm4b_auto_set(int v) {
+  const int old = gemm4b_auto() ? 1 : 0;
+  if (v >= 0) g_gemm4b_auto = v ? 1 : 0;
+  return old;
+}
+static int g_gemm4b = -1;
+static bool gemm4b_enabled() {
+  if (g_gemm4b < 0) {
+    const char* e = getenv("RTDC_GEMM4B");
+    g_gemm4b = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_gemm4b == 1;
+}
+extern "C" int rtdc_gemm4b_set(int v) {
+  const int old = gemm4b_enabled() ? 1 : 0;
+  if (v >= 0) g_gemm4b = v ? 1 : 0;
+  return old;
+}
 
 // cfg 10: the 4-wave 256x256 kernel (gemm_8ph.hip gemm4_kernel, 128x128 per wave).
 // RTDC_GEMM4W=1 routes the 8-wave 256x256 choices (cfg 6 / 8) to it.
@@ -700,6 +732,10 @@ static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
   const double e6 = est(256, b_kmajor && t6 > 256 ? 1.58 : 1.74);
   const double e7 = (b_kmajor || a.K <= 4096) ? est(192, b_kmajor ? 1.42 : 1.37) : 1e30;
   const double e11 = est(128, b_kmajor ? 1.10 : 1.16);
+  // cfg 12 (gemm4b.hip, one barrier per K-tile): 1.52 us per 256x256 K-tile on the forward layout
+  // (profiles/gemm_4wave_one_barrier_r4.txt); its MN-major-B form trails the 8-wave kernel
+  const double e12 = b_kmajor && gemm4b_auto() ? est(256, 1.52) : 1e30;
+  if (e12 < e6 && e12 < e7 && e12 < e11) return 12;
   if (e11 < e6 && e11 < e7) return 11;
   return e7 < e6 ? 7 : 6;
 }
@@ -719,11 +755,13 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     cfg = pick_cfg_few_rows(a, b_kmajor, plain && a.ws != nullptr);
   }
   if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4w_enabled()) cfg = 10;
+  if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_enabled()) cfg = 12;
+  if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_auto() && a_kmajor && b_kmajor && a.K >= 2048) cfg = 12;
   // the 8-wave kernels write bf16 outputs 16 B at a time through tile-relative 32-bit buffer
   // offsets (gemm_8ph.hip tile_epilogue)
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
                        (uintptr_t)a.bias;
-  if (cfg >= 6 && cfg <= 11 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
+  if (cfg >= 6 && cfg <= 12 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
@@ -732,17 +770,21 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
   // cfg 11: the 8-wave kernel on 256x128 tiles (bf16 output, K-major A)
   if (cfg == 11 && (out_fp32 || !a_kmajor)) cfg = 6;
-  const bool big = cfg >= 6 && cfg <= 11;  // counted-vmcnt pipelines (gemm_8ph.hip)
+  const bool big = cfg >= 6 && cfg <= 12;  // counted-vmcnt pipelines (gemm_8ph.hip, gemm4b.hip)
   const int bn = (cfg == 7 || cfg == 9) ? 192 : cfg == 11 ? 128 : 256;
   if (big) {
     if (batch != 1 || a.causal != 0) return 1;
     tiles = (long long)((a.M + 255) / 256) * ((a.N + bn - 1) / bn);
   }
   // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
-  if (plain && (cfg <= 7 || cfg == 10 || cfg == 11))
-    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : cfg == 11 ? 1.0 : 1.8) : pick_splitk(a, tiles);
+  if (plain && (cfg <= 7 || cfg >= 10))
+    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : cfg == 11 ? 1.0 : cfg == 12 ? 1.52 : 1.8)
+                        : pick_splitk(a, tiles);
   if (cfg == 10) {
     const int rc = rtdc_gemm4_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
+    if (rc) return rc;
+  } else if (cfg == 12) {
+    const int rc = rtdc_gemm4b_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
     if (rc) return rc;
   } else if (big) {
     // cfg 8 / 9 force the persistent form; 6 / 7 take it automatically where it applies

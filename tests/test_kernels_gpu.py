@@ -638,6 +638,94 @@ def test_gemm_persistent_multi_tile(cfg, a_k, b_k, K):
     _close(Cb, ref, 1e-2)
 
 
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("K", [64, 128, 192, 320, 768])
+def test_gemm_4wave_one_barrier(a_k, b_k, K):
+    """tile_cfg 12 (gemm4b.hip: 4 waves, 128x128 per wave, one barrier per K-tile), every operand
+    layout: 1, 2, 3, 5 and 12 K-tiles (the last two K-tiles are peeled out of the steady-state
+    loop), partial edge tiles, fp32 and bf16 outputs, and (forward layout) the fused bias + GELU /
+    residual epilogues."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(1200 + K + 2 * a_k + b_k)
+    M, N = 1024 + 40, 768 + 8
+    A = _bf(M, K) if a_k else _bf(K, M)
+    B = _bf(N, K) if b_k else _bf(K, N)
+    Af = A.float() if a_k else A.float().t()
+    Bf = B.float().t() if b_k else B.float()
+    ref = Af @ Bf
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k, tile_cfg=12)
+    _close(C, ref, 1e-5)
+    Cb = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, Cb, M, N, K, A.shape[1], B.shape[1], N, a_k, b_k, tile_cfg=12)
+    _close(Cb, ref, 1e-2)
+    if not (a_k and b_k):
+        return
+    bias = torch.randn(N, device=DEV)
+    pre_ref = ref + bias
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, y, M, N, K, K, K, N, True, True, bias=bias, aux_out=pre, act=G.ACT_GELU, tile_cfg=12)
+    _close(pre, pre_ref, 1e-2)
+    _close(y, F.gelu(pre_ref, approximate="tanh"), 1e-2)
+    res = _bf(M, N)
+    y2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, y2, M, N, K, K, K, N, True, True, Cin=res, beta=1.0, bias=bias, tile_cfg=12)
+    _close(y2, pre_ref + res.float(), 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 28672, 4096), (2048, 4096, 14336), (4096, 4096, 4096)])
+def test_gemm_auto_long_k_forward_routes_to_4wave(M, N, K):
+    """Long-K forward products (Llama-3-8B gate/up and down projections, 4096^3) take the
+    one-barrier 4-wave kernel automatically (bitwise the forced cfg 12 result, split-K included)
+    and match the fp32 reference."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(M + N + K)
+    x, w = _bf(M, K), _bf(N, K, scale=0.05)
+    y = G.linear_fwd(x, w)
+    y12 = torch.empty_like(y)
+    G.gemm_bf16(x, w, y12, M, N, K, K, K, N, True, True, tile_cfg=12)
+    assert torch.equal(y, y12)
+    _close(y, x.float() @ w.float().t(), 1e-2)
+
+
+def test_gemm_4wave_one_barrier_dgrad_gelu():
+    """cfg 12 with the dgrad layout and the GELU-backward epilogue (aux_in, column sums)."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(1277)
+    M, N, K = 2048, 1024, 768  # dx[M, N] = dy[M, K] . W[K, N]
+    dy, w, pre = _bf(M, K), _bf(K, N, scale=0.05), _bf(M, N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    cs = torch.empty(N, device=DEV)
+    G.gemm_bf16(dy, w, out, M, N, K, K, N, N, True, False, aux_in=pre, act=G.ACT_GELU_BWD, tile_cfg=12,
+                colsum_out=cs)
+    x = pre.float().requires_grad_(True)
+    F.gelu(x, approximate="tanh").backward(torch.ones_like(x))
+    ref = (dy.float() @ w.float()) * x.grad
+    _close(out, ref, 1e-2)
+    _close(cs, ref.sum(0), 2e-2)
+
+
+def test_gemm_4wave_one_barrier_splitk_and_large():
+    """cfg 12 through split-K (a long-K product with few tiles: fp32 slabs + reduce) and on a
+    GPT-2 c_fc-sized forward (768 tiles, 12 K-tiles)."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(1299)
+    M, N, K = 512, 512, 8192
+    A, B = _bf(M, K), _bf(N, K)
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, K, K, N, True, True, tile_cfg=12)
+    _close(C, A.float() @ B.float().t(), 1e-5)
+    x, w = _bf(16384, 768), _bf(3072, 768)
+    y = torch.empty(16384, 3072, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(x, w, y, 16384, 3072, 768, 768, 768, 3072, True, True, tile_cfg=12)
+    _close(y, x.float() @ w.float().t(), 1e-2)
+
+
 def test_gemm_persistent_epilogues():
     """bias + GELU (pre-activation side output) and residual epilogues through the persistent
     kernel, against the 2-launch reference."""
