@@ -720,10 +720,23 @@ def test_gemm_4wave_one_barrier_splitk_and_large():
     C = torch.empty(M, N, device=DEV, dtype=torch.float32)
     G.gemm_bf16(A, B, C, M, N, K, K, K, N, True, True, tile_cfg=12)
     _close(C, A.float() @ B.float().t(), 1e-5)
-    x, w = _bf(16384, 768), _bf(3072, 768)
-    y = torch.empty(16384, 3072, device=DEV, dtype=torch.bfloat16)
-    G.gemm_bf16(x, w, y, 16384, 3072, 768, 768, 768, 3072, True, True, tile_cfg=12)
-    _close(y, x.float() @ w.float().t(), 1e-2)
+    # GPT-2 c_fc-sized forward (768 tiles, 3 per CU): plain, bias + GELU with the pre-activation
+    # side output, and residual epilogues
+    M, N, K = 16384 + 128, 3072, 768
+    x, w = _bf(M, K), _bf(N, K, scale=0.05)
+    bias, res = torch.randn(N, device=DEV), _bf(M, N)
+    ref = x.float() @ w.float().t()
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(x, w, y, M, N, K, K, K, N, True, True, tile_cfg=12)
+    _close(y, ref, 1e-2)
+    yg = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(x, w, yg, M, N, K, K, K, N, True, True, bias=bias, aux_out=pre, act=G.ACT_GELU, tile_cfg=12)
+    _close(pre, ref + bias, 1e-2)
+    _close(yg, F.gelu(ref + bias, approximate="tanh"), 1e-2)
+    yr = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(x, w, yr, M, N, K, K, K, N, True, True, Cin=res, beta=1.0, bias=bias, tile_cfg=12)
+    _close(yr, ref + bias + res.float(), 1e-2)
 
 
 def test_gemm_persistent_epilogues():
