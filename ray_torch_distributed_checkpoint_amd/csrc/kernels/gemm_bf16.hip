@@ -611,22 +611,26 @@ extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmaj
                                   hipStream_t st);
 extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 extern "C" int rtdc_gemm4b_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
+extern "C" int rtdc_gemm8b_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 
-// cfg 12: the one-barrier-per-K-tile 4-wave kernel (gemm4b.hip), any operand layout.  Chosen
-// automatically for K-major x K-major products with K >= 2048 (where it beats the 8-wave kernels,
-// profiles/gemm_4wave_one_barrier_r4.txt; RTDC_GEMM4B_AUTO=0 turns that off);
-// RTDC_GEMM4B=1 routes every 8-wave 256x256 choice (cfg 6 / 8) to it (A/B of the routing).
+// cfg 12 / 13: the one-barrier-per-K-tile kernels (gemm4b.hip: 4 waves, any operand layout;
+// gemm8b.hip: 8 waves, forward layout).  RTDC_GEMM4B_AUTO: 2 (default) cfg 12 for K-major x
+// K-major products with K >= 2048 (Llama-3-8B step -0.7 %); 1 cfg 13 for every forward-layout
+// product up to 8 rounds of 256x256 tiles (faster in isolation, but the GPT-2 step ran 4 %
+// slower: profiles/gemm_8wave_one_barrier_r4.txt); 0 neither.  RTDC_GEMM4B=1 routes every
+// 8-wave 256x256 choice (cfg 6 / 8) to cfg 12 (A/B).
 static int g_gemm4b_auto = -1;
-static bool gemm4b_auto() {
+static int gemm4b_mode() {  // 0 off, 1 cfg 13 for the forward layout, 2 cfg 12 for K >= 2048 forwards
   if (g_gemm4b_auto < 0) {
     const char* e = getenv("RTDC_GEMM4B_AUTO");
-    g_gemm4b_auto = (e && e[0] == '0') ? 0 : 1;
+    g_gemm4b_auto = e ? atoi(e) : 2;
   }
-  return g_gemm4b_auto == 1;
+  return g_gemm4b_auto;
 }
+static bool gemm4b_auto() { return gemm4b_mode() == 1; }
 extern "C" int rtdc_gemm4b_auto_set(int v) {
-  const int old = gemm4b_auto() ? 1 : 0;
-  if (v >= 0) g_gemm4b_auto = v ? 1 : 0;
+  const int old = gemm4b_mode();
+  if (v >= 0) g_gemm4b_auto = v;
   return old;
 }
 static int g_gemm4b = -1;
@@ -732,9 +736,11 @@ static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
   const double e6 = est(256, b_kmajor && t6 > 256 ? 1.58 : 1.74);
   const double e7 = (b_kmajor || a.K <= 4096) ? est(192, b_kmajor ? 1.42 : 1.37) : 1e30;
   const double e11 = est(128, b_kmajor ? 1.10 : 1.16);
-  // cfg 12 (gemm4b.hip, one barrier per K-tile): 1.52 us per 256x256 K-tile on the forward layout
-  // (profiles/gemm_4wave_one_barrier_r4.txt); its MN-major-B form trails the 8-wave kernel
-  const double e12 = b_kmajor && gemm4b_auto() ? est(256, 1.52) : 1e30;
+  // cfg 13 (gemm8b.hip, 8 waves, one barrier per K-tile): ~1.45 us per 256x256 K-tile on the
+  // forward layout (profiles/gemm_8wave_one_barrier_r4.txt); forward layout only
+  const double e13 = b_kmajor && gemm4b_mode() == 1 ? est(256, 1.45) : 1e30;
+  if (e13 < e6 && e13 < e7 && e13 < e11) return 13;
+  const double e12 = b_kmajor && gemm4b_mode() == 2 ? est(256, 1.52) : 1e30;
   if (e12 < e6 && e12 < e7 && e12 < e11) return 12;
   if (e11 < e6 && e11 < e7) return 11;
   return e7 < e6 ? 7 : 6;
@@ -756,12 +762,19 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   }
   if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4w_enabled()) cfg = 10;
   if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_enabled()) cfg = 12;
-  if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_auto() && a_kmajor && b_kmajor && a.K >= 2048) cfg = 12;
+  // RTDC_GEMM4B_AUTO=1: the one-barrier 8-wave kernel for the forward layout up to 8 rounds of
+  // 256x256 tiles (beyond that - the LM head's 12608 tiles - the persistent 8-wave kernel hides
+  // the per-tile prologue better)
+  if (cfg >= 6 && cfg <= 9 && a.tile_cfg < 0 && gemm4b_auto() && a_kmajor && b_kmajor && batch == 1 &&
+      (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) <= 2048)
+    cfg = 13;
+  if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_mode() == 2 && a_kmajor && b_kmajor && a.K >= 2048) cfg = 12;
+  if (cfg == 13 && !(a_kmajor && b_kmajor)) cfg = 6;  // the 8-wave one-barrier kernel: forward layout only
   // the 8-wave kernels write bf16 outputs 16 B at a time through tile-relative 32-bit buffer
   // offsets (gemm_8ph.hip tile_epilogue)
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
                        (uintptr_t)a.bias;
-  if (cfg >= 6 && cfg <= 12 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
+  if (cfg >= 6 && cfg <= 13 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
@@ -770,7 +783,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
   // cfg 11: the 8-wave kernel on 256x128 tiles (bf16 output, K-major A)
   if (cfg == 11 && (out_fp32 || !a_kmajor)) cfg = 6;
-  const bool big = cfg >= 6 && cfg <= 12;  // counted-vmcnt pipelines (gemm_8ph.hip, gemm4b.hip)
+  const bool big = cfg >= 6 && cfg <= 13;  // counted-vmcnt pipelines (gemm_8ph.hip, gemm4b.hip, gemm8b.hip)
   const int bn = (cfg == 7 || cfg == 9) ? 192 : cfg == 11 ? 128 : 256;
   if (big) {
     if (batch != 1 || a.causal != 0) return 1;
@@ -778,13 +791,16 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   }
   // 8-phase 256x256: one 512-thread block per CU; 128x128: two per CU; ~1.8 us per k-tile either way
   if (plain && (cfg <= 7 || cfg >= 10))
-    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : cfg == 11 ? 1.0 : cfg == 12 ? 1.52 : 1.8)
+    a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : cfg == 11 ? 1.0 : cfg == 12 ? 1.52 : cfg == 13 ? 1.45 : 1.8)
                         : pick_splitk(a, tiles);
   if (cfg == 10) {
     const int rc = rtdc_gemm4_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
     if (rc) return rc;
   } else if (cfg == 12) {
     const int rc = rtdc_gemm4b_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
+    if (rc) return rc;
+  } else if (cfg == 13) {
+    const int rc = rtdc_gemm8b_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
     if (rc) return rc;
   } else if (big) {
     // cfg 8 / 9 force the persistent form; 6 / 7 take it automatically where it applies

@@ -676,10 +676,10 @@ def test_gemm_4wave_one_barrier(a_k, b_k, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(2048, 28672, 4096), (2048, 4096, 14336), (4096, 4096, 4096)])
-def test_gemm_auto_long_k_forward_routes_to_4wave(M, N, K):
+def test_gemm_auto_long_k_forward_routes_to_one_barrier(M, N, K):
     """Long-K forward products (Llama-3-8B gate/up and down projections, 4096^3) take the
-    one-barrier 4-wave kernel automatically (bitwise the forced cfg 12 result, split-K included)
-    and match the fp32 reference."""
+    one-barrier 4-wave kernel automatically (RTDC_GEMM4B_AUTO=2, the default: bitwise the forced
+    cfg 12 result, split-K included) and match the fp32 reference."""
     from ray_torch_distributed_checkpoint_amd.ops import gemm as G
 
     torch.manual_seed(M + N + K)
@@ -707,6 +707,35 @@ def test_gemm_4wave_one_barrier_dgrad_gelu():
     ref = (dy.float() @ w.float()) * x.grad
     _close(out, ref, 1e-2)
     _close(cs, ref.sum(0), 2e-2)
+
+
+@pytest.mark.parametrize("K", [64, 128, 192, 768])
+def test_gemm_8wave_one_barrier(K):
+    """tile_cfg 13 (gemm8b.hip: 8 waves, 128x64 per wave, one barrier per K-tile; K-major A and B):
+    1-3 and 12 K-tiles, partial edge tiles, fp32 / bf16 outputs, split-K, bias + GELU epilogue."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(1300 + K)
+    M, N = 1024 + 40, 768 + 8
+    A, B = _bf(M, K), _bf(N, K)
+    ref = A.float() @ B.float().t()
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A, B, C, M, N, K, K, K, N, True, True, tile_cfg=13)
+    _close(C, ref, 1e-5)
+    Cb = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, Cb, M, N, K, K, K, N, True, True, tile_cfg=13)
+    _close(Cb, ref, 1e-2)
+    bias = torch.randn(N, device=DEV)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm_bf16(A, B, y, M, N, K, K, K, N, True, True, bias=bias, aux_out=pre, act=G.ACT_GELU, tile_cfg=13)
+    _close(pre, ref + bias, 1e-2)
+    _close(y, F.gelu(ref + bias, approximate="tanh"), 1e-2)
+    Ms, Ns, Ks = 512, 512, 8192  # few tiles, long K: split-K slabs
+    A2, B2 = _bf(Ms, Ks), _bf(Ns, Ks)
+    C2 = torch.empty(Ms, Ns, device=DEV, dtype=torch.float32)
+    G.gemm_bf16(A2, B2, C2, Ms, Ns, Ks, Ks, Ks, Ns, True, True, tile_cfg=13)
+    _close(C2, A2.float() @ B2.float().t(), 1e-5)
 
 
 def test_gemm_4wave_one_barrier_splitk_and_large():
