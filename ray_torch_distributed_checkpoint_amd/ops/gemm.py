@@ -140,11 +140,14 @@ _BIG_TILES = 4096     # ... and, over a short K (< 4096 tokens), products of up 
 # tiles per round (one 8-wave block per CU); groups are packed up to it (RTDC_WGRAD_ROUND: A/B of
 # smaller groups that leave CUs to the compute stream's kernels while a group runs)
 _ROUND = int(os.environ.get("RTDC_WGRAD_ROUND", "256"))
-# Grouped launches inside backward go to a side stream, so the next layer's backward kernels
-# can take the CUs a 216-tile group leaves idle (one 8-wave block fills a CU); the compute
-# stream joins it at the end of backward.  -0.17 ms/step on GPT-2-small
-# (profiles/wgrad_group_ab_r3.txt); RTDC_WGRAD_SIDE=0 keeps them on the compute stream.
-_GROUP_SIDE = os.environ.get("RTDC_WGRAD_SIDE", "1") != "0"
+# RTDC_WGRAD_SIDE=1 launches the grouped products inside backward on a side stream, so the next
+# layer's backward kernels can take the CUs a group leaves idle; the compute stream joins it at
+# the end of backward.  It was -0.17 ms/step on GPT-2-small in round 3
+# (profiles/wgrad_group_ab_r3.txt); with round 4's whole-round groups a group holds every CU and
+# the compute stream's small kernels (norm backward, split-K reduces, column sums) run starved
+# beside it: the compute stream is now faster on both models (GPT-2 -0.05 ms, Llama-3-8B
+# -1.1 ms per step, profiles/wgrad_side_stream_ab_r4.txt), so it is the default.
+_GROUP_SIDE = os.environ.get("RTDC_WGRAD_SIDE", "0") == "1"
 # Short-K multi-round weight gradients packed into whole rounds (see _groupable);
 # RTDC_WGRAD_GROUP_BIG=0 launches them one by one.
 _GROUP_BIG = os.environ.get("RTDC_WGRAD_GROUP_BIG", "1") != "0"
