@@ -708,8 +708,10 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
 // bwd_dkdv_kernel, whose Dh = 64 loop is LDS-bound (per step and wave 24 ds_read_b128 + 32
 // ds_read_b64_tr_b16 = 160 LDS-array cycles for 32 MFMAs, 12 waves per CU; MI355X_MICROARCH.md
 // §LDS).  Same ring, row-constant DMA and output contract (incl. the GQA head split).
+// (Dh = 128: 2 x 2 x 8 accumulators + 2 x 2 x 4 K / V fragments need the AGPR half of the
+// register file, so one wave per SIMD)
 template <int DH, int NS>
-__global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(Args a) {
+__global__ __launch_bounds__(256, DH == 64 ? 2 : 1) void bwd_dkdv2_kernel(Args a) {
   constexpr int KS = DH / 32, DT = DH / 16, DB = 2, TILE = 64 * DH * 2, KG = 2, BK2 = 128;
   constexpr int STG = 2 * TILE + 512, PER = DH / 16 + 1;
   __shared__ __attribute__((aligned(16))) char smem[NS * STG];
@@ -1054,6 +1056,175 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     wave_colsum16<DT>(dq, a.scale, a.cs_ws + (((long long)b * a.T + qb * BQ + wave * 16) >> 4) * W + qcol, lane);
 }
 
+// dQ with 32 query rows per wave (block = 128 rows): every K / V fragment read from LDS (row and
+// transposed) feeds the MFMAs of two 16-row query groups, halving LDS bytes per MFMA of
+// bwd_dq_kernel - the change that took dK/dV from 130 to 82 us at GPT-2 shapes (bwd_dkdv2_kernel).
+// Same DMA ring, delta prologue, causal skip / mask and output contract.
+template <int DH, int NS>
+__global__ __launch_bounds__(256, 2) void bwd_dq2_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2, PER = DH / 16;
+  constexpr int QG = 2, BQ2 = 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE];  // K[NS], V[NS]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = a.T / BQ2;
+  int bx, bh;
+  grid_pos(a, bx, bh);
+  const int qb = nqb - 1 - bx;  // heaviest (longest causal prefix) blocks first
+  const int b = bh / a.H, h = bh % a.H;
+  const int grp = a.H / a.Hkv, kvh = h / grp;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const int qcol = h * DH, kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int q0w = qb * BQ2 + wave * 32;  // this wave: rows [q0w, q0w + 32)
+  int myq[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) myq[qg] = q0w + 16 * qg + (lane & 15);
+  const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
+  const int nkb = (qb + 1) * (BQ2 / BKV);
+
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (NS + (s)) * TILE)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkb) {
+      stage<DH>(base, W, s * BKV, kcol, KT(s), wave, lane);
+      stage<DH>(base, W, s * BKV, vcol, VT(s), wave, lane);
+    }
+  bf16x8 qf[QG][KS], of[QG][KS], ofw[QG][KS];
+  float lse2[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qf[qg][ks] = gload8(base + (long long)myq[qg] * W + qcol + ks * 32 + g * 8);
+      of[qg][ks] = gload8(a.dout + ((long long)b * a.T + myq[qg]) * C + h * DH + ks * 32 + g * 8);
+      ofw[qg][ks] = gload8(a.out + ((long long)b * a.T + myq[qg]) * C + h * DH + ks * 32 + g * 8);
+    }
+    lse2[qg] = a.lse[(long long)bh * a.T + myq[qg]];
+  }
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      settle(qf[qg][ks]);
+      settle(of[qg][ks]);
+      settle(ofw[qg][ks]);
+    }
+    settle(lse2[qg]);
+  }
+  // delta = sum_d dO * O per row (the softmax-backward row term), stored for the dK/dV kernel
+  float del[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f((bf16_t)of[qg][ks][e]), bf2f((bf16_t)ofw[qg][ks][e]), dsum);
+    del[qg] = sum_rows4(dsum);
+    if (g == 0) a.delta[(long long)bh * a.T + myq[qg]] = del[qg];
+  }
+  step_barrier();
+
+  f32x4 dq[QG][DT];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[qg][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb % NS;
+    if (kb + NS - 1 < nkb) {
+      const int nx = (kb + NS - 1) % NS;
+      stage<DH>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
+      stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
+    }
+    // keys of this tile all after this wave's last row: nothing to add (barriers still run)
+    if (kb * BKV <= q0w + 31) {
+      const char* kt = KT(cur);
+      const char* vt = VT(cur);
+      const uint32_t kbase_lds = lds_addr(kt);
+      const bool diag = kb * BKV + BKV - 1 > q0w;
+      f32x4 ds[QG][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x4 sacc[QG], dpacc[QG];
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) sacc[qg] = dpacc[qg] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 kf = frag_rows<DH>(kt, 16 * t, ks, lane), vf = frag_rows<DH>(vt, 16 * t, ks, lane);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) {
+            sacc[qg] = mfma(kf, qf[qg][ks], sacc[qg]);    // D[key][q]
+            dpacc[qg] = mfma(vf, of[qg][ks], dpacc[qg]);  // D[key][q]
+          }
+        }
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const float pv = fexp2(fmaf(sacc[qg][rr], c, -lse2[qg]));
+            ds[qg][t][rr] = pv * (dpacc[qg][rr] - del[qg]);
+          }
+      }
+      if (diag) {  // causal mask where the tile meets this wave's rows (wave-uniform)
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+              if (kb * BKV + 16 * t + 4 * g + rr > myq[qg]) ds[qg][t][rr] = 0.f;
+      }
+      bf16x8 d0[QG], d1[QG];
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) {
+        d0[qg] = pack_pair(ds[qg][0], ds[qg][1]);
+        d1[qg] = pack_pair(ds[qg][2], ds[qg][3]);
+      }
+#pragma unroll
+      for (int e0 = 0; e0 < DT; e0 += DB) {
+        TrPair fk[DB][2];
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const uint32_t lk = kbase_lds + troff[e0 + d];
+          fk[d][0] = frag_cols_at<DH, 0>(lk);
+          fk[d][1] = frag_cols_at<DH, 32>(lk);
+        }
+        lgkm_wait0();
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const bf16x8 k0 = tr_use(fk[d][0]), k1 = tr_use(fk[d][1]);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) {
+            dq[qg][e0 + d] = mfma(k0, d0[qg], dq[qg][e0 + d]);
+            dq[qg][e0 + d] = mfma(k1, d1[qg], dq[qg][e0 + d]);
+          }
+        }
+      }
+    }
+    if (kb + 1 < nkb && !(a.diag & 1)) wait_vm_upto(PER * (min(kb + NS - 1, nkb - 1) - kb - 1));
+    step_barrier();
+  }
+#undef KT
+#undef VT
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    bf16_t* qrow = a.dqkv + ((long long)b * a.T + myq[qg]) * W + qcol;
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+      *(uint2*)(qrow + 16 * d + 4 * g) = make_uint2(pack_bf2(dq[qg][d][0] * a.scale, dq[qg][d][1] * a.scale),
+                                                   pack_bf2(dq[qg][d][2] * a.scale, dq[qg][d][3] * a.scale));
+    if (a.cs_ws)
+      wave_colsum16<DT>(dq[qg], a.scale, a.cs_ws + (((long long)b * a.T + q0w + 16 * qg) >> 4) * W + qcol, lane);
+  }
+}
+
 }  // namespace fa
 }  // namespace rtdc
 
@@ -1133,8 +1304,14 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   // dK/dV at Dh = 64: 32 keys per wave (bwd_dkdv2_kernel) unless RTDC_FA_DKDV=1 (16 keys per wave)
   const char* dkdv_env = getenv("RTDC_FA_DKDV");  // (read per call: tests A/B it in one process)
   const int dkdv_v = dkdv_env ? atoi(dkdv_env) : 2;
+  // dQ: 32 query rows per wave (bwd_dq2_kernel; GPT-2 63 -> 59 us, Llama-3-8B shapes 165 -> 140 us
+  // per call, benchmarks/attn_bench.py under rocprofv3) unless RTDC_FA_DQ=1 (16 rows per wave)
+  const char* dq_env = getenv("RTDC_FA_DQ");  // (read per call: tests A/B it in one process)
+  const bool dq2 = (dq_env ? atoi(dq_env) : 2) == 2 && T % 128 == 0;
+  const dim3 g2b(T / 128, B * H);
   if (Dh == 64) {
-    FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
+    if (dq2) FA_DISPATCH(fa::bwd_dq2_kernel, 64, ns, g2b, a);
+    else FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
     if (dkdv_v == 2 && T % 128 == 0) {
       dim3 g3(T / 128, B * Hkv * qs);
       FA_DISPATCH(fa::bwd_dkdv2_kernel, 64, ns, g3, a);
@@ -1142,8 +1319,14 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
       FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
     }
   } else {
-    FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
-    FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
+    if (dq2) FA_DISPATCH(fa::bwd_dq2_kernel, 128, ns, g2b, a);
+    else FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
+    if (dkdv_env && dkdv_v == 2 && T % 128 == 0) {  // opt-in at Dh = 128 (occupancy 1)
+      dim3 g3(T / 128, B * Hkv * qs);
+      FA_DISPATCH(fa::bwd_dkdv2_kernel, 128, ns, g3, a);
+    } else {
+      FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
+    }
   }
   if (qs > 1) {
     const int KV = Hkv * 2 * Dh;

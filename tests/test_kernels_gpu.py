@@ -1024,3 +1024,54 @@ def test_flash_dkdv_32_keys_per_wave_equals_16(monkeypatch, H, Hkv, T):
         out[v] = (qkv.grad.clone(), cs.clone())
     assert torch.equal(out["1"][0], out["2"][0])
     _close(out["1"][1], out["2"][1], 1e-6)
+
+
+@pytest.mark.parametrize("Dh,H,Hkv,T", [(64, 4, 4, 256), (64, 4, 2, 512), (64, 2, 2, 1024), (128, 4, 1, 384)])
+def test_flash_dq_32_rows_per_wave_equals_16(monkeypatch, Dh, H, Hkv, T):
+    """dQ with two 16-row query groups per wave (bwd_dq2_kernel, RTDC_FA_DQ=2) runs every row
+    over the same key tiles in the same MFMA order as the 16-rows-per-wave kernel (a tile the
+    wave's upper group reaches but its lower one does not adds exact zeros): bitwise equal
+    gradients and row terms; colsum partials equal to fp32 rounding."""
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+    from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref
+
+    torch.manual_seed(T + H + Dh)
+    Bn = 2
+    W = (H + 2 * Hkv) * Dh
+    qkv0 = _bf(Bn, T, W)
+    g = _bf(Bn, T, H * Dh)
+    out = {}
+    for v in ("1", "2"):
+        monkeypatch.setenv("RTDC_FA_DQ", v)
+        qkv = qkv0.clone().requires_grad_(True)
+        causal_attention(qkv, H, Hkv).backward(g)
+        cs = G.colsum(qkv.grad.view(-1, W))
+        torch.cuda.synchronize()
+        out[v] = (qkv.grad.clone(), cs.clone())
+    assert torch.equal(out["1"][0], out["2"][0])
+    _close(out["1"][1], out["2"][1], 1e-6)
+    qr = qkv0.float().requires_grad_(True)
+    causal_attention_ref(qr, Bn, T, H, Hkv, Dh).backward(g.float())
+    _close(out["2"][0][..., :H * Dh], qr.grad[..., :H * Dh], 3e-2)
+
+
+@pytest.mark.parametrize("H,Hkv,T", [(4, 1, 384), (8, 2, 512)])
+def test_flash_dkdv_32_keys_per_wave_dh128(monkeypatch, H, Hkv, T):
+    """Opt-in Dh = 128 dK/dV with two 16-key groups per wave (RTDC_FA_DKDV=2, occupancy 1):
+    bitwise equal to the 16-keys-per-wave kernel, as at Dh = 64."""
+    from ray_torch_distributed_checkpoint_amd.ops import causal_attention
+
+    torch.manual_seed(T + H)
+    Dh, Bn = 128, 2
+    W = (H + 2 * Hkv) * Dh
+    qkv0 = _bf(Bn, T, W)
+    g = _bf(Bn, T, H * Dh)
+    out = {}
+    for v in ("1", "2"):
+        monkeypatch.setenv("RTDC_FA_DKDV", v)
+        qkv = qkv0.clone().requires_grad_(True)
+        causal_attention(qkv, H, Hkv).backward(g)
+        torch.cuda.synchronize()
+        out[v] = qkv.grad.clone()
+    assert torch.equal(out["1"], out["2"])
