@@ -746,6 +746,12 @@ static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
   return e7 < e6 ? 7 : 6;
 }
 
+// RTDC_GEMM_TAIL=0 disables the tail split of rtdc_gemm_bf16 (read per call: A/B in one process).
+static bool tail_split_enabled() {
+  const char* e = getenv("RTDC_GEMM_TAIL");
+  return !(e && e[0] == '0');
+}
+
 // cs_rows_out (optional): with cs_ws set and cs_out null the column sums are DEFERRED - the
 // 8-wave gelu-backward epilogue leaves its partial rows in cs_ws, *cs_rows_out = their count
 // (0: this kernel choice wrote none; the caller reduces C itself).
@@ -770,6 +776,34 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     cfg = 13;
   if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_mode() == 2 && a_kmajor && b_kmajor && a.K >= 2048) cfg = 12;
   if (cfg == 13 && !(a_kmajor && b_kmajor)) cfg = 6;  // the 8-wave one-barrier kernel: forward layout only
+  // Tail split: a forward-layout product on 256x256 tiles whose last round of tiles fills at
+  // most half the 256 CUs (Llama-3-8B gate|up at 2048 tokens: 8 x 112 = 896 tiles = 3.5 rounds)
+  // runs its whole rounds as one launch and the remaining column tiles on 256x128 tiles - twice
+  // the blocks, one full round at ~1.10 us per K-tile instead of half a round at ~1.52 - as a
+  // second (model: 389 -> 362 us for gate|up).  Same per-element K order in both kernels.
+  if (a.tile_cfg < 0 && (cfg == 6 || cfg == 8 || cfg == 12) && batch == 1 && a.causal == 0 && a_kmajor &&
+      b_kmajor && !out_fp32 && !a.cs_out && !a.cs_ws && !a.Cin && !a.aux_in && !a.aux_out && a.act == 0 &&
+      a.N % 256 == 0 && a.K >= 16 * gemm::BK && tail_split_enabled()) {
+    const int tm = (a.M + 255) / 256, tn = a.N / 256;
+    if (tm <= 256 && 256 % tm == 0 && (long long)tm * tn > 256) {
+      const int tail_cols = tn % (256 / tm);
+      if (tail_cols > 0 && tail_cols * tm <= 128) {
+        const int n1 = (tn - tail_cols) * 256;
+        GemmArgs h = a;
+        h.N = n1;
+        h.tile_cfg = cfg;
+        int rc = rtdc_gemm_bf16(&h, 1, 1, 0, 1, stream, nullptr);
+        if (rc) return rc;
+        GemmArgs t = a;
+        t.N = a.N - n1;
+        t.tile_cfg = 11;
+        t.B = a.B + (long long)n1 * a.ldb;
+        t.C = (bf16_t*)a.C + n1;
+        if (a.bias) t.bias = (const char*)a.bias + (long long)n1 * (a.bias_type == 2 ? 4 : 2);
+        return rtdc_gemm_bf16(&t, 1, 1, 0, 1, stream, nullptr);
+      }
+    }
+  }
   // the 8-wave kernels write bf16 outputs 16 B at a time through tile-relative 32-bit buffer
   // offsets (gemm_8ph.hip tile_epilogue)
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
