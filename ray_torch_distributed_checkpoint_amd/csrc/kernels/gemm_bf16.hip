@@ -783,6 +783,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   // second (model: 389 -> 362 us for gate|up).  Same per-element K order in both kernels.
   if (a.tile_cfg < 0 && (cfg == 6 || cfg == 8 || cfg == 12) && batch == 1 && a.causal == 0 && a_kmajor &&
       b_kmajor && !out_fp32 && !a.cs_out && !a.cs_ws && !a.Cin && !a.aux_in && !a.aux_out && a.act == 0 &&
+      !a.stats_mean && !a.bnb_x &&
       a.N % 256 == 0 && a.K >= 16 * gemm::BK && tail_split_enabled()) {
     const int tm = (a.M + 255) / 256, tn = a.N / 256;
     if (tm <= 256 && 256 % tm == 0 && (long long)tm * tn > 256) {
