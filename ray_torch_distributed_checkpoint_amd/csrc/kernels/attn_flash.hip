@@ -105,10 +105,16 @@ __device__ __forceinline__ int toff(int row, int chunk) {
 // global -> LDS copy of rows [r0, r0+64) (row stride ld elements, column offset col0) by all
 // 4 waves: 1 KiB global_load_lds pieces, swizzle applied on the source address.
 // DH/32 DMA instructions per wave.
-template <int DH>
+// HOIST = false keeps the per-piece 64-bit address math: the Dh = 64 backward kernels measured
+// faster that way (GPT-2 bwd 122 vs 129 us), the forward and the Dh = 128 kernels slower
+// (GPT-2 fwd 44.7 vs 43.3 us, Llama bwd 268 vs 264 us)
+template <int DH, bool HOIST = true>
 __device__ __forceinline__ void stage(const bf16_t* base, long long ld, int r0, int col0, char* tile, int wave,
                                       int lane) {
   constexpr int RB = DH * 2, CPR = RB / 16, RPP = 1024 / RB, PIECES = 64 * RB / 1024, PPW = PIECES / 4;
+  // wave-uniform tile origin (scalar math) + a 32-bit per-lane offset that does not depend on
+  // r0 (the swizzle uses the tile-local row), so it is computed once per kernel, not per tile
+  const bf16_t* tb = base + (long long)r0 * ld + col0;
 #pragma unroll
   for (int ii = 0; ii < PPW; ++ii) {
     const int piece = wave * PPW + ii;
@@ -117,7 +123,7 @@ __device__ __forceinline__ void stage(const bf16_t* base, long long ld, int r0, 
     int lch;
     if constexpr (DH == 64) lch = pch ^ ((row >> 1) & 7);
     else lch = pch ^ (row & 15);
-    const bf16_t* src = base + (long long)(r0 + row) * ld + col0 + lch * 8;
+    const bf16_t* src = HOIST ? tb + (row * (int)ld + lch * 8) : base + (long long)(r0 + row) * ld + col0 + lch * 8;
     __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(tile + piece * 1024), 16, 0, 0);
   }
 }
@@ -588,8 +594,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(Args a) {
     char* st = smem + (it % NS) * STG;
     const int gi = it / nq, qb = kb + it % nq;
     const int h = kvh * grp + qsub * gper + gi;
-    stage<DH>(base, W, qb * BQ, h * DH, st, wave, lane);
-    stage<DH>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
+    stage<DH, DH != 64>(base, W, qb * BQ, h * DH, st, wave, lane);
+    stage<DH, DH != 64>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
     const float* src = rowsrc + ((long long)b * a.H + h) * a.T + qb * BQ + rowoff;
     if (lane < 8) __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(st + rowdst), 16, 0, 0);
   };
@@ -746,8 +752,8 @@ __global__ __launch_bounds__(256, DH == 64 ? 2 : 1) void bwd_dkdv2_kernel(Args a
     char* st = smem + (it % NS) * STG;
     const int gi = it / nq, qb = qb0 + it % nq;
     const int h = kvh * grp + qsub * gper + gi;
-    stage<DH>(base, W, qb * BQ, h * DH, st, wave, lane);
-    stage<DH>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
+    stage<DH, DH != 64>(base, W, qb * BQ, h * DH, st, wave, lane);
+    stage<DH, DH != 64>(dob, C, qb * BQ, h * DH, st + TILE, wave, lane);
     const float* src = rowsrc + ((long long)b * a.H + h) * a.T + qb * BQ + rowoff;
     if (lane < 8) __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(st + rowdst), 16, 0, 0);
   };
@@ -955,8 +961,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nkb) {
-      stage<DH>(base, W, s * BKV, kcol, KT(s), wave, lane);
-      stage<DH>(base, W, s * BKV, vcol, VT(s), wave, lane);
+      stage<DH, DH != 64>(base, W, s * BKV, kcol, KT(s), wave, lane);
+      stage<DH, DH != 64>(base, W, s * BKV, vcol, VT(s), wave, lane);
     }
   bf16x8 qf[KS], of[KS];
 #pragma unroll
@@ -996,8 +1002,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     const int cur = kb % NS;
     if (kb + NS - 1 < nkb) {
       const int nx = (kb + NS - 1) % NS;
-      stage<DH>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
-      stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
+      stage<DH, DH != 64>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
+      stage<DH, DH != 64>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
     }
     const char* kt = KT(cur);
     const char* vt = VT(cur);
@@ -1091,8 +1097,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq2_kernel(Args a) {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nkb) {
-      stage<DH>(base, W, s * BKV, kcol, KT(s), wave, lane);
-      stage<DH>(base, W, s * BKV, vcol, VT(s), wave, lane);
+      stage<DH, DH != 64>(base, W, s * BKV, kcol, KT(s), wave, lane);
+      stage<DH, DH != 64>(base, W, s * BKV, vcol, VT(s), wave, lane);
     }
   bf16x8 qf[QG][KS], of[QG][KS], ofw[QG][KS];
   float lse2[QG];
@@ -1140,8 +1146,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq2_kernel(Args a) {
     const int cur = kb % NS;
     if (kb + NS - 1 < nkb) {
       const int nx = (kb + NS - 1) % NS;
-      stage<DH>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
-      stage<DH>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
+      stage<DH, DH != 64>(base, W, (kb + NS - 1) * BKV, kcol, KT(nx), wave, lane);
+      stage<DH, DH != 64>(base, W, (kb + NS - 1) * BKV, vcol, VT(nx), wave, lane);
     }
     // keys of this tile all after this wave's last row: nothing to add (barriers still run)
     if (kb * BKV <= q0w + 31) {
