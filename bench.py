@@ -87,6 +87,11 @@ def main():
     ap.add_argument("--simulate-rank", type=int, default=0)
     ap.add_argument("--sweep", type=int, default=1, choices=[0, 1],
                     help="N > 1: after the timed run, a short bucket_cap_mb x grad-comm-dtype sweep (comm.sweep)")
+    ap.add_argument("--ckpt-budget-s", type=float, default=float(os.environ.get("RTDC_BENCH_CKPT_BUDGET_S", 300)),
+                    help="wall-clock budget of the checkpoint phase; on overrun the measured headline is printed "
+                         "with phase_timed_out and the run exits")
+    ap.add_argument("--sweep-budget-s", type=float, default=float(os.environ.get("RTDC_BENCH_SWEEP_BUDGET_S", 240)))
+    ap.add_argument("--pg-timeout-s", type=float, default=300.0, help="process-group (collective) timeout")
     args = ap.parse_args()
     args.batch_set, args.seq_len_set = args.batch is not None, args.seq_len is not None
     if args.batch is None:
@@ -125,10 +130,16 @@ def main():
 
         args.zero = default_zero_stage(args.model, world)
     if dist_on:
+        import datetime
+
+        # a hung collective raises after the timeout instead of blocking forever (RCCL's
+        # watchdog aborts the communicator; async error handling tears the rank down)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        to = datetime.timedelta(seconds=args.pg_timeout_s)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=to)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=to)
 
     from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
     from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
@@ -198,23 +209,92 @@ def main():
     # every rank must hold bitwise the same parameters (and, without ZeRO, optimizer state)
     in_sync = ranks_in_sync(model, opt, world, dev) if dist_on else None
 
-    ck = {}
+    out = headline(args, wl, model, world, B, T, ms_per_step, samples_per_s, final_loss, overlap, dist_on,
+                   comm_plan, pre, in_sync, dev)
+    # from here on the headline is measured: a later phase that hangs (a stuck collective on a
+    # first contact with a new node, a filesystem that stops answering) must not hide it
+    wd = PhaseWatchdog(out, rank)
+
     if not args.no_ckpt:
         # the throughput above is measured and must be reported even if the checkpoint phase
         # fails (e.g. a filesystem that refuses the shard writes): the failure is reported too
-        try:
-            ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync)
-        except Exception as e:  # noqa: BLE001
-            ck = {"ckpt_unmeasured": f"checkpoint phase failed: {type(e).__name__}: {e}"[:300]}
-            print(f"[bench] rank {rank}: {ck['ckpt_unmeasured']}", file=sys.stderr, flush=True)
+        with wd.phase("checkpoint", args.ckpt_budget_s):
+            try:
+                ck = checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync)
+            except Exception as e:  # noqa: BLE001
+                ck = {"ckpt_unmeasured": f"checkpoint phase failed: {type(e).__name__}: {e}"[:300]}
+                print(f"[bench] rank {rank}: {ck['ckpt_unmeasured']}", file=sys.stderr, flush=True)
+        out.update(ck)
 
-    sweep = None
     if dist_on and args.sweep and args.zero == 0 and not args.overlap_opt:
-        try:
-            sweep = comm_sweep(args, model, opt, net, cur, step, world, sync)
-        except Exception as e:  # noqa: BLE001
-            sweep = {"error": f"{type(e).__name__}: {e}"[:300]}
+        with wd.phase("sweep", args.sweep_budget_s):
+            try:
+                sweep = comm_sweep(args, model, opt, net, cur, step, world, sync)
+            except Exception as e:  # noqa: BLE001
+                sweep = {"error": f"{type(e).__name__}: {e}"[:300]}
+        out["comm"]["sweep"] = sweep
+    wd.stop()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        with wd.phase("teardown", 120.0, exit_code=0):
+            dist.barrier()
+            dist.destroy_process_group()
+        wd.stop()
 
+
+class PhaseWatchdog:
+    """Wall-clock budget per post-headline phase.  If a phase overruns, rank 0 prints the JSON
+    line with everything measured so far plus `"phase_timed_out": <name>` and the process ends
+    with os._exit (no re-exec, no cleanup that could block on the hung collective)."""
+
+    def __init__(self, out: dict, rank: int):
+        import threading
+
+        self.out, self.rank = out, rank
+        self._lock = threading.Lock()
+        self._cur = None  # (name, deadline, exit_code)
+        self._t = threading.Thread(target=self._run, daemon=True, name="bench-watchdog")
+        self._t.start()
+
+    def _run(self):
+        while True:
+            time.sleep(0.5)
+            with self._lock:
+                cur = self._cur
+            if cur is not None and time.monotonic() > cur[1]:
+                name, _d, code = cur
+                if self.rank == 0 and code != 0:
+                    o = dict(self.out)
+                    o["phase_timed_out"] = name
+                    print(json.dumps(o), flush=True)
+                print(f"[bench] rank {self.rank}: phase {name!r} exceeded its budget; exiting", file=sys.stderr,
+                      flush=True)
+                os._exit(code)
+
+    def phase(self, name: str, budget_s: float, exit_code: int = 3):
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            with self._lock:
+                self._cur = (name, time.monotonic() + budget_s, exit_code)
+            try:
+                yield
+            finally:
+                with self._lock:
+                    self._cur = None
+
+        return cm()
+
+    def stop(self):
+        with self._lock:
+            self._cur = None
+
+
+def headline(args, wl, model, world, B, T, ms_per_step, samples_per_s, final_loss, overlap, dist_on, comm_plan,
+             pre, in_sync, dev) -> dict:
+    """The JSON line's fields known right after the timed run."""
     metric, published = _baseline_metric()
     base = published.get("samples_per_sec") if isinstance(published, dict) else None
     out = {
@@ -235,6 +315,7 @@ def main():
                    "params": model.num_params()},
         "samples_per_sec_per_gpu": round(samples_per_s / world, 3),
         "model_tflops_per_gpu": round(wl["flops_per_sample"] * samples_per_s / world / 1e12, 2),
+        "model_tflops_note": wl.get("flops_note", ""),
         "final_loss": round(final_loss, 4),
     }
     if wl.get("tokens_per_sample"):
@@ -249,16 +330,9 @@ def main():
         comm["allreduce_GB_per_s_needed_at_this_step_time"] = round(
             comm["allreduce_bytes_per_step"] * 2 * (world - 1) / world / (ms_per_step / 1e3) / 1e9, 2)
         comm["preflight"] = pre
-        if sweep is not None:
-            comm["sweep"] = sweep
         out["ranks_in_sync"] = in_sync
     out["comm"] = comm
-    out.update(ck)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist_on:
-        dist.barrier()
-        dist.destroy_process_group()
+    return out
 
 
 def preflight(world, rank, dev, args) -> dict:
@@ -341,6 +415,7 @@ def comm_sweep(args, model, opt, net, cur, step, world, sync) -> list:
     space and optimizer); the timed headline above is untouched."""
     from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
 
+    _maybe_hang("sweep")
     out = []
     net.detach()
     cells = [(d, c) for d in ("fp32", "bf16") for c in (16.0, 32.0, 64.0, 128.0)]
@@ -441,10 +516,21 @@ def build_workload(args, dev, rank):
     return dict(model=model, opt=opt, batch=B, seq_len=T, loss=loss, tokens_per_sample=T,
                 unit=f"samples/s (sequences of {T} tokens, all GPUs)", optim_name="fused AdamW (fp32 master)",
                 data="synthetic (random tokens), random-init weights",
-                flops_per_sample=model.flops_per_token(T) * T)
+                flops_per_sample=model.flops_per_token(T, causal=True) * T,
+                flops_note="6N + 6·L·d·T per token (N without the position/input embedding; causal attention: "
+                           "the lower triangle only - rounds 1-4 counted the full square, ~7 % more on GPT-2)")
+
+
+def _maybe_hang(phase: str) -> None:
+    """RTDC_BENCH_HANG_PHASE=<phase>: fault injection for the watchdog test (a hung phase)."""
+    if os.environ.get("RTDC_BENCH_HANG_PHASE") == phase:
+        print(f"[bench] injected hang in phase {phase!r}", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(60)
 
 
 def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
+    _maybe_hang("checkpoint")
     base = args.ckpt_dir or os.environ.get("RTDC_BENCH_CKPT_DIR") or tempfile.gettempdir()
     path = os.path.join(base, "rtdc_bench_ckpt")
     if rank == 0:
@@ -498,16 +584,35 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     if nbytes_of(state()) / share * 1.15 > free:
         return {"ckpt_unmeasured": f"state larger than free disk ({free / 1e9:.0f} GB)"}
 
-    # ---- async save overlapped with training steps
+    # ---- startup-time allocation a trainer does once (engine: pinned ring + writers; this
+    # rank's HBM snapshot arena), reported on its own, outside every timed window below
+    sync()
+    tp = time.perf_counter()
+    arena_bytes = dcp.prepare_async(state(), simulate=sim)
+    sync()
+    t_prepare = time.perf_counter() - tp
+    # ---- async save overlapped with training steps; each step timed on the device (events
+    # between consecutive steps, no host sync inside the window) and on the host (enqueue)
+    cuda = dev.type == "cuda"
+    n_ov = max(1, args.overlap_steps)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n_ov + 1)] if cuda else []
     sync()
     t0 = time.perf_counter()
     h = dcp.async_save(state(), path, simulate=sim)
     t_resume = time.perf_counter() - t0  # training may continue from here
     t1 = time.perf_counter()
-    for i in range(args.overlap_steps):
+    host_each = []
+    if cuda:
+        evs[0].record()
+    for i in range(n_ov):
+        th = time.perf_counter()
         step(i)
+        if cuda:
+            evs[i + 1].record()
+        host_each.append((time.perf_counter() - th) * 1e3)
     sync()
-    overlap_ms = (time.perf_counter() - t1) / max(1, args.overlap_steps) * 1e3
+    overlap_ms = (time.perf_counter() - t1) / n_ov * 1e3
+    each_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n_ov)] if cuda else host_each
     local_write = h.wait()
     if dist.is_initialized():
         dist.barrier()
@@ -575,6 +680,12 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
         "ckpt_write_GBps": round(total / max(t_sync, 1e-9) / 1e9, 3),
         "ckpt_restore_GBps": round(total / max(t_restore, 1e-9) / 1e9, 3),
         "ms_per_step_during_async_save": round(overlap_ms, 3),
+        "ms_per_step_during_async_save_each": [round(x, 3) for x in each_ms],
+        "host_ms_per_step_during_async_save_each": [round(x, 3) for x in host_each],
+        "ckpt_d2h_drained_s": (round(h.d2h_s, 4) if h.d2h_s else None),  # submit -> last byte in the pinned ring
+        "ckpt_d2h_mode": _d2h_mode(),
+        "ckpt_prepare_s": round(t_prepare, 4),  # one-time: engine + snapshot arena (startup in a trainer)
+        "ckpt_snapshot_arena_bytes": int(arena_bytes),
         "ckpt_format": f"torch.distributed.checkpoint (.metadata + __<rank>_0.distcp x {world}), native engine",
         "ckpt_scope": "model + optimizer + step" if scope == "full" else "model + step",
         "ckpt_fs": _fs_of(base),
@@ -589,6 +700,15 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
         if zsim:
             out["ckpt_simulated"]["layout"] = "ZeRO-1 owner shards (optimizer state), dedup plan (parameters)"
     return out
+
+
+def _d2h_mode() -> str:
+    from ray_torch_distributed_checkpoint_amd.checkpoint import torchsave
+
+    try:
+        return torchsave.get_engine().d2h_mode
+    except Exception:  # noqa: BLE001
+        return "?"
 
 
 def drop_page_cache(path: str) -> float:

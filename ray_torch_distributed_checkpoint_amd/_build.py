@@ -103,7 +103,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         tmp = out + ".tmp"
         link = [hipcc, "-shared", "-fPIC", f"--offload-arch={arch}", *objs, "-o", tmp,
                 "-L", os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
-                "-ltorch_hip", "-ltorch_python", "-lz", f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+                "-ltorch_hip", "-ltorch_python", "-lhsa-runtime64", "-lz", f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
         _run(link, verbose)
         os.replace(tmp, out)
     return out

@@ -41,7 +41,7 @@ from torch.distributed.checkpoint.metadata import (BytesStorageMetadata, ChunkSt
                                                    TensorStorageMetadata)
 
 from ..ops import _ext
-from . import torchsave
+from . import snapshot, torchsave
 
 METADATA_FN = ".metadata"
 DCP_VERSION = "1.0.0"
@@ -162,6 +162,9 @@ class AsyncSave:
         self.checkpoint_id, self._h, self._metadata = checkpoint_id, handle, metadata
         self.rank, self.t_start, self.t_return, self.nbytes, self.pg = rank, t_start, t_return, nbytes, pg
         self.write_s = None
+        self.d2h_s = None  # seconds until the snapshot's last byte reached the pinned ring
+        self._h_timings = getattr(handle, "d2h_seconds", None)
+        self._lease = None
         self._error: BaseException | None = None
         # waited on by the training loop and by the session's committer thread
         self._lock = threading.Lock()
@@ -175,15 +178,26 @@ class AsyncSave:
                 try:
                     if self._h is not None:
                         self._h.wait()
+                    from ..parallel import health
+
+                    health.assert_healthy("checkpoint commit", sync=False)
                     if getattr(self, "_verify", None):
                         _verify_written(self._verify)
                         self._verify = None
+                    self._lease = None
                     self.write_s = time.perf_counter() - self.t_start
+                    if self._h_timings is not None:
+                        self.d2h_s = self._h_timings()
                 except BaseException as e:  # noqa: BLE001
                     self._error = e
                 finally:
                     self._h = None
+                    self._lease = None
             if self._error is not None:
+                from ..parallel.health import CommPoisonedError
+
+                if isinstance(self._error, CommPoisonedError):
+                    raise CommPoisonedError(str(self._error)) from self._error
                 raise IOError(f"sharded save to {self.checkpoint_id} failed: {self._error}") from self._error
             return self.write_s
 
@@ -285,18 +299,10 @@ def _merge_rank_metadata(metadata: Metadata, parts: list) -> None:
         metadata.planner_data.update(p.planner_data)
 
 
-def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsync: bool = True,
-               crc: bool = True, replicated: bool = True, simulate=None) -> AsyncSave:
-    """Start a sharded save; returns once the HBM snapshot is enqueued (non-blocking).
-    `simulate=(W, r)`: see `_simulated`."""
-    t0 = time.perf_counter()
-    from ..parallel import health
-
-    # a timed-out P2P collective left NaN gradients behind: never snapshot that state
-    health.assert_healthy("checkpoint save")
-    sim = _simulated(simulate)
+def _plan_save(state_dict, process_group, replicated, sim):
+    """(world, rank, items, flatten mapping, {rank: owned items}) of a save - deterministic on
+    every rank, no collectives."""
     world, rank = sim if sim else _world(process_group)
-    os.makedirs(checkpoint_id, exist_ok=True)
     items, mapping = _collect(state_dict, world, rank)
     rep = [it for it in items if it.owner is None]
     if replicated:
@@ -309,11 +315,42 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     per_rank: dict[int, list[_Item]] = {r: [] for r in range(world)}
     for it in items:
         per_rank[it.owner].append(it)
+    return world, rank, items, mapping, per_rank
+
+
+def prepare_async(state_dict: dict, process_group=None, *, replicated: bool = True, simulate=None) -> int:
+    """Startup-time allocation for async saves of `state_dict`-shaped state: the native engine
+    (pinned ring, writer threads) and this rank's HBM snapshot arena, so that the first
+    checkpoint of a run allocates nothing between two training steps (a trainer calls this
+    once; the session does for its registered state).  Returns the arena bytes."""
+    sim = _simulated(simulate)
+    _w, rank, _items, _m, per_rank = _plan_save(state_dict, process_group, replicated, sim)
+    torchsave.get_engine()
+    return snapshot.reserve([it.tensor for it in per_rank[rank] if it.kind == "tensor"])
+
+
+def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsync: bool = True,
+               crc: bool = True, replicated: bool = True, simulate=None) -> AsyncSave:
+    """Start a sharded save; returns once the HBM snapshot is enqueued (non-blocking).
+    `simulate=(W, r)`: see `_simulated`."""
+    t0 = time.perf_counter()
+    from ..parallel import health
+
+    # a timed-out P2P collective left NaN gradients behind: never snapshot that state.  No
+    # device sync here (that would drain the compute stream on the non-blocking path): the word
+    # is checked again in wait(), after the drain - the snapshot is stream-ordered after every
+    # collective the optimizer consumed, so by then any timeout among them is visible
+    health.assert_healthy("checkpoint save", sync=False)
+    sim = _simulated(simulate)
+    world, rank, items, mapping, per_rank = _plan_save(state_dict, process_group, replicated, sim)
+    os.makedirs(checkpoint_id, exist_ok=True)
     mine = per_rank[rank]
-    # HBM / host snapshot of owned tensors: cloned in stream order on the compute stream
-    for it in mine:
-        if it.kind == "tensor":
-            it.tensor = it.tensor.clone(memory_format=torch.contiguous_format)
+    # HBM / host snapshot of owned tensors, in stream order on the compute stream: into a
+    # reused arena, one copy per flat storage (checkpoint/snapshot.py)
+    owned_t = [it for it in mine if it.kind == "tensor"]
+    lease, snaps = snapshot.take([it.tensor for it in owned_t])
+    for it, t in zip(owned_t, snaps):
+        it.tensor = t
     ready = None
     if any(it.kind == "tensor" and it.tensor.is_cuda for it in mine):
         ready = torch.cuda.Event()
@@ -367,13 +404,14 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     if mine:
         arcs = _archives_for(mine, with_ptrs=True)
         path = os.path.join(checkpoint_id, f"__{rank}_0.distcp")
-        handle = torchsave.submit_files([(path, fsync, crc, arcs)], [it.tensor for it in mine if it.tensor is not None],
-                                        nbytes, ready)
+        handle = torchsave.submit_files([(path, fsync, crc, arcs)],
+                                        [lease] + [it.tensor for it in mine if it.tensor is not None], nbytes, ready)
         if os.environ.get("RTDC_CKPT_VERIFY", "0") == "1":
             _, lay = ext.plan_layout(_archives_for(mine, with_ptrs=False))
             verify = [(path, base, size, it.tensor) for it, (base, size, _r) in zip(mine, lay) if it.kind == "tensor"]
     h = AsyncSave(checkpoint_id, handle, metadata, rank, t0, time.perf_counter() - t0, nbytes, process_group)
     h._verify = verify
+    h._lease = lease if verify else None  # the verify pass reads the snapshot after the drain
     return h
 
 

@@ -163,6 +163,14 @@ class SaveHandle:
         self._error: str | None = None
         self._lock = threading.Lock()  # waited on by the training thread AND the committer thread
 
+    def d2h_seconds(self) -> float | None:
+        """After wait(): seconds from submit until the last device piece was in the pinned
+        ring (the end of the D2H traffic that overlaps training)."""
+        try:
+            return get_engine().timings(self.job_id)[0]
+        except Exception:  # noqa: BLE001
+            return None
+
     def done(self) -> bool:
         return self._result is not None or self._error is not None or get_engine().poll(self.job_id)
 
@@ -172,7 +180,11 @@ class SaveHandle:
         with self._lock:
             if self._result is None and self._error is None:
                 err, _secs = get_engine().wait(self.job_id)
-                self._keep = None
+                self._keep = None  # the snapshot (arena lease / clones) is drained: release it
+                from ..parallel import health
+
+                if not err and health.error():
+                    err = "a P2P gradient all-reduce timed out before the snapshot (state poisoned)"
                 if err:
                     self._error = str(err)
                 else:
@@ -218,16 +230,18 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
     """
     from ..parallel import health
 
-    health.assert_healthy("checkpoint save")
+    health.assert_healthy("checkpoint save", sync=False)  # re-checked after the drain (SaveHandle.wait)
     pkl, tensors = pickle_state(obj)
     if snapshot is None:
         snapshot = async_
-    contig = []
-    for t in tensors:
-        t = t.detach()
-        if snapshot or not t.is_contiguous() or t.storage_offset() < 0:
-            t = t.clone(memory_format=torch.contiguous_format)
-        contig.append(t)
+    lease = None
+    if snapshot:
+        from . import snapshot as _snap
+
+        lease, contig = _snap.take(tensors)
+    else:
+        contig = [t.detach() if t.is_contiguous() else t.detach().clone(memory_format=torch.contiguous_format)
+                  for t in tensors]
     ready = None
     if any(t.is_cuda for t in contig):
         ready = torch.cuda.Event()
@@ -235,7 +249,7 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
     stor = _storages_of(contig)
     nbytes = sum(s[1] for s in stor)
     recs = build_records(pkl, stor, prefix=os.path.splitext(os.path.basename(path))[0] or "archive")
-    h = submit_files([(path, fsync, crc, [(False, recs)])], contig, nbytes, ready)
+    h = submit_files([(path, fsync, crc, [(False, recs)])], [lease] + contig, nbytes, ready)
     if async_:
         return h
     h.wait()

@@ -1066,6 +1066,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             e.read_to_device(path, offs, lens, dsts, nthreads);
           },
           py::arg("path"), py::arg("offs"), py::arg("lens"), py::arg("dsts"), py::arg("nthreads") = 8)
+      .def(
+          "timings",
+          [](Engine& e, int id) {
+            py::gil_scoped_release nogil;
+            return e.timings(id);
+          },
+          "(seconds to the last D2H piece in the pinned ring, seconds to durable) of a finished job")
+      .def_property_readonly("d2h_mode", &Engine::d2h_mode)
       .def_property_readonly("slot_bytes", &Engine::slot_bytes)
       .def_property_readonly("pinned", &Engine::pinned);
 }

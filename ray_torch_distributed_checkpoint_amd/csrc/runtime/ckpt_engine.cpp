@@ -7,7 +7,8 @@
 //
 //   device snapshot (HBM, taken by the caller on its compute stream)
 //     -> bounded ring of pinned host slots (hipHostMalloc)            [PinnedRing]
-//     -> hipMemcpyAsync D2H on a dedicated non-blocking copy stream     [enqueue thread]
+//     -> D2H by the SDMA engines (hsa_amd_memory_async_copy, no AQL queue)  [enqueue thread]
+//        (or hipMemcpyAsync on a dedicated copy stream: RTDC_CKPT_D2H=hip)
 //     -> writer thread pool: event wait, CRC32 of the piece, pwrite     [writer threads]
 //     -> per-file finalize: CRCs patched into the zip headers, central directory, fsync.
 //
@@ -19,6 +20,8 @@
 // Reads (restore) go the other way: `read_to_host` preads file ranges with a thread pool into
 // caller memory (pinned or pageable); H2D and the cross-rank broadcast are issued from Python.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <zlib.h>
 #include <fcntl.h>
 #include <sys/resource.h>
@@ -30,6 +33,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -272,7 +276,10 @@ class PinnedRing {
       slots_.push_back(p);
       pinned_.push_back(pinned);
       hipEvent_t ev = nullptr;
-      if (g_have_gpu()) hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      // blocking sync: a writer waiting on its slot sleeps instead of spinning a core (the
+      // default event spins, and 8 spinning writers exhaust a cgroup CPU quota that the
+      // rank's launch thread shares - the whole process is then throttled mid-step)
+      if (g_have_gpu()) hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventBlockingSync);
       events_.push_back(ev);
       free_.push_back((int)i);
     }
@@ -315,9 +322,38 @@ class PinnedRing {
 };
 
 // ------------------------------------------------------------------------------------------
+// SDMA drain.  A HIP copy stream is one of the process's GPU_MAX_HW_QUEUES (4) AQL queues,
+// shared round-robin with every other stream: when it lands on the compute stream's queue, the
+// barrier packet that orders each D2H copy blocks the kernels queued behind it, and a 1.5 GB
+// drain costs the training step the whole copy time.  hsa_amd_memory_async_copy hands the
+// piece straight to an SDMA engine (device -> pinned host, src agent != dst agent, so never a
+// blit kernel on the CUs) with an HSA completion signal: no AQL packet, no CU, no queue shared
+// with compute.  The snapshot's readiness is waited on the host first (the event recorded after
+// the snapshot copies carries a system-scope release, so the bytes are visible to the DMA).
+// ------------------------------------------------------------------------------------------
+static bool agent_of(const void* p, hsa_agent_t* a) {
+  hsa_amd_pointer_info_t info;
+  std::memset(&info, 0, sizeof(info));
+  info.size = sizeof(info);
+  if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
+  if (info.type == HSA_EXT_POINTER_TYPE_UNKNOWN || info.agentOwner.handle == 0) return false;
+  *a = info.agentOwner;
+  return true;
+}
+
+// host wait without spinning a core (the caller's event may use active synchronization)
+static hipError_t wait_event_sleepy(hipEvent_t ev) {
+  while (true) {
+    hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Engine
 // ------------------------------------------------------------------------------------------
-// One file = a sequence of archives written back to back: a torch.save zip archive per tensor
+// One file =a sequence of archives written back to back: a torch.save zip archive per tensor
 // item (the DCP `__r_i.distcp` layout: each item at a recorded (offset, length), readable by
 // `torch.load` on the slice), or a raw byte item (DCP BYTE_IO).  A `.pt` file is one archive.
 struct Archive {
@@ -377,7 +413,14 @@ struct SaveJob {
   bool done = false;
   std::string error;
   double t_submit = 0, t_done = 0;
+  std::atomic<double> t_d2h{0.0};  // last device piece landed in the pinned ring
+  std::atomic<int> dev_left{0};
   uint64_t bytes = 0;
+};
+
+struct JobResult {
+  std::string error;
+  double durable_s = 0, d2h_s = 0;
 };
 
 static double now_s() {
@@ -391,6 +434,17 @@ class Engine {
     if (g_have_gpu()) {
       hipSetDevice(device_);
       hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
+      const char* m = std::getenv("RTDC_CKPT_D2H");
+      const bool want_sdma = !(m && std::string(m) == "hip");
+      // HIP has initialised the runtime already; hsa_init only takes a reference on it
+      if (want_sdma && ring_.pinned() && hsa_init() == HSA_STATUS_SUCCESS && agent_of(ring_.ptr(0), &host_agent_)) {
+        for (size_t i = 0; i < ring_.nslots(); ++i) {
+          hsa_signal_t sg{0};
+          if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) break;
+          sig_.push_back(sg);
+        }
+        sdma_ = sig_.size() == ring_.nslots();
+      }
     }
     for (int i = 0; i < nwriters; ++i) writers_.emplace_back([this] { writer_loop(); });
     enqueuer_ = std::thread([this] { enqueue_loop(); });
@@ -410,7 +464,11 @@ class Engine {
     jcv_.notify_all();
     for (auto& t : writers_) t.join();
     if (stream_) hipStreamDestroy(stream_);
+    for (auto& sg : sig_) hsa_signal_destroy(sg);
   }
+
+  // "sdma" (hsa_amd_memory_async_copy) or "hip" (hipMemcpyAsync on the copy stream)
+  std::string d2h_mode() const { return sdma_ ? "sdma" : (stream_ ? "hip" : "host"); }
 
   int submit(std::vector<std::shared_ptr<FileJob>> files, hipEvent_t ready) {
     auto job = std::make_shared<SaveJob>();
@@ -454,6 +512,18 @@ class Engine {
   // job itself - its staged buffers - is released), so a second waiter on the same id gets the
   // same answer - in particular the same error - instead of "unknown id == success".
   std::pair<std::string, double> wait(int id) {
+    JobResult r = wait_result(id);
+    return {r.error, r.durable_s};
+  }
+
+  // seconds from submit until the last device piece had landed in the pinned ring (the end of
+  // the D2H traffic that overlaps training) and until durable; valid after wait()
+  std::pair<double, double> timings(int id) {
+    JobResult r = wait_result(id);
+    return {r.d2h_s, r.durable_s};
+  }
+
+  JobResult wait_result(int id) {
     std::unique_lock<std::mutex> lk(jmu_);
     auto it = jobs_.find(id);
     if (it == jobs_.end()) {
@@ -463,7 +533,8 @@ class Engine {
     }
     std::shared_ptr<SaveJob> job = it->second;
     jcv_.wait(lk, [&] { return job->done; });
-    std::pair<std::string, double> res{job->error, job->t_done - job->t_submit};
+    const double d2h = job->t_d2h.load();
+    JobResult res{job->error, job->t_done - job->t_submit, d2h > 0 ? d2h - job->t_submit : 0.0};
     if (jobs_.erase(id)) {
       results_[id] = res;
       result_order_.push_back(id);
@@ -557,7 +628,8 @@ class Engine {
     int slot = -1;
     const void* host = nullptr;  // direct host source (no slot)
     uint64_t len = 0, off = 0;
-    bool wait_event = false;
+    bool wait_event = false;   // copy-stream D2H: ring slot event
+    bool wait_signal = false;  // SDMA D2H: ring slot HSA signal
     bool final_marker = false;
   };
 
@@ -582,8 +654,30 @@ class Engine {
 
   void run_job(std::shared_ptr<SaveJob> job) {
     if (g_have_gpu()) hipSetDevice(device_);
-    if (stream_ && job->ready) hipStreamWaitEvent(stream_, job->ready, 0);
     const size_t S = ring_.slot_bytes();
+    int dev_pieces = 0;
+    const char* first_dev = nullptr;
+    for (auto& f : job->files)
+      for (auto& a : f->archives)
+        for (auto& r : a.recs)
+          if (r.src && r.on_device) {
+            dev_pieces += (int)((r.nbytes + S - 1) / S);
+            if (!first_dev) first_dev = r.src;
+          }
+    job->dev_left = dev_pieces;
+    if (dev_pieces == 0) job->t_d2h = now_s();
+    // SDMA needs the source's GPU agent (a caching-allocator block is an ordinary HSA
+    // allocation); anything else falls back to the copy stream for this job
+    hsa_agent_t gpu_agent{0};
+    const bool sdma = sdma_ && first_dev && agent_of(first_dev, &gpu_agent);
+    if (job->ready) {
+      if (sdma) {
+        hipError_t e = wait_event_sleepy(job->ready);
+        if (e != hipSuccess) throw std::runtime_error(std::string("snapshot event: ") + hipGetErrorString(e));
+      } else if (stream_) {
+        hipStreamWaitEvent(stream_, job->ready, 0);
+      }
+    }
     for (auto& f : job->files) {
       f->fd = ::open(f->path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
       if (f->fd < 0) throw std::runtime_error("open failed: " + f->path + ": " + strerror(errno));
@@ -615,14 +709,25 @@ class Engine {
             w.off = a.base + r.data_off + o;
             if (r.on_device) {
               const int s = ring_.acquire();
-              hipError_t e = hipMemcpyAsync(ring_.ptr(s), r.src + o, len, hipMemcpyDeviceToHost, stream_);
-              if (e != hipSuccess) {
-                ring_.release(s);
-                throw std::runtime_error(std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+              if (sdma) {
+                hsa_signal_store_screlease(sig_[s], 1);
+                hsa_status_t st = hsa_amd_memory_async_copy(ring_.ptr(s), host_agent_, r.src + o, gpu_agent, len, 0,
+                                                            nullptr, sig_[s]);
+                if (st != HSA_STATUS_SUCCESS) {
+                  ring_.release(s);
+                  throw std::runtime_error("hsa_amd_memory_async_copy failed: status " + std::to_string((int)st));
+                }
+                w.wait_signal = true;
+              } else {
+                hipError_t e = hipMemcpyAsync(ring_.ptr(s), r.src + o, len, hipMemcpyDeviceToHost, stream_);
+                if (e != hipSuccess) {
+                  ring_.release(s);
+                  throw std::runtime_error(std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+                }
+                hipEventRecord(ring_.event(s), stream_);
+                w.wait_event = true;
               }
-              hipEventRecord(ring_.event(s), stream_);
               w.slot = s;
-              w.wait_event = true;
             } else {
               w.host = r.src + o;
             }
@@ -680,7 +785,17 @@ class Engine {
         } else {
           const void* src = w.host;
           if (w.slot >= 0) {
-            if (w.wait_event) hipEventSynchronize(ring_.event(w.slot));
+            if (w.wait_event) {
+              hipError_t e = hipEventSynchronize(ring_.event(w.slot));
+              if (e != hipSuccess) throw std::runtime_error(std::string("D2H: ") + hipGetErrorString(e));
+            }
+            if (w.wait_signal) {
+              // blocked wait: the writer sleeps on the signal's interrupt, no spinning core
+              const hsa_signal_value_t v = hsa_signal_wait_scacquire(sig_[w.slot], HSA_SIGNAL_CONDITION_LT, 1,
+                                                                     UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+              if (v < 0) throw std::runtime_error("SDMA D2H copy failed");
+            }
+            if ((w.wait_event || w.wait_signal) && w.job->dev_left.fetch_sub(1) == 1) w.job->t_d2h = now_s();
             src = ring_.ptr(w.slot);
           }
           uint32_t c = 0;
@@ -805,7 +920,10 @@ class Engine {
   std::deque<std::shared_ptr<SaveJob>> save_q_;
   std::deque<WJob> wq_;
   std::map<int, std::shared_ptr<SaveJob>> jobs_;
-  std::map<int, std::pair<std::string, double>> results_;  // outcomes of waited (finished) jobs
+  std::map<int, JobResult> results_;  // outcomes of waited (finished) jobs
+  bool sdma_ = false;
+  hsa_agent_t host_agent_{0};
+  std::vector<hsa_signal_t> sig_;  // per ring slot: SDMA completion
   std::deque<int> result_order_;
   int next_id_ = 1;
   std::atomic<bool> stop_{false};

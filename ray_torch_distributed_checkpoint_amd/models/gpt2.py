@@ -135,8 +135,10 @@ class GPT2(nn.Module):
         logits = ops.linear(x, self.wte)
         return logits[..., : self.cfg.vocab_size]
 
-    def flops_per_token(self, T: int) -> float:
+    def flops_per_token(self, T: int, causal: bool = True) -> float:
         """Training FLOPs per token (6N + attention), N without the embedding table."""
         c = self.cfg
         n = self.num_params() - c.n_positions * c.n_embd
-        return 6 * n + 12 * c.n_layer * c.n_embd * T
+        # attention scores + weighted sum: 12·L·d·T per token over the full T×T square; a causal
+        # mask computes only the lower triangle, so the causal count is half of that
+        return 6 * n + (6 if causal else 12) * c.n_layer * c.n_embd * T

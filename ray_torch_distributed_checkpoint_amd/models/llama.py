@@ -150,10 +150,12 @@ class Llama(nn.Module):
                         f"layers.{i}.gate_proj": g, f"layers.{i}.up_proj": u})
         return out
 
-    def flops_per_token(self, T: int) -> float:
+    def flops_per_token(self, T: int, causal: bool = True) -> float:
         c = self.cfg
         n = self.num_params() - c.vocab_size * c.dim  # input embedding is a gather
-        return 6 * n + 12 * c.n_layers * c.dim * T
+        # attention scores + weighted sum: 12·L·d·T per token over the full T×T square; a causal
+        # mask computes only the lower triangle, so the causal count is half of that
+        return 6 * n + (6 if causal else 12) * c.n_layers * c.dim * T
 
 
 class _nullctx:

@@ -183,13 +183,16 @@ class DistributedDataParallel(nn.Module):
         if self._collective and grad_comm_dtype == "bf16":
             self._comm = torch.empty(self.space.numel, dtype=torch.bfloat16, device=dev)
         if self._collective:
-            self._verify_plan_across_ranks()
             self._engine = self._native_engine(process_group)
-            if self._engine is not None and self.defer_tail and tail_piece_mb > 0:
-                # the deferred last bucket (GPT-2: the 154 MB tied token table) as collectives of
-                # <= tail_piece_mb communicated bytes: the optimizer updates piece i while pieces
-                # i+1.. are still on the wire (see FlatParamSpace.pending_tail)
-                self._engine.set_tail_split(int(tail_piece_mb * (1 << 20) / esz))
+            # the deferred last bucket (GPT-2: the 154 MB tied token table) as collectives of
+            # <= tail_piece_mb communicated bytes: the optimizer updates piece i while pieces
+            # i+1.. are still on the wire (see FlatParamSpace.pending_tail)
+            tail_max = int(tail_piece_mb * (1 << 20) / esz) \
+                if self._engine is not None and self.defer_tail and tail_piece_mb > 0 else 0
+            # everything that shapes the sequence of collectives must agree before the first one
+            self._verify_plan_across_ranks(tail_max, p2p_max_kb)
+            if tail_max:
+                self._engine.set_tail_split(tail_max)
             self._attach_p2p(process_group, p2p_max_kb)
             for p in self.space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
@@ -226,13 +229,20 @@ class DistributedDataParallel(nn.Module):
             raise RuntimeError(f"DDP {what} differs across ranks (rank {dist.get_rank(self.process_group)} has "
                                f"{value}): collectives would deadlock or mix unrelated buffers")
 
-    def _verify_plan_across_ranks(self) -> None:
+    def _verify_plan_across_ranks(self, tail_max: int = 0, p2p_max_kb: float = 0.0) -> None:
         """Parameter shapes + bucket plan fingerprint identical on every rank (the role of torch
-        DDP's _verify_param_shape_across_processes)."""
+        DDP's _verify_param_shape_across_processes) - including every knob that
+        changes the number or sizes of the collectives: the deferred tail's piece split, the
+        communicated dtype, ZeRO, the engine and the P2P threshold.  Ranks that disagree on any
+        of them would issue different collective sequences (hang, or sums over mismatched
+        ranges); this raises before the first one instead."""
         import zlib
 
         desc = ";".join(f"{tuple(s.shape)}@{s.offset}" for s in self.space.segments)
         desc += "|" + ",".join(f"{b.start}-{b.end}" for b in self.buckets)
+        desc += (f"|tail={tail_max}|defer={int(bool(self.defer_tail))}|comm={self.grad_comm_dtype}"
+                 f"|zero={int(self.zero)}|engine={'native' if self._engine is not None else 'python'}"
+                 f"|p2p={float(p2p_max_kb)}")
         self._agree(zlib.crc32(desc.encode()) & 0x7FFFFFFF, "parameter/bucket plan")
 
     def _native_engine(self, process_group):
@@ -266,6 +276,9 @@ class DistributedDataParallel(nn.Module):
         Opt-in (0 = off); needs the native engine, device gradients and <= 8 ranks."""
         self.p2p = None
         self.p2p_max_bytes = 0
+        # a re-wrap reuses the flat space: never keep a previous communicator's error word
+        # (freed with it, or set by its timeout) as this wrap's optimizer skip flag
+        self.space.skip_ptr = 0
         if max_kb <= 0 or self._engine is None or self.space.device.type != "cuda" or self.world_size > 8 \
                 or self.zero:
             return
@@ -446,6 +459,12 @@ class DistributedDataParallel(nn.Module):
             h.remove()
         self._hooks = []
         self._engine = None
+        if self.p2p is not None:
+            from . import health
+
+            health.unregister(self.p2p)
+            self.space.skip_ptr = 0
+            self.p2p = None
 
     # ------------------------------------------------------------------ passthrough
     def state_dict(self, *args, **kwargs):

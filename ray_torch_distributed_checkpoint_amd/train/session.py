@@ -197,7 +197,7 @@ class _Session:
 
         # a rank whose gradient collective timed out (NaN-poisoned, update skipped) fails here,
         # before the commit barrier: the attempt dies and nothing of this report is committed
-        health.assert_healthy("report")
+        health.assert_healthy("report", sync=False)  # the save's wait() re-checks after its drain
         rank = self.ctx.world_rank
         n = self.n_reports
         key = f"s{self.ctx.attempt}/r{n}"
