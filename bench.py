@@ -557,7 +557,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
             from ray_torch_distributed_checkpoint_amd.checkpoint.sharded import simulated_zero_optimizer_state
 
             msd = get_state_dict(model, None)[0]
-            osd = simulated_zero_optimizer_state(model, opt, sim[0], sim[1], args.bucket_mb)
+            osd = simulated_zero_optimizer_state(model, opt, sim[0], sim[1], args.bucket_mb, args.grad_comm_dtype)
         else:
             msd, osd = get_state_dict(model, opt)
         return {"model": msd, "optim": osd, "step": 1} if scope == "full" else {"model": msd, "step": 1}
@@ -591,19 +591,22 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     arena_bytes = dcp.prepare_async(state(), simulate=sim)
     sync()
     t_prepare = time.perf_counter() - tp
-    # ---- async save overlapped with training steps; each step timed on the device (events
-    # between consecutive steps, no host sync inside the window) and on the host (enqueue)
+    # ---- async save overlapped with training steps, as a training loop issues it: between two
+    # steps with the device still busy (no host sync before the save - an idle device drops its
+    # clocks and the next step pays the ramp).  Each step timed on the device (events between
+    # consecutive steps; the first interval also holds the HBM snapshot copy) and on the host.
     cuda = dev.type == "cuda"
     n_ov = max(1, args.overlap_steps)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n_ov + 1)] if cuda else []
-    sync()
+    for i in range(2):  # back to a busy device after the prepare's sync
+        step(i)
+    if cuda:
+        evs[0].record()
     t0 = time.perf_counter()
     h = dcp.async_save(state(), path, simulate=sim)
     t_resume = time.perf_counter() - t0  # training may continue from here
     t1 = time.perf_counter()
     host_each = []
-    if cuda:
-        evs[0].record()
     for i in range(n_ov):
         th = time.perf_counter()
         step(i)
@@ -611,8 +614,8 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
             evs[i + 1].record()
         host_each.append((time.perf_counter() - th) * 1e3)
     sync()
-    overlap_ms = (time.perf_counter() - t1) / n_ov * 1e3
     each_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n_ov)] if cuda else host_each
+    overlap_ms = sum(each_ms) / n_ov if cuda else (time.perf_counter() - t1) / n_ov * 1e3
     local_write = h.wait()
     if dist.is_initialized():
         dist.barrier()
@@ -679,7 +682,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
         "ckpt_save_plus_restore_s": round(t_sync + t_restore, 4),
         "ckpt_write_GBps": round(total / max(t_sync, 1e-9) / 1e9, 3),
         "ckpt_restore_GBps": round(total / max(t_restore, 1e-9) / 1e9, 3),
-        "ms_per_step_during_async_save": round(overlap_ms, 3),
+        "ms_per_step_during_async_save": round(overlap_ms, 3),  # device time, snapshot copy included
         "ms_per_step_during_async_save_each": [round(x, 3) for x in each_ms],
         "host_ms_per_step_during_async_save_each": [round(x, 3) for x in host_each],
         "ckpt_d2h_drained_s": (round(h.d2h_s, 4) if h.d2h_s else None),  # submit -> last byte in the pinned ring

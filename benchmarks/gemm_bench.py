@@ -73,9 +73,14 @@ def main():
     ap.add_argument("--set", default="gpt2", choices=["gpt2", "llama", "all"])
     ap.add_argument("--sweep", action="store_true", help="also time forced tile configurations (all layouts)")
     ap.add_argument("--cfgs", default="0,6,7", help="tile configurations for --sweep")
+    ap.add_argument("--wgrad-group", default=None, choices=["llama", "gpt2"],
+                    help="time one layer's grouped weight-gradient launch (gemm_bf16_grouped) against the "
+                         "same products on hipBLASLt with fp32 output")
     args = ap.parse_args()
     torch.manual_seed(0)
     warm_up_clocks()
+    if args.wgrad_group:
+        return wgrad_group(args)
     res = []
     shapes = {"gpt2": SHAPES, "llama": LLAMA_SHAPES, "all": SHAPES + LLAMA_SHAPES}[args.set]
     for name, M, K, N in shapes:
@@ -131,6 +136,42 @@ def main():
         row["fwd_rel_err"] = err
         res.append(row)
         print(json.dumps(row), flush=True)
+
+
+def wgrad_group(args):
+    """One grouped launch of a layer's weight gradients (Llama-3-8B: qkv, o, gate_up, down at
+    2048 tokens; GPT-2: two layers' qkv / proj / fc / mlp_proj at 16384 tokens) vs hipBLASLt."""
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+
+    if args.wgrad_group == "llama":
+        M, prods = 2048, [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
+    else:
+        M, prods = 16384, [(2304, 768), (768, 768), (3072, 768), (768, 3072)] * 2
+    dys = [torch.randn(M, n, device="cuda").bfloat16() for n, _ in prods]
+    xs = [torch.randn(M, k, device="cuda").bfloat16() for _, k in prods]
+    outs = [torch.empty(n, k, device="cuda") for n, k in prods]
+    dims = []
+    for n, k in prods:
+        dims += [n, k, M, n, k, k]
+    flops = sum(2.0 * M * n * k for n, k in prods)
+
+    def ours():
+        gpu_ext().gemm_bf16_grouped(dys, xs, outs, dims, False, False)
+
+    def ref():
+        for dy, x in zip(dys, xs):
+            _mm_f32(dy.t(), x)
+
+    t_o = t_r = float("inf")
+    for _ in range(3):
+        t_o = min(t_o, timeit(ours, args.reps))
+        t_r = min(t_r, timeit(ref, args.reps))
+    tiles = sum(((n + 255) // 256) * ((k + 255) // 256) for n, k in prods)
+    row = {"wgrad_group": args.wgrad_group, "tokens": M, "products": len(prods), "tiles": tiles,
+           "persistent": os.environ.get("RTDC_G8G_PERSIST", "1") != "0",
+           "ours_TF": round(flops / t_o / 1e12, 1), "hipblaslt_TF": round(flops / t_r / 1e12, 1),
+           "ours_us": round(t_o * 1e6, 1), "hipblaslt_us": round(t_r * 1e6, 1)}
+    print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":

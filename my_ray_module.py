@@ -84,6 +84,18 @@ def _set_rng_state(st, dev):
         torch.cuda.set_rng_state(st["torch_cuda"].cpu(), dev)
 
 
+def raise_if_poisoned(model) -> None:
+    """After a replayed (hipGraph) step: no host code runs inside a replay, so a P2P all-reduce
+    that timed out waiting for a late peer has only NaN-poisoned its bucket and set the error
+    word - the fused optimizer kernel read it and skipped the update on the device
+    (kernels/optim.hip comm_poisoned).  Fail the attempt here, before anything reports or
+    checkpoints that step."""
+    p2p = getattr(model, "p2p", None)
+    if p2p is not None and p2p.error():
+        raise RuntimeError("P2P all-reduce timed out waiting for a peer rank during a captured step "
+                           "(gradients poisoned with NaN, update skipped)")
+
+
 def train_func_per_worker(config: Dict):
     lr = config["lr"]
     epochs = config["epochs"]
@@ -174,11 +186,8 @@ def train_func_per_worker(config: Dict):
                     captured = CapturedStep(graph_step, warmup=0)
                 with phase("step"):
                     captured.replay()
-                if world > 1 and model.p2p.error():
-                    # no host code runs inside a replay: the poisoned step's update was skipped on
-                    # the device (kernels/optim.hip comm_poisoned); fail the attempt here
-                    raise RuntimeError("P2P all-reduce timed out waiting for a peer rank during a captured step "
-                                       "(gradients poisoned with NaN, update skipped)")
+                if world > 1:
+                    raise_if_poisoned(model)
                 continue
             # before a capture, run the eager steps on a side stream (as CapturedStep's warm-up
             # does): autograd's AccumulateGrad nodes must not belong to the default stream

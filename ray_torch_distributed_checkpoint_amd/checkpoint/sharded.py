@@ -127,34 +127,37 @@ class FlatShardedTensor:
                 f"local={self.local_numel()} elems)")
 
 
-def simulated_zero_ranges(numels, world: int, bucket_cap_mb: float = 32.0, first_bucket_mb: float = 2.0):
-    """The ZeRO-1 partition a `world`-rank job lays over parameters of these sizes (in flat
-    layout order = reverse registration order, as DistributedDataParallel(zero_stage=1) lays
-    them): 64-element-aligned segment offsets, the same bucket plan (parallel/ddp.py `_plan`,
-    fp32 caps), each bucket split into `world` shards of a 64-element-aligned size (the last
-    one may be shorter: the partition covers the flat space exactly).
+def simulated_zero_ranges(numels, world: int, bucket_cap_mb: float = 32.0, first_bucket_mb: float = 2.0,
+                          grad_comm_dtype: str = "fp32"):
+    """The ZeRO-1 partition a `world`-rank DistributedDataParallel(zero_stage=1) job lays over
+    parameters of these sizes (flat layout order = reverse registration order), reproduced
+    exactly: the same bucket plan (parallel/ddp.py `_plan`, caps in communicated bytes of
+    `grad_comm_dtype`), FlatParamSpace's 64-element segment alignment with each bucket's end
+    padded to a multiple of 64 x world (`align_after`), buckets spanning to the next bucket's
+    first segment (the last to the padded end), and ZeroLayout's equal per-rank shards.
     Returns (segment offsets, [rank] -> [(flat start, flat end)])."""
+    from ..optim.flat import ALIGN, ZeroLayout
     from ..parallel.ddp import DistributedDataParallel
 
+    esz = 2 if grad_comm_dtype == "bf16" else 4
+    numels = list(numels)
+    groups = DistributedDataParallel._plan(numels, int(first_bucket_mb * (1 << 20) / esz),
+                                           int(bucket_cap_mb * (1 << 20) / esz))
+    align = {g[-1]: 64 * world for g in groups}
     offs, off = [], 0
-    for n in numels:
+    for i, n in enumerate(numels):
         offs.append(off)
-        off += -(-n // 64) * 64
-    groups = DistributedDataParallel._plan(list(numels), int(first_bucket_mb * (1 << 20) / 4),
-                                           int(bucket_cap_mb * (1 << 20) / 4))
-    out = [[] for _ in range(world)]
-    for k, g in enumerate(groups):
-        a = offs[g[0]]
-        b = offs[groups[k + 1][0]] if k + 1 < len(groups) else off
-        sh = -(-(b - a) // (world * 64)) * 64
-        for r in range(world):
-            lo, hi = min(b, a + r * sh), min(b, a + (r + 1) * sh)
-            if lo < hi:
-                out[r].append((lo, hi))
-    return offs, out
+        off += (n + ALIGN - 1) // ALIGN * ALIGN
+        a = align.get(i)
+        if a:
+            off = (off + a - 1) // a * a
+    buckets = [(offs[g[0]], offs[groups[k + 1][0]] if k + 1 < len(groups) else off) for k, g in enumerate(groups)]
+    lay = ZeroLayout(buckets, 0, world)
+    return offs, [[(a, b) for a, b in lay.owned_by(r) if a < b] for r in range(world)]
 
 
-def simulated_zero_optimizer_state(model, opt, world: int, rank: int, bucket_cap_mb: float = 32.0) -> dict:
+def simulated_zero_optimizer_state(model, opt, world: int, rank: int, bucket_cap_mb: float = 32.0,
+                                   grad_comm_dtype: str = "fp32") -> dict:
     """The FQN-keyed optimizer state dict rank `rank` of a `world`-rank ZeRO-1 job would save
     (checkpoint/state_dict.py get_optimizer_state_dict under ZeRO-1): every state tensor a
     FlatShardedTensor over that rank's owned ranges, viewing this (replicated) optimizer's own
@@ -167,7 +170,8 @@ def simulated_zero_optimizer_state(model, opt, world: int, rank: int, bucket_cap
     m = model.module if hasattr(model, "module") else model
     named = [(n, p) for n, p in m.named_parameters() if p.requires_grad]
     order = list(reversed(named))
-    offs, ranges = simulated_zero_ranges([p.numel() for _, p in order], world, bucket_cap_mb)
+    offs, ranges = simulated_zero_ranges([p.numel() for _, p in order], world, bucket_cap_mb,
+                                         grad_comm_dtype=grad_comm_dtype)
     for (name, p), lo in zip(order, offs):
         hi = lo + p.numel()
         per_rank = [[(max(lo, a) - lo, min(hi, b) - lo) for a, b in rr if max(lo, a) < min(hi, b)] for rr in ranges]

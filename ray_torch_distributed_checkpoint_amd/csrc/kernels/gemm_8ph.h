@@ -702,6 +702,206 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs a) {
   }
 }
 
+// ---- plain fp32 tile store through a buffer descriptor (no bias / Cin / activation: the
+// grouped weight-gradient form).  Out-of-range rows / columns get BUF_OOB offsets instead of
+// per-lane branches, so no wait on the next tile's in-flight loads is inserted at a join;
+// re-zeroes the accumulators.
+template <int TMQ, int TNQ, int SA, int SB, int BH>
+__device__ __forceinline__ void tile_store_f32(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
+                                               int wa, int wb, int lane, float alpha) {
+  const long long tile_off = (long long)m0 * a.ldc * 4, rows_bytes = (long long)(a.M - m0) * a.ldc * 4;
+  const auto rC = make_rsrc(a.C, tile_off, rows_bytes);
+  const int rows_left = a.M - m0;
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i) {
+        const int r = 128 * qa + SA * wa + 16 * i + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j) {
+          const int n = n0 + BH * qb + SB * wb + 16 * j + 4 * (lane >> 4);
+          const uint32_t off = (r < rows_left && n < a.N) ? (uint32_t)(r * a.ldc + n) * 4u : BUF_OOB;
+          const f32x4 x = acc[qa][qb][i][j];
+          buf_store16(rC, off, u32x4{__float_as_uint(x[0] * alpha), __float_as_uint(x[1] * alpha),
+                                     __float_as_uint(x[2] * alpha), __float_as_uint(x[3] * alpha)});
+          acc[qa][qb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+}
+
+// ---- grouped persistent variant (gemm8gp_kernel): gemm8p_kernel's cross-tile pipeline over
+// the tiles of a GROUP of independent products with the same K (a layer's weight gradients:
+// K = tokens).  Global tile T indexes the products' tiles back to back (gg.start); the XCD
+// remap runs over the global list, so each XCD walks a contiguous run of tiles - consecutive
+// GROUP_M-ordered tiles of one product, sharing operand panels in that XCD's L2 - and the
+// stagers switch product where the run crosses a product boundary.  Against the one-block-per-
+// tile gemm8g_kernel this overlaps each tile's fp32 epilogue (256 KiB of stores) and the next
+// tile's prologue with MFMA work: with K = 2048 (Llama-3-8B, 32 K-tiles per tile) those were
+// ~25 % of a tile's time.
+__device__ __forceinline__ void group_tile(const GemmGroup& gg, int T, int total, int& p, int& tm, int& tn) {
+  int wgid = T;
+  if (total > 8) {
+    const int xcd = T & 7, q = total >> 3, r = total & 7;
+    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (T >> 3);
+  }
+  int pp = 0;
+#pragma unroll
+  for (int i = 1; i < G8_MAX_GROUP; ++i) pp += (i < gg.n && wgid >= gg.start[i]) ? 1 : 0;
+  p = __builtin_amdgcn_readfirstlane(pp);
+  const int local = wgid - gg.start[p];
+  const int tiles_m = (gg.g[p].M + BM - 1) / BM, tiles_n = (gg.g[p].N + 255) / 256;
+  constexpr int GROUP_M = 8;
+  const int group = local / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  tm = first_m + (local % (GROUP_M * tiles_n)) % gsize;
+  tn = (local % (GROUP_M * tiles_n)) / gsize;
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(512, 1) void gemm8gp_kernel(GemmGroup gg) {
+  constexpr int BN = 256, BH = BN / 2, WA = 2, WB = 8 / WA;
+  constexpr int SA = 128 / WA, SB = BH / WB, TMQ = SA / 16, TNQ = SB / 16;
+  constexpr int BHALF = BH * 128, BUF = 2 * HALF + 2 * BHALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 1024];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wave % WA, wb = wave / WA;
+
+  const int ntiles = gg.start[gg.n];
+  const int G = gridDim.x, b = blockIdx.x;
+  const int my_tiles = b < ntiles ? (ntiles - b + G - 1) / G : 0;
+  const int nt = gg.g[0].K / gemm::BK;  // same K for every product, >= 2 (host-checked)
+  const int total_kt = my_tiles * nt;
+  const int total_ev = 4 * total_kt;
+  if (total_kt == 0) return;
+
+  Stager<AK, 128, 8> sa0, sa1;
+  Stager<BKM, BH, 8> sb0, sb1;
+  auto stage_tile = [&](int s) {
+    int p, tm, tn;
+    group_tile(gg, b + s * G, ntiles, p, tm, tn);
+    const GemmArgs& a = gg.g[p];
+    sa0.init(a.A, a.lda, a.M, tm * BM, wave, lane);
+    sa1.init(a.A, a.lda, a.M, tm * BM + 128, wave, lane);
+    sb0.init(a.B, a.ldb, a.N, tn * BN, wave, lane);
+    sb1.init(a.B, a.ldb, a.N, tn * BN + BH, wave, lane);
+  };
+  auto issue = [&](int e, int j) {
+    if (e >= total_ev) return;
+    const int kind = e & 3;
+    const int k0 = j * gemm::BK;
+    char* base = smem + ((e >> 2) & 1) * BUF;
+    if (kind == 0) sa0.issue(k0, base, wave);
+    else if (kind == 3) sa1.issue(k0, base + HALF, wave);
+    else if (kind == 1) sb0.issue(k0, base + 2 * HALF, wave);
+    else sb1.issue(k0, base + 2 * HALF + BHALF, wave);
+  };
+
+  f32x4 acc[2][2][TMQ][TNQ];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile(0);
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  issue(4, 1);
+  wait_vm(6);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8 fa[TMQ][2], fbl[TNQ][2], fbh[TNQ][2];
+  for (int s = 0; s < my_tiles; ++s) {
+    int p, tm, tn;
+    group_tile(gg, b + s * G, ntiles, p, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const bool more = s + 1 < my_tiles;
+    for (int t = 0; t < nt; ++t) {
+      const int g = s * nt + t;
+      const char* buf = smem + (g & 1) * BUF;
+      const bool first = t == 0 && s > 0;
+      const bool last = t == nt - 1;
+#pragma unroll
+      for (int ph = 1; ph <= 4; ++ph) {
+        typename Frag<AK>::T ra[TMQ][2];
+        typename Frag<BKM>::T rb[TNQ][2];
+        if (ph == 1 || ph == 3) {
+          const char* ah = buf + (ph == 1 ? 0 : HALF);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < TMQ; ++i) ra[i][ks] = load_fragx<AK, 128>(ah, SA * wa + 16 * i, ks, lane);
+        }
+        if (ph == 1 || ph == 2) {
+          const char* bh = buf + 2 * HALF + (ph == 1 ? 0 : BHALF);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < TNQ; ++j) rb[j][ks] = load_fragx<BKM, 128>(bh, SB * wb + 16 * j, ks, lane);
+        }
+        if (ph == 4 && t == nt - 2 && more) stage_tile(s + 1);
+        if (ph < 4) issue(4 * g + 4 + ph, last ? 0 : t + 1);
+        else issue(4 * g + 8, t + 2 < nt ? t + 2 : t + 2 - nt);
+        if (ph == 1 || ph == 2) {
+          if (!first) {
+            const int e = 4 * g + 4 + ph, need = 4 * g + 1 + ph;
+            wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
+          }
+        } else if (ph == 4 && g + 1 < total_kt) {
+          const int e = 4 * g + 8;
+          const int need = last ? 4 * g + 7 : 4 * g + 5;
+          wait_vm(2 * (min(e + 1, total_ev) - 1 - need));
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (ph == 1 || ph == 3) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < TMQ; ++i) fa[i][ks] = fval(ra[i][ks]);
+        }
+        if (ph == 1 || ph == 2) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < TNQ; ++j) {
+              if (ph == 1) fbl[j][ks] = fval(rb[j][ks]);
+              else fbh[j][ks] = fval(rb[j][ks]);
+            }
+        }
+        const int qa = (ph - 1) >> 1, qb = (ph - 1) & 1;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+            for (int j = 0; j < TNQ; ++j) {
+              if (qb == 0)
+                acc[qa][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[j][ks], fa[i][ks], acc[qa][0][i][j], 0, 0, 0);
+              else
+                acc[qa][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbh[j][ks], fa[i][ks], acc[qa][1][i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    const GemmArgs& a = gg.g[p];
+    tile_store_f32<TMQ, TNQ, SA, SB, BH>(a, acc, m0, n0, wa, wb, lane, a.alpha);
+  }
+}
+
 // ---- 4-wave 256x256 kernel: a 128x128 output per wave (accumulators in AGPRs) ----------
 //
 // Why: the 8-wave kernel's per-wave 128x64 tile reads (128 + 64) x 64 x 2 B of LDS fragments per

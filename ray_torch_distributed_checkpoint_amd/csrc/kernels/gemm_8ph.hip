@@ -1,7 +1,11 @@
 // Launchers of the 8-wave / 4-wave 256-row GEMM kernels (kernels and schedules: gemm_8ph.h).
 #include "gemm_8ph.h"
 
+#include <cstdlib>
+
 using namespace rtdc;
+
+static int g_num_cus = 0;
 
 #ifndef RTDC_G4_ONLY  // (-DRTDC_G4_ONLY: a quick build of the 4-wave kernel alone for ISA inspection)
 // Launch the 8-phase kernel (batch 1, no causal modes).  a->splitk is honoured as set.
@@ -36,8 +40,6 @@ extern "C" int rtdc_gemm8_launch(const GemmArgs* args, int a_kmajor, int b_kmajo
 #undef G8
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
-
-static int g_num_cus = 0;
 
 // Persistent launch (gemm8p_kernel): grid = min(tiles, #CUs rounded down to a multiple of 8);
 // plain (non split-K) products with K >= 128 only.
@@ -96,15 +98,33 @@ extern "C" int rtdc_gemm8_grouped(const GemmArgs* args, int n, int a_kmajor, int
   }
   gg.start[n] = tiles;
   gg.n = n;
-  dim3 grid((unsigned)tiles, 1, 1), block(512);
-#define G8G(AK, BKM, T) hipLaunchKernelGGL((g8::gemm8g_kernel<AK, BKM, T>), grid, block, 0, st, gg)
-  if (out_fp32) {
-    if (!a_kmajor && !b_kmajor) G8G(false, false, float);
-    else return 1;
-  } else {
-    return 1;
+  if (!out_fp32 || a_kmajor || b_kmajor) return 1;
+  // persistent form (gemm8gp_kernel) when every product has the same K >= 128: one block per CU
+  // walks its tiles with the next tile's loads in flight under this tile's epilogue.
+  // RTDC_G8G_PERSIST=0 keeps one block per tile (A/B switch; read once).
+  static int persist = -1;
+  if (persist < 0) {
+    const char* e = std::getenv("RTDC_G8G_PERSIST");
+    persist = (e && e[0] == '0') ? 0 : 1;
   }
-#undef G8G
+  bool same_k = args[0].K >= 2 * gemm::BK;
+  for (int i = 1; i < n; ++i) same_k = same_k && args[i].K == args[0].K;
+  if (persist && same_k) {
+    if (g_num_cus == 0) {
+      int dev = 0, c = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+        c = 256;
+      g_num_cus = c;
+    }
+    long long gsz = (g_num_cus / 8) * 8;
+    if (gsz < 8) gsz = 8;
+    if (tiles < gsz) gsz = tiles;
+    hipLaunchKernelGGL((g8::gemm8gp_kernel<false, false>), dim3((unsigned)gsz), dim3(512), 0, st, gg);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
+  dim3 grid((unsigned)tiles, 1, 1), block(512);
+  hipLaunchKernelGGL((g8::gemm8g_kernel<false, false, float>), grid, block, 0, st, gg);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -790,14 +790,18 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
       const int tail_cols = tn % (256 / tm);
       if (tail_cols > 0 && tail_cols * tm <= 128) {
         const int n1 = (tn - tail_cols) * 256;
+        // both halves accumulate every element over the full K in one pass (no split-K slabs:
+        // ws = null makes pick_splitk return 1), so the result is bitwise the unsplit kernel's
         GemmArgs h = a;
         h.N = n1;
         h.tile_cfg = cfg;
+        h.ws = nullptr;
         int rc = rtdc_gemm_bf16(&h, 1, 1, 0, 1, stream, nullptr);
         if (rc) return rc;
         GemmArgs t = a;
         t.N = a.N - n1;
         t.tile_cfg = 11;
+        t.ws = nullptr;
         t.B = a.B + (long long)n1 * a.ldb;
         t.C = (bf16_t*)a.C + n1;
         if (a.bias) t.bias = (const char*)a.bias + (long long)n1 * (a.bias_type == 2 ? 4 : 2);

@@ -47,3 +47,25 @@ def test_bench_n_rank_path_on_gloo(tmp_path):
 def test_bench_n_rank_zero1_in_sync(tmp_path):
     out = _bench(2, "--zero", "1", "--sweep", "0", tmp=tmp_path)
     assert out["ranks_in_sync"] is True and out["comm"]["zero_stage"] == 1
+
+
+def test_bench_watchdog_prints_headline_when_a_later_phase_hangs(tmp_path):
+    """a hung post-headline phase (here an injected hang in the bucket
+    sweep, as a stuck collective on a first 8-GPU contact would be) must not hide the measured
+    throughput: rank 0's watchdog prints the JSON line with `phase_timed_out` and the run exits
+    non-zero instead of blocking until the driver's limit."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", RTDC_BENCH_CKPT_DIR=str(tmp_path), RTDC_BENCH_HANG_PHASE="sweep")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--cpu", "--model", "gpt2-tiny", "--batch", "2", "--seq-len", "64",
+           "--steps", "2", "--warmup", "1", "--overlap-steps", "1", "--sweep-budget-s", "4"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["phase_timed_out"] == "sweep"
+    assert out["value"] > 0 and out["n_gpus"] == 2 and out["ranks_in_sync"] is True
+    # the checkpoint phase finished before the hang and is reported
+    assert out["ckpt_scope"] == "model + optimizer + step"
+    assert len(out["ms_per_step_during_async_save_each"]) == 1

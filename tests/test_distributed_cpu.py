@@ -233,3 +233,39 @@ def _ddp_seq_check(rank, world):
 
 def test_ddp_collective_sequence_check():
     assert all(mp_util.run(_ddp_seq_check, 2))
+
+
+def _ddp_tail_split_mismatch(rank, world):
+    """Ranks that disagree on the deferred tail's piece size would issue different numbers of
+    collectives: the plan fingerprint must catch it before the first one."""
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.Linear(64, 64))
+    try:
+        DistributedDataParallel(m, defer_tail_to_optimizer=True, tail_piece_mb=0.01 if rank == 0 else 0.02)
+    except RuntimeError as e:
+        return "differs across ranks" in str(e)
+    return False
+
+
+def test_ddp_detects_mismatched_tail_split():
+    assert all(mp_util.run(_ddp_tail_split_mismatch, 2))
+
+
+def _ddp_rewrap_clears_skip_ptr(rank, world):
+    """A re-wrap of the same model (same flat space) without P2P must not keep the previous
+    communicator's error word as the optimizer's skip flag."""
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    m = torch.nn.Linear(16, 16)
+    a = DistributedDataParallel(m)
+    a.space.skip_ptr = 0xDEAD000  # what a P2P wrap leaves behind
+    a.detach()
+    b = DistributedDataParallel(m, p2p_max_kb=0.0)
+    return b.space is a.space and b.space.skip_ptr == 0
+
+
+def test_ddp_rewrap_without_p2p_clears_skip_ptr():
+    assert all(mp_util.run(_ddp_rewrap_clears_skip_ptr, 2))

@@ -342,3 +342,80 @@ def test_p2p_timeout_never_reaches_optimizer_or_checkpoint(tmp_path):
     sd = {"model": model.state_dict()}
     dcp.load(sd, os.path.join(tmp_path, "ck1"))
     assert all(bool(torch.isfinite(v).all()) for v in sd["model"].values() if torch.is_tensor(v))
+
+
+def _late_peer_graph_worker(rank, world, port, q):
+    """The captured 2-worker toy step (every bucket on P2P, 1 s bounded wait): one replay in
+    step, then rank 1 replays 3 s late.  Records what the post-replay check raised and whether
+    the parameters / momentum moved."""
+    try:
+        import time
+
+        import torch.distributed as dist
+
+        dev = _init(rank, world, port)
+        import my_ray_module
+        from ray_torch_distributed_checkpoint_amd import ops
+        from ray_torch_distributed_checkpoint_amd.models import NeuralNetwork
+        from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
+        from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+        from ray_torch_distributed_checkpoint_amd.utils.graphs import CapturedStep
+
+        torch.manual_seed(0)
+        ops.manual_seed(1234 + rank)
+        model = NeuralNetwork().to(dev)
+        net = DistributedDataParallel(model, p2p_max_kb=4096.0, p2p_timeout_s=1.0)
+        opt = FusedSGD(model.parameters(), lr=1e-2, momentum=0.9)
+        g = torch.Generator().manual_seed(100 + rank)
+        sx = torch.randn(16, 1, 28, 28, generator=g).to(dev)
+        sy = torch.randint(0, 10, (16,), generator=g).to(dev)
+
+        def step():
+            opt.zero_grad()
+            loss = ops.cross_entropy(net(sx), sy)
+            loss.backward()
+            opt.step()
+            return loss
+
+        side = torch.cuda.Stream()
+        for _ in range(2):  # eager warm-up on a side stream (lazy state), then capture
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                step()
+            torch.cuda.current_stream().wait_stream(side)
+        cs = CapturedStep(step, warmup=0)
+        cs.replay()
+        torch.cuda.synchronize()
+        my_ray_module.raise_if_poisoned(net)  # the in-step replay is healthy
+        before = {n: p.detach().clone() for n, p in model.named_parameters()}
+        mom = [b.clone() for b in opt._bufs.values()] if hasattr(opt, "_bufs") else []
+        dist.barrier()
+        if rank == 1:
+            time.sleep(3.0)
+        raised = None
+        cs.replay()
+        torch.cuda.synchronize()
+        try:
+            my_ray_module.raise_if_poisoned(net)
+        except RuntimeError as e:
+            raised = str(e)
+        finite = all(bool(torch.isfinite(p).all()) for p in model.parameters())
+        unchanged = all(torch.equal(p.detach(), before[n]) for n, p in model.named_parameters()) and \
+            all(torch.equal(a, b) for a, b in zip(mom, opt._bufs.values() if hasattr(opt, "_bufs") else []))
+        cs.close()
+        q.put((rank, "ok", (raised, finite, unchanged, net.p2p.error())))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def test_p2p_timeout_inside_graph_replay_raises_and_skips_update():
+    """a late peer during `captured.replay()` (no host code inside the
+    replay) - the post-replay check raises on every rank whose collective timed out, and no
+    parameter or momentum value moves (the fused SGD kernel read the error word and skipped)."""
+    out = _spawn(_late_peer_graph_worker, 2)
+    for r in range(2):
+        raised, finite, unchanged, err = out[r]
+        assert err == 1, f"rank {r}: expected a recorded timeout"
+        assert raised and "timed out" in raised, f"rank {r} did not raise: {raised}"
+        assert finite, f"rank {r} stepped NaN into its parameters"
+        assert unchanged, f"rank {r} applied the poisoned update"

@@ -42,6 +42,34 @@ def test_grouped_wgrad_matches_fp32_reference():
         assert torch.isfinite(out).all() and err < 1e-5, f"{tuple(out.shape)}: {err:.3e}"
 
 
+def test_grouped_wgrad_persistent_multi_round_ragged():
+    """The persistent grouped kernel (gemm8gp_kernel: one block per CU walking several tiles,
+    products switching mid-run, edge tiles of N = 1000 / K-in = 2736) against fp32: K = 2048
+    tokens like a Llama-3-8B layer, 332 tiles > one round of the chip."""
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+
+    torch.manual_seed(1)
+    M = 2048
+    dev = torch.device("cuda", 0)
+    dys, xs, outs, dims = [], [], [], []
+    for N, K in [(4096, 4096), (1000, 2736), (2048, 1024)]:
+        dys.append(torch.randn(M, N, device=dev).bfloat16())
+        xs.append(torch.randn(M, K, device=dev).bfloat16())
+        outs.append(torch.full((N, K), float("nan"), device=dev))
+        dims += [N, K, M, N, K, K]
+    gpu_ext().gemm_bf16_grouped(dys, xs, outs, dims, False, False)
+    torch.cuda.synchronize()
+    for dy, x, out in zip(dys, xs, outs):
+        ref = dy.float().t() @ x.float()
+        err = (out - ref).norm() / ref.norm()
+        assert torch.isfinite(out).all() and err < 1e-5, f"{tuple(out.shape)}: {err:.3e}"
+    # run-to-run bitwise (fixed per-tile K order)
+    again = [torch.empty_like(o) for o in outs]
+    gpu_ext().gemm_bf16_grouped(dys, xs, again, dims, False, False)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(outs, again))
+
+
 def _mlp_model(dev, n_layer=2):
     from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
 

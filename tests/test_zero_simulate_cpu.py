@@ -78,3 +78,29 @@ def test_simulated_checkpoint_is_refused_by_a_real_load(tmp_path):
     dcp.save({"model": get_state_dict(model, None)[0]}, path, simulate=(4, 1))
     with pytest.raises(ValueError, match="simulated"):
         dcp.load({"model": get_state_dict(model, None)[0]}, path)
+
+
+def _real_zero_layout(rank, world, dtype):
+    from ray_torch_distributed_checkpoint_amd.checkpoint.sharded import simulated_zero_ranges
+    from ray_torch_distributed_checkpoint_amd.models import GPT2, GPT2Config
+    from ray_torch_distributed_checkpoint_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    model = GPT2(GPT2Config(vocab_size=250, n_positions=64, n_embd=64, n_layer=3, n_head=2))
+    net = DistributedDataParallel(model, bucket_cap_mb=0.02, first_bucket_mb=0.005, zero_stage=1,
+                                  grad_comm_dtype=dtype)
+    sp = net.space
+    numels = [s.numel for s in sp.segments]
+    offs, ranges = simulated_zero_ranges(numels, world, 0.02, 0.005, grad_comm_dtype=dtype)
+    real = [(a, b) for a, b in sp.zero.owned if a < b]
+    return offs == [s.offset for s in sp.segments] and ranges[rank] == real and len(net.buckets) > 2
+
+
+def test_simulated_zero_ranges_are_the_real_ddp_layout():
+    """the simulated per-rank ZeRO-1 shard must be the one a real W-rank
+    DistributedDataParallel(zero_stage=1) owns - bucket-end padding to 64 x world, caps in
+    communicated bytes - so the single-process per-rank save/restore figures are pinned to it."""
+    from tests import mp_util
+
+    for dtype in ("fp32", "bf16"):
+        assert all(mp_util.run(_real_zero_layout, 4, dtype))
