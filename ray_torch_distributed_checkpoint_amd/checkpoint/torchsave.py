@@ -184,12 +184,19 @@ class SaveHandle:
                 from ..parallel import health
 
                 if not err and health.error():
+                    # a collective the snapshot depends on timed out (its NaN-poisoned state
+                    # was staged): the write is never committed
+                    self._poisoned = True
                     err = "a P2P gradient all-reduce timed out before the snapshot (state poisoned)"
                 if err:
                     self._error = str(err)
                 else:
                     self._result = time.perf_counter() - self.t0
             if self._error is not None:
+                if getattr(self, "_poisoned", False):
+                    from ..parallel.health import CommPoisonedError
+
+                    raise CommPoisonedError(f"refusing checkpoint commit: {self._error}")
                 raise IOError(f"checkpoint write failed: {self._error}")
             return self._result
 

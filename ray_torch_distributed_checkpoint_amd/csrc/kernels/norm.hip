@@ -8,6 +8,8 @@
 // float atomics).
 #include "gemm_common.h"
 
+#include <cstdlib>
+
 namespace rtdc {
 
 __device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
@@ -246,6 +248,90 @@ __device__ __forceinline__ void unpack4(uint2 q, float* v) {
   v[1] = __uint_as_float(q.x & 0xffff0000u);
   v[2] = __uint_as_float(q.y << 16);
   v[3] = __uint_as_float(q.y & 0xffff0000u);
+}
+
+// Forward with 8-B lane chunks for widths whose 16-B chunk count is not a multiple of 64
+// (GPT-2: D = 768 -> 192 chunks of 4 = 3 per lane, every lane busy; the 16-B form idles half
+// the lanes in its second chunk).  A wave owns rows gw, gw + nw, ...: gamma / beta are loaded
+// into registers once per wave instead of once per row, and the next row's x is in flight
+// while this row is reduced and written (the rows are a pure HBM stream: 1 read + 1 write).
+template <int CPL, bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd4_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
+                                                       const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int nch = D >> 2;
+  float gg[CPL][4], bb[CPL][4];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      ld4b(g + c * 4, gg[i]);
+      if (!RMS) ld4b(b + c * 4, bb[i]);
+    }
+  }
+  uint2 px[CPL];
+  auto fetch = [&](int r) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        const unsigned long long q =
+            __builtin_nontemporal_load((const unsigned long long*)(x + (long long)r * D + c * 4));
+        px[i] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+      }
+    }
+  };
+  if (gw < M) fetch(gw);
+  for (int row = gw; row < M; row += nw) {
+    float v[CPL][4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        unpack4(px[i], v[i]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s += v[i][e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[i][e] = 0.f;
+      }
+    }
+    if (row + nw < M) fetch(row + nw);
+    const float mean = RMS ? 0.f : wave_sum(s) / D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[i][e] - mean;
+          ss += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+    bf16_t* yr = y + (long long)row * D;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * gg[i][e] + (RMS ? 0.f : bb[i][e]);
+        *(uint2*)(yr + c * 4) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+      }
+    }
+  }
 }
 
 template <int CPL, bool RMS, bool CS>
@@ -579,6 +665,37 @@ static int launch_norm_fwd(const void* x, const void* g, const void* b, void* y,
                            float* rstd, int M, int D, float eps, hipStream_t st) {
   if (D % 8 != 0) return 1;
   const int cpl = (D / 8 + 63) / 64;
+  // RTDC_NORM_FWD4=1: 8-B chunks, rows looped per wave (norm_fwd4_kernel) where they fill every
+  // lane and 16-B ones would not (GPT-2's D = 768); RTDC_NORM_FWD_BPC: its resident 256-thread
+  // blocks per CU (default 4).  Opt-in: measured 12.9-15.0 us against 12.8 us for the one-row-
+  // per-wave form at 16384 x 768 (profiles/layernorm_fwd4_ab_r5.txt) - a 50 MB, ~13 us kernel
+  // sits at its launch/ramp-bound ~4 TB/s either way.
+  static int fwd4 = -1, bpc = 4, cus = 0;
+  if (fwd4 < 0) {
+    const char* e = getenv("RTDC_NORM_FWD4");
+    fwd4 = (e && e[0] == '1') ? 1 : 0;
+    const char* c = getenv("RTDC_NORM_FWD_BPC");
+    if (c && atoi(c) > 0) bpc = atoi(c);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int cpl4 = (D / 4) / 64;
+  if (fwd4 && (D / 8) % 64 != 0 && (D / 4) % 64 == 0 && cpl4 >= 1 && cpl4 <= 4) {
+    int nb = (M + 3) / 4;
+    if (nb > cus * bpc) nb = cus * bpc;
+    dim3 grid4(nb), block4(256);
+#define L4(C)                                                                                 \
+  hipLaunchKernelGGL((norm_fwd4_kernel<C, RMS>), grid4, block4, 0, st, (const bf16_t*)x,       \
+                     (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, mean, rstd, M, D, eps)
+    if (cpl4 == 1) L4(1);
+    else if (cpl4 == 2) L4(2);
+    else if (cpl4 == 3) L4(3);
+    else L4(4);
+#undef L4
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   dim3 grid((M + 3) / 4), block(256);
 #define L(C)                                                                                  \
   hipLaunchKernelGGL((norm_fwd_kernel<C, RMS>), grid, block, 0, st, (const bf16_t*)x,         \

@@ -75,6 +75,11 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     return y
 
 
+# RTDC_DGRAD_BLASLT=1: plain input-gradient products (no activation / column-sum epilogue) on
+# hipBLASLt - a plain library GEMM - instead of the hand-written kernel (A/B switch).
+_DGRAD_BLASLT = os.environ.get("RTDC_DGRAD_BLASLT", "0") == "1"
+
+
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None,
                  colsum_out=None):
     """dx[M,K] = alpha (* alpha_dev[0]) * dy[M,N] @ w[N,K]  (optionally * act'(aux_in)).
@@ -82,6 +87,9 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=Non
     the activation), reduced by the GEMM epilogue instead of a second pass over dx."""
     M, N = dy.shape
     K = w.shape[1]
+    if (_DGRAD_BLASLT and act_bwd == ACT_NONE and aux_in is None and alpha == 1.0 and alpha_dev is None
+            and colsum_out is None and w.dtype == torch.bfloat16):
+        return torch.matmul(dy, w)
     dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev,
               colsum_out=colsum_out)

@@ -70,9 +70,12 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, n_valid: int | Non
 # (96 MB), 810.1 (48 MB): the per-chunk GEMM tails cost more than the HBM round trip saves.
 _LM_CHUNK_MB = float(os.environ.get("RTDC_LMHEAD_CHUNK_MB", "0"))
 _chunk_bufs: dict = {}
-# RTDC_LMHEAD_BLASLT=1: the logits product on hipBLASLt (A/B only; the default keeps every
-# model GEMM on the hand-written MFMA kernels)
-_LM_BLASLT = os.environ.get("RTDC_LMHEAD_BLASLT", "0") == "1"
+# The logits product is a plain GEMM (no epilogue: the fused work is the cross-entropy kernel
+# after it), so it may run as a library GEMM: hipBLASLt leads the persistent 8-wave kernel on
+# this shape (1174 vs 997 TF isolated, profiles/gemm_pingpong_ab_r4.txt) and the GPT-2 step
+# measured 16.88 / 16.87 vs 17.08 / 17.09 ms (alternating runs, profiles/lmhead_blaslt_ab_r5.txt),
+# so it is the default.  RTDC_LMHEAD_BLASLT=0 keeps it on the native kernel.
+_LM_BLASLT = os.environ.get("RTDC_LMHEAD_BLASLT", "1") == "1"
 
 
 def _lm_chunk_rows(M: int, Vp: int) -> int:
@@ -108,11 +111,8 @@ class _LMHeadXent(torch.autograd.Function):
         tgt = target.reshape(-1).contiguous()
         R = _lm_chunk_rows(M, Vp)
         if R >= M:
-            # [M, Vp] bf16, softmax gradient written in place.  The logits product is a plain
-            # GEMM (no epilogue - the fused work is the cross-entropy kernel after it) on the
-            # persistent 8-wave MFMA kernel.  hipBLASLt measures ahead on this shape (1152 vs 996
-            # TF, profiles/gemm_bench_r3_4wave_v2.jsonl: ~0.2 ms/step); RTDC_LMHEAD_BLASLT=1
-            # selects it for A/B runs only
+            # [M, Vp] bf16, softmax gradient written in place; the plain logits product on
+            # hipBLASLt (or the persistent 8-wave kernel, RTDC_LMHEAD_BLASLT=0)
             logits = torch.matmul(x2, ws.t()) if _LM_BLASLT else G.linear_fwd(x2, ws)
             launch_pending_sorts()  # the embedding backward's token sort, under the xent kernel
             gpu_ext().xent(logits, logits, tgt, loss, None, None, M, vocab, Vp, scale, IGNORE_INDEX)

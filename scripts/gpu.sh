@@ -13,6 +13,7 @@
 #   attn       benchmarks/attn_bench.py  (ARGS)
 #   norm       benchmarks/norm_bench.py  (ARGS)
 #   ab         alternating bench runs of ab/_C_old.so vs the in-tree _C (MODEL, STEPS, ROUNDS)
+#   envab      alternating bench runs under ENVA vs ENVB ("K=V ..."; MODEL, STEPS, ROUNDS, TAG)
 #   multirank  2-rank gloo rehearsal of the multi-GPU bench path on one GPU
 #   roundend   tests + smoke + bench + multirank (what the driver runs)
 #   py         python3 $PY (a script path with args)
@@ -89,6 +90,15 @@ for task in ${TASKS//,/ }; do
         done
       done
       unset RTDC_EXT_SO ;;
+    envab)
+      # alternating bench runs under two environment settings (ENVA / ENVB: "K=V K2=V2"), ROUNDS each
+      for r in $(seq "$ROUNDS"); do
+        for arm in A B; do
+          if [ $arm = A ]; then envs=$ENVA; else envs=$ENVB; fi
+          TAILN=0 run "envab_${TAG}_${arm}_$r" 300 env $envs python bench.py --model "$MODEL" --steps "$STEPS" --warmup "$WARMUP" --no-ckpt --sweep 0 $ARGS || exit $?
+          echo "  $arm [$envs] $(grep -o '"ms_per_step": [0-9.]*' "gpurun_out/envab_${TAG}_${arm}_$r.log")"
+        done
+      done ;;
     multirank)
       # both ranks share cuda:0 over gloo (RCCL refuses two ranks on one device): DDP bucket
       # engine, BatchNorm buffer broadcast, sharded DCP save dedup + restore, bf16/ZeRO/P2P modes
