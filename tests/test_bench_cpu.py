@@ -69,3 +69,18 @@ def test_bench_watchdog_prints_headline_when_a_later_phase_hangs(tmp_path):
     # the checkpoint phase finished before the hang and is reported
     assert out["ckpt_scope"] == "model + optimizer + step"
     assert len(out["ms_per_step_during_async_save_each"]) == 1
+
+
+def test_ckpt_multiwriter_plumbing_on_gloo(tmp_path):
+    """benchmarks/ckpt_multiwriter.py (8 ranks writing their ZeRO-1 Llama shards at once on
+    one node) end to end on CPU: every rank's shard written, committed, restored cold and
+    verified bitwise."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", RTDC_BENCH_CKPT_DIR=str(tmp_path))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "benchmarks", "ckpt_multiwriter.py"), "--cpu", "--model", "llama3-tiny"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["world"] == 3 and out["verified_bitwise"] is True and out["restore_cold"] is True
+    assert len(out["per_rank_GB"]) == 3 and min(out["per_rank_GB"]) > 0
