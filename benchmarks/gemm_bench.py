@@ -96,6 +96,9 @@ def main():
         bias32 = bias.float()  # the models pass their fp32 master bias
         res_in = torch.randn(M, N, device="cuda").bfloat16()
         pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        wt = w.t().contiguous()
+        dxk = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+        cs_out = torch.empty(K, device="cuda", dtype=torch.float32)
         for lay, ours, ref in [
             ("fwd", lambda: G.linear_fwd(x, w), lambda: x @ w.t()),
             # fused epilogues as the GPT-2 blocks use them (reference: unfused torch ops)
@@ -106,6 +109,12 @@ def main():
             ("fwd_bias_res", lambda: G.linear_fwd(x, w, bias, residual=res_in),
              lambda: torch.addmm(bias, x, w.t()) + res_in),
             ("dgrad_gelu", lambda: G.linear_dgrad(dy, w, G.ACT_GELU_BWD, aux_in=x), lambda: dy @ w),
+            # as the MLP backward runs it: + the bias-gradient column sums in the epilogue
+            ("dgrad_gelu_cs", lambda: G.linear_dgrad(dy, w, G.ACT_GELU_BWD, aux_in=x, colsum_out=cs_out),
+             lambda: dy @ w),
+            # the same on a K-major image of w (persistent 8-wave kernel eligible)
+            ("dgrad_gelu_cs_kmaj", lambda: G.gemm_bf16(dy, wt, dxk, M, K, N, N, N, K, True, True, aux_in=x,
+                                                       act=G.ACT_GELU_BWD, colsum_out=cs_out), lambda: dy @ w),
             ("dgrad", lambda: G.linear_dgrad(dy, w), lambda: dy @ w),
             ("wgrad", lambda: G.linear_wgrad(dy, x), lambda: (dy.t() @ x)),
             # same product, hipBLASLt writing fp32 like our kernel does

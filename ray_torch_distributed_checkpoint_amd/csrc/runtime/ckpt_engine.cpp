@@ -341,6 +341,29 @@ static bool agent_of(const void* p, hsa_agent_t* a) {
   return true;
 }
 
+// The pinned slot must be directly accessible by the GPU whose SDMA engine copies into it
+// (hipHostMalloc normally grants every GPU; a process that sees several GPUs - one rank per
+// GPU under torchrun - must not depend on it): add `gpu` to the slot's access list if missing,
+// keeping every agent that already has access.
+static bool ensure_access(void* slot, hsa_agent_t gpu) {
+  hsa_amd_pointer_info_t info;
+  std::memset(&info, 0, sizeof(info));
+  info.size = sizeof(info);
+  uint32_t n = 0;
+  hsa_agent_t* agents = nullptr;
+  if (hsa_amd_pointer_info(slot, &info, std::malloc, &n, &agents) != HSA_STATUS_SUCCESS) return false;
+  bool has = false;
+  std::vector<hsa_agent_t> all;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (agents[i].handle == gpu.handle) has = true;
+    all.push_back(agents[i]);
+  }
+  std::free(agents);
+  if (has) return true;
+  all.push_back(gpu);
+  return hsa_amd_agents_allow_access((uint32_t)all.size(), all.data(), nullptr, slot) == HSA_STATUS_SUCCESS;
+}
+
 // host wait without spinning a core (the caller's event may use active synchronization)
 static hipError_t wait_event_sleepy(hipEvent_t ev) {
   while (true) {
@@ -669,7 +692,14 @@ class Engine {
     // SDMA needs the source's GPU agent (a caching-allocator block is an ordinary HSA
     // allocation); anything else falls back to the copy stream for this job
     hsa_agent_t gpu_agent{0};
-    const bool sdma = sdma_ && first_dev && agent_of(first_dev, &gpu_agent);
+    bool sdma = sdma_ && first_dev && agent_of(first_dev, &gpu_agent);
+    if (sdma && gpu_agent.handle != access_agent_) {
+      // once per GPU agent: every ring slot reachable by its SDMA engines, else this engine
+      // falls back to the copy stream for good
+      for (size_t i = 0; i < ring_.nslots() && sdma; ++i) sdma = ensure_access(ring_.ptr((int)i), gpu_agent);
+      if (sdma) access_agent_ = gpu_agent.handle;
+      else sdma_ = false;
+    }
     if (job->ready) {
       if (sdma) {
         hipError_t e = wait_event_sleepy(job->ready);
@@ -713,12 +743,18 @@ class Engine {
                 hsa_signal_store_screlease(sig_[s], 1);
                 hsa_status_t st = hsa_amd_memory_async_copy(ring_.ptr(s), host_agent_, r.src + o, gpu_agent, len, 0,
                                                             nullptr, sig_[s]);
-                if (st != HSA_STATUS_SUCCESS) {
-                  ring_.release(s);
-                  throw std::runtime_error("hsa_amd_memory_async_copy failed: status " + std::to_string((int)st));
+                if (st == HSA_STATUS_SUCCESS) {
+                  w.wait_signal = true;
+                } else {
+                  // the runtime refused the DMA: this piece and the rest of the job (and every
+                  // later one) go through the copy stream, ordered after the snapshot event
+                  sdma = false;
+                  sdma_ = false;
+                  hsa_signal_store_screlease(sig_[s], 0);
+                  if (stream_ && job->ready) hipStreamWaitEvent(stream_, job->ready, 0);
                 }
-                w.wait_signal = true;
-              } else {
+              }
+              if (!w.wait_signal) {
                 hipError_t e = hipMemcpyAsync(ring_.ptr(s), r.src + o, len, hipMemcpyDeviceToHost, stream_);
                 if (e != hipSuccess) {
                   ring_.release(s);
@@ -922,6 +958,7 @@ class Engine {
   std::map<int, std::shared_ptr<SaveJob>> jobs_;
   std::map<int, JobResult> results_;  // outcomes of waited (finished) jobs
   bool sdma_ = false;
+  uint64_t access_agent_ = 0;  // GPU agent the ring slots were made accessible to
   hsa_agent_t host_agent_{0};
   std::vector<hsa_signal_t> sig_;  // per ring slot: SDMA completion
   std::deque<int> result_order_;
