@@ -110,6 +110,12 @@ __device__ __forceinline__ typename Frag<KMAJOR>::T load_frag96(const char* tile
 // behind stores waits for them too (vmcnt counts both), which would serialise the store
 // stream behind each load.  One specialisation per
 // activation keeps the per-element code branch-free.
+// residual / activation-input pairs loaded ahead of their use in the bf16 epilogue (A/B builds:
+// -DRTDC_EPI_W=N)
+#ifndef RTDC_EPI_W
+#define RTDC_EPI_W 2
+#endif
+
 template <int ACT, int TMQ, int TNQ, int SA, int SB, int BH, bool ZERO>
 __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
                                                    int wa, int wb, int lane, float alpha) {
@@ -135,7 +141,7 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
   // fragment pairs in order P = (qa * TMQ + i) * TNQ + c: consecutive stores complete a row's
   // run of SB columns (a column-run-outer order left each 128-B line half written for half
   // the epilogue; with outputs that miss the caches, c_fc forward took 159 instead of 124 us)
-  constexpr int NP = 2 * TMQ * TNQ, W = 2;
+  constexpr int NP = 2 * TMQ * TNQ, W = RTDC_EPI_W < NP ? RTDC_EPI_W : NP;
   // (the lane part of the offset is one register; the per-pair parts are wave-uniform, so
   // nothing per pair is loop-invariant across the persistent kernel's tiles)
   const int lbase = rrow * a.ldc + nrun, rows_left = a.M - m0;
