@@ -148,6 +148,7 @@ def main():
     if not args.cpu:
         _ext.gpu_ext()  # native kernels are mandatory on the GPU path
     sync = (lambda: None) if args.cpu else torch.cuda.synchronize
+    _progress(rank, "process group up" if dist_on else "start")
     pre = preflight(world, rank, dev, args) if dist_on else None
     torch.manual_seed(1234)
     wl = build_workload(args, dev, rank)
@@ -184,12 +185,14 @@ def main():
             opt.zero_grad()
         return loss
 
+    _progress(rank, "workload built; warmup")
     for i in range(args.warmup):
         loss = step(i)
     sync()
     if dist_on:
         dist.barrier()
     sync()
+    _progress(rank, f"timing {args.steps} steps")
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
@@ -214,6 +217,7 @@ def main():
     # from here on the headline is measured: a later phase that hangs (a stuck collective on a
     # first contact with a new node, a filesystem that stops answering) must not hide it
     wd = PhaseWatchdog(out, rank)
+    _progress(rank, f"headline measured: {ms_per_step:.3f} ms/step")
 
     if not args.no_ckpt:
         # the throughput above is measured and must be reported even if the checkpoint phase
@@ -243,6 +247,13 @@ def main():
         wd.stop()
 
 
+def _progress(rank: int, msg: str) -> None:
+    """One stderr line per bench phase (stdout carries only the JSON line): a run that stops
+    progressing shows where.  Rank 0 always; every rank with RTDC_BENCH_VERBOSE=1."""
+    if rank == 0 or os.environ.get("RTDC_BENCH_VERBOSE", "0") == "1":
+        print(f"[bench] rank {rank} {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 class PhaseWatchdog:
     """Wall-clock budget per post-headline phase.  If a phase overruns, rank 0 prints the JSON
     line with everything measured so far plus `"phase_timed_out": <name>` and the process ends
@@ -254,6 +265,7 @@ class PhaseWatchdog:
         self.out, self.rank = out, rank
         self._lock = threading.Lock()
         self._cur = None  # (name, deadline, exit_code)
+        self._beat = time.monotonic()
         self._t = threading.Thread(target=self._run, daemon=True, name="bench-watchdog")
         self._t.start()
 
@@ -262,7 +274,12 @@ class PhaseWatchdog:
             time.sleep(0.5)
             with self._lock:
                 cur = self._cur
-            if cur is not None and time.monotonic() > cur[1]:
+            now = time.monotonic()
+            if cur is not None and now - self._beat > 60.0:
+                # heartbeat: a long phase is visibly alive (and a hung one names itself)
+                self._beat = now
+                _progress(self.rank, f"still in phase {cur[0]!r} ({cur[1] - now:.0f} s of budget left)")
+            if cur is not None and now > cur[1]:
                 name, _d, code = cur
                 if self.rank == 0 and code != 0:
                     o = dict(self.out)
@@ -279,6 +296,8 @@ class PhaseWatchdog:
         def cm():
             with self._lock:
                 self._cur = (name, time.monotonic() + budget_s, exit_code)
+                self._beat = time.monotonic()
+            _progress(self.rank, f"phase {name!r} (budget {budget_s:.0f} s)")
             try:
                 yield
             finally:
@@ -445,6 +464,7 @@ def comm_sweep(args, model, opt, net, cur, step, world, sync) -> list:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         out.append({"bucket_cap_mb": cap, "grad_comm_dtype": dtype, "buckets": len(w.buckets),
                     "ms_per_step": round(tt[0].item() * 1e3, 3), "ms_per_step_mean": round(tt[1].item() * 1e3, 3)})
+        _progress(dist.get_rank(), f"sweep cell {dtype}/{cap:g} MB: {out[-1]['ms_per_step']} ms/step")
         w.detach()
     cur["net"] = net
     return out
@@ -591,6 +611,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     arena_bytes = dcp.prepare_async(state(), simulate=sim)
     sync()
     t_prepare = time.perf_counter() - tp
+    _progress(rank, f"checkpoint: prepared ({arena_bytes / 1e9:.2f} GB arena); async save + {args.overlap_steps} steps")
     # ---- async save overlapped with training steps, as a training loop issues it: between two
     # steps with the device still busy (no host sync before the save - an idle device drops its
     # clocks and the next step pays the ramp).  Each step timed on the device (events between
@@ -616,6 +637,7 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     sync()
     each_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n_ov)] if cuda else host_each
     overlap_ms = sum(each_ms) / n_ov if cuda else (time.perf_counter() - t1) / n_ov * 1e3
+    _progress(rank, "checkpoint: overlap steps done; waiting for durability")
     local_write = h.wait()
     if dist.is_initialized():
         dist.barrier()
@@ -635,9 +657,11 @@ def checkpoint_phase(args, model, opt, net, step, world, rank, dev, dcp, sync):
     if dist.is_initialized():
         dist.barrier()
     sync()
+    _progress(rank, "checkpoint: blocking save")
     t2 = time.perf_counter()
     dcp.save(state(), path2, simulate=sim)
     t_sync = time.perf_counter() - t2
+    _progress(rank, "checkpoint: restores")
     # ---- restore into the live model + optimizer: first warm (shards still in the page cache
     # right after the write), then cold (every shard dropped from the page cache with
     # posix_fadvise(DONTNEED) after its fsync, so the bytes come from the device)

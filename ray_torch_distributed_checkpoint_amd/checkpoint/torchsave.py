@@ -150,7 +150,10 @@ def get_engine():
             if _engine is None:
                 nslots, slot_bytes, writers = engine_config()
                 dev = torch.cuda.current_device() if torch.cuda.is_available() else 0
-                _engine = _ext.ext().CkptEngine(nslots, slot_bytes, writers, dev)
+                # the copy stream comes from PyTorch's pool: a private stream would add a
+                # hardware queue to the process (see the Engine constructor)
+                stream = torch.cuda.Stream(device=dev).cuda_stream if torch.cuda.is_available() else 0
+                _engine = _ext.ext().CkptEngine(nslots, slot_bytes, writers, dev, stream=stream)
     return _engine
 
 

@@ -1033,8 +1033,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       "parallel pread of (offset, len) ranges into raw destination pointers");
 
   py::class_<Engine>(m, "CkptEngine")
-      .def(py::init<size_t, size_t, int, int, bool>(), py::arg("nslots"), py::arg("slot_bytes"), py::arg("nwriters"),
-           py::arg("device"), py::arg("direct_io") = true)
+      .def(py::init<size_t, size_t, int, int, bool, uintptr_t>(), py::arg("nslots"), py::arg("slot_bytes"),
+           py::arg("nwriters"), py::arg("device"), py::arg("direct_io") = true, py::arg("stream") = 0)
       .def(
           "submit",
           [](Engine& e, const py::list& files, uintptr_t ready_event) {

@@ -452,11 +452,21 @@ static double now_s() {
 
 class Engine {
  public:
-  Engine(size_t nslots, size_t slot_bytes, int nwriters, int device, bool direct_io = true)
+  // `stream`: the copy stream (restore H2D, the hipMemcpy D2H fallback) - a stream the caller
+  // already owns (PyTorch's pool).  0 creates a private one.  Every stream a process creates can
+  // cost a hardware queue: with two ranks time-sharing one GPU, ONE extra idle stream per process
+  // made the training step 10-15x slower (hardware-queue oversubscription; measured with a bare
+  // hipStreamCreate, scripts/diag_postckpt.py, profiles/ckpt_engine_stream_r5.txt).
+  Engine(size_t nslots, size_t slot_bytes, int nwriters, int device, bool direct_io = true, uintptr_t stream = 0)
       : ring_(nslots, slot_bytes), device_(device), direct_io_(direct_io) {
     if (g_have_gpu()) {
       hipSetDevice(device_);
-      hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
+      if (stream) {
+        stream_ = reinterpret_cast<hipStream_t>(stream);
+      } else {
+        hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
+        own_stream_ = true;
+      }
       const char* m = std::getenv("RTDC_CKPT_D2H");
       const bool want_sdma = !(m && std::string(m) == "hip");
       // HIP has initialised the runtime already; hsa_init only takes a reference on it
@@ -486,7 +496,7 @@ class Engine {
     wcv_.notify_all();
     jcv_.notify_all();
     for (auto& t : writers_) t.join();
-    if (stream_) hipStreamDestroy(stream_);
+    if (stream_ && own_stream_) hipStreamDestroy(stream_);
     for (auto& sg : sig_) hsa_signal_destroy(sg);
   }
 
@@ -949,6 +959,7 @@ class Engine {
   int device_;
   bool direct_io_;
   hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
   std::vector<std::thread> writers_;
   std::thread enqueuer_;
   std::mutex qmu_, wmu_, jmu_;
