@@ -15,8 +15,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
-    dist.init_process_group("gloo")
-    rank = dist.get_rank()
+    nodist = os.environ.get("DIAG_NODIST") == "1"  # independent processes on the same GPU, no gloo
+    if nodist:
+        rank = int(os.environ["RANK"])
+        dist.barrier = lambda: None
+        dist.destroy_process_group = lambda: None
+    else:
+        dist.init_process_group("gloo")
+        rank = dist.get_rank()
     torch.cuda.set_device(0)
     from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
     from ray_torch_distributed_checkpoint_amd.checkpoint.state_dict import get_state_dict, set_state_dict
@@ -27,12 +33,12 @@ def main():
     torch.manual_seed(0)
     model = GPT2(GPT2Config.named("gpt2-small")).cuda()
     opt = FusedAdamW(model.parameters(), lr=1e-4)
-    cur = {"net": DistributedDataParallel(model, bucket_cap_mb=32, defer_tail_to_optimizer=True)}
+    cur = {"net": model if nodist else DistributedDataParallel(model, bucket_cap_mb=32, defer_tail_to_optimizer=True)}
     d = torch.randint(0, 50257, (4, 1025), device="cuda")
     x, y = d[:, :-1].contiguous(), d[:, 1:].contiguous()
     seed = torch.ones((), device="cuda")
 
-    def steps(tag, n=4):
+    def steps(tag, n=int(os.environ.get("DIAG_N", "4"))):
         torch.cuda.synchronize()
         dist.barrier()
         t = time.perf_counter()
@@ -42,8 +48,8 @@ def main():
             opt.zero_grad()
         torch.cuda.synchronize()
         dist.barrier()
-        if rank == 0:
-            print(f"{tag:28s} {(time.perf_counter() - t) / n * 1e3:9.1f} ms/step", flush=True)
+        if rank == 0 or nodist:
+            print(f"r{rank} {tag:28s} {(time.perf_counter() - t) / n * 1e3:9.1f} ms/step", flush=True)
 
     def state():
         msd, osd = get_state_dict(model, opt)
@@ -68,7 +74,20 @@ def main():
         elif mode == "engine_small":
             from ray_torch_distributed_checkpoint_amd.ops import _ext
 
-            keep = _ext.ext().CkptEngine(1, 4096, 1, 0)
+            keep = _ext.ext().CkptEngine(1, 4096, 1, 0, stream=torch.cuda.Stream().cuda_stream)
+        elif mode in ("ev_block", "ev_plain"):
+            import ctypes
+
+            hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+            evs = [ctypes.c_void_p() for _ in range(8)]
+            flags = 0x3 if mode == "ev_block" else 0x2  # hipEventBlockingSync | hipEventDisableTiming
+            rcs = [hip.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(flags)) for e in evs]
+            if rank == 0:
+                print(f"{mode} rc={rcs}", flush=True)
+        elif mode == "engine_nowriter":
+            from ray_torch_distributed_checkpoint_amd.ops import _ext
+
+            keep = _ext.ext().CkptEngine(1, 4096, 0, 0, stream=torch.cuda.Stream().cuda_stream)
         elif mode in ("rawstream", "rawstream0", "hostmalloc"):
             import ctypes
 

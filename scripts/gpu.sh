@@ -103,10 +103,14 @@ for task in ${TASKS//,/ }; do
       # both ranks share cuda:0 over gloo (RCCL refuses two ranks on one device): DDP bucket
       # engine, BatchNorm buffer broadcast, sharded DCP save dedup + restore, bf16/ZeRO/P2P modes
       mr() { local name=$1 port=$2; shift 2
-        TAILN=1 run "mr_$name" 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        TAILN=1 run "mr_$name" 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port "$port" bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo "$@"; }
-      mr gpt2 29533 --batch 4 || exit $?
-      mr resnet 29534 --model resnet18 --batch 32 || exit $?
+      # two sweep cells: gloo's host-staged all-reduce of CUDA tensors with two processes on one
+      # device runs 10-40x slower once the checkpoint engine exists (profiles/ckpt_engine_stream_r5.txt)
+      export RTDC_SWEEP_CELLS=fp32:32,bf16:64
+      mr gpt2 29533 --batch 4 --sweep-budget-s 420 || exit $?
+      mr resnet 29534 --model resnet18 --batch 32 --sweep-budget-s 420 || exit $?
+      unset RTDC_SWEEP_CELLS
       mr gpt2_zero 29535 --batch 4 --zero 1 --grad-comm-dtype bf16 || exit $?
       mr gpt2_p2p 29536 --batch 4 --p2p-kb 4096 --no-ckpt || exit $? ;;
     roundend)
