@@ -359,6 +359,144 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(Args a) {
   if (g == 0) a.lse[(long long)bh * a.T + myq] = m + log2f(l);
 }
 
+// Forward, software-pipelined across key tiles inside each wave: the S = K.Q MFMAs of tile kb+1
+// are issued before the softmax of tile kb, so one wave's matrix work runs under its own
+// exp/max/pack VALU instead of waiting for a co-resident wave to fill the gap (the serial
+// S -> max -> exp -> P.V chain of fwd_kernel).  K therefore streams one tile further ahead than
+// V: a 3-slot K ring and a 2-slot V ring (40 KiB, the same 4 blocks per CU as fwd_kernel's
+// 2+2 slots would allow at this register count).  Step kb issues K(kb+2) and V(kb+1) - into the
+// slots of K(kb-1) (read in step kb-2) and V(kb-1) (read in step kb-1) - and retires both
+// before its closing barrier, so each DMA has one step to land, as in fwd_kernel.  Same math in
+// the same order as fwd_kernel: bitwise equal output.
+template <int DH>
+__global__ __launch_bounds__(256, 2) void fwd3_kernel(Args a) {
+  constexpr int KS = DH / 32, DT = DH / 16, DB = DT < 4 ? DT : 4, TILE = 64 * DH * 2;
+  __shared__ __attribute__((aligned(16))) char smem[5 * TILE];  // K[3], V[2]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = a.T / BQ;
+  int bx, bh;
+  grid_pos(a, bx, bh);
+  const int qb = nqb - 1 - bx;
+  const int b = bh / a.H, h = bh % a.H;
+  const int grp = a.H / a.Hkv, kvh = h / grp;
+  const int C = a.H * DH, W = C + 2 * a.Hkv * DH;
+  const bf16_t* base = a.qkv + (long long)b * a.T * W;
+  const int qcol = h * DH, kcol = C + kvh * DH, vcol = C + a.Hkv * DH + kvh * DH;
+  const int q0w = qb * BQ + wave * 16;
+  const int myq = q0w + (lane & 15);
+  const float c = a.scale * LOG2E;
+  uint32_t troff[DH / 16];
+  tr_lane_offsets<DH>(troff, lane);
+  const int nkb = qb + 1;
+
+#define KT(s) (smem + (s) * TILE)
+#define VT(s) (smem + (3 + (s)) * TILE)
+  stage<DH>(base, W, 0, kcol, KT(0), wave, lane);
+  stage<DH>(base, W, 0, vcol, VT(0), wave, lane);
+  if (nkb > 1) stage<DH>(base, W, BKV, kcol, KT(1), wave, lane);
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = gload8(base + (long long)myq * W + qcol + ks * 32 + g * 8);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) settle(qf[ks]);  // (retires the DMA above with it)
+  step_barrier();
+
+  auto scores = [&](const char* kt, f32x4 (&s)[4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[t] = mfma(frag_rows<DH>(kt, 16 * t, ks, lane), qf[ks], s[t]);
+    }
+  };
+  f32x4 o[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 lacc = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
+  float m = -INFINITY;
+  f32x4 s[4];
+  scores(KT(0), s);
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 2 < nkb) stage<DH>(base, W, (kb + 2) * BKV, kcol, KT((kb + 2) % 3), wave, lane);
+    if (kb + 1 < nkb) stage<DH>(base, W, (kb + 1) * BKV, vcol, VT((kb + 1) & 1), wave, lane);
+    // next tile's scores first: independent of this tile's softmax
+    f32x4 sn[4];
+    if (kb + 1 < nkb) scores(KT((kb + 1) % 3), sn);
+    const uint32_t vbase = lds_addr(VT(kb & 1));
+    float mx = -INFINITY;
+    const bool diag = (kb == qb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = s[t][r];
+        if (diag) {
+          const int key = kb * BKV + 16 * t + 4 * g + r;
+          if (key > myq) v = -INFINITY;
+        }
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = max_rows4(mx);
+    if (__any(mx * c > m + 8.f)) {
+      const float mn = fmaxf(m, mx * c);
+      const float alpha = fexp2(m - mn);
+      m = mn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lacc[r] *= alpha;
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[d][r] *= alpha;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[t][r] = fexp2(fmaf(s[t][r], c, -m));
+    const bf16x8 p0 = pack_pair(s[0], s[1]), p1 = pack_pair(s[2], s[3]);
+    lacc = mfma(ones, p0, lacc);
+    lacc = mfma(ones, p1, lacc);
+#pragma unroll
+    for (int d0 = 0; d0 < DT; d0 += DB) {
+      TrPair vq[DB][2];
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        const uint32_t la = vbase + troff[d0 + d];
+        vq[d][0] = frag_cols_at<DH, 0>(la);
+        vq[d][1] = frag_cols_at<DH, 32>(la);
+      }
+      lgkm_wait0();
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        o[d0 + d] = mfma(tr_use(vq[d][0]), p0, o[d0 + d]);
+        o[d0 + d] = mfma(tr_use(vq[d][1]), p1, o[d0 + d]);
+      }
+    }
+    // step kb+1 reads K(kb+2) and V(kb+1), both issued at the top of this step
+    if (kb + 1 < nkb && !(a.diag & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    step_barrier();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s[t] = sn[t];
+  }
+#undef KT
+#undef VT
+  const float l = lacc[0];
+  const float inv = 1.f / l;
+  bf16_t* orow = a.out + ((long long)b * a.T + myq) * C + h * DH;
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    const uint2 v = make_uint2(pack_bf2(o[d][0] * inv, o[d][1] * inv), pack_bf2(o[d][2] * inv, o[d][3] * inv));
+    *(uint2*)(orow + 16 * d + 4 * g) = v;
+  }
+  if (g == 0) a.lse[(long long)bh * a.T + myq] = m + log2f(l);
+}
+
 // Forward, 32 query rows per wave (block = 128 rows): every K fragment read from LDS feeds
 // two S MFMAs and every V fragment two P.V MFMAs, halving LDS bytes per FLOP.  Same
 // accumulator-as-operand layout and the same DMA ring as fwd_kernel.
@@ -1275,10 +1413,14 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
   // measured (benchmarks/attn_bench.py, before the DMA ring): 32 rows/wave wins at Dh = 128
   // (Llama: 101 vs 108 us), 16 rows/wave at Dh = 64 (GPT-2: 100 vs 109 us); RTDC_FA_FWD=1|2
   // forces one
-  static const int forced = getenv("RTDC_FA_FWD") ? atoi(getenv("RTDC_FA_FWD")) : 0;
+  const char* fwd_env = getenv("RTDC_FA_FWD");  // (read per call: tests A/B it in one process)
+  const int forced = fwd_env ? atoi(fwd_env) : 0;
   const int variant = forced ? forced : (Dh == 128 ? 2 : 1);
   const int ns = fa_ns(Dh);
-  if (variant == 2 && T % 128 == 0) {  // 32 rows per wave
+  if (variant == 3 && Dh == 64) {  // software-pipelined 16 rows per wave
+    dim3 grid(T / 64, B * H);
+    hipLaunchKernelGGL((fa::fwd3_kernel<64>), grid, dim3(256), 0, st, a);
+  } else if (variant == 2 && T % 128 == 0) {  // 32 rows per wave
     dim3 grid(T / 128, B * H);
     if (Dh == 64) FA_DISPATCH(fa::fwd2_kernel, 64, ns, grid, a);
     else FA_DISPATCH(fa::fwd2_kernel, 128, ns, grid, a);

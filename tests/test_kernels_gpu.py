@@ -1101,3 +1101,31 @@ def test_gemm_tail_split_forward(monkeypatch, M, N, K, bias):
         # a 4-tile tail over K = 8192 is a split-K candidate on its own: the tail launch must
         # still accumulate in one pass, i.e. bitwise the single launch
         assert torch.equal(out["1"], out["0"])
+
+
+@pytest.mark.parametrize("H,Hkv,T", [(4, 4, 64), (4, 4, 256), (4, 2, 512), (2, 2, 1024)])
+def test_flash_forward_pipelined_equals_plain(monkeypatch, H, Hkv, T):
+    """Forward with the next key tile's scores issued before this tile's softmax (fwd3_kernel,
+    RTDC_FA_FWD=3: 3-slot K ring, 2-slot V ring) performs the same operations in the same
+    order as the 16-rows-per-wave kernel: bitwise equal output and row log-sum-exp, including
+    one-tile (T = 64) and two-tile heads."""
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+    from ray_torch_distributed_checkpoint_amd.ops.attention import causal_attention_ref
+
+    torch.manual_seed(T + H)
+    Dh, Bn = 64, 2
+    W = (H + 2 * Hkv) * Dh
+    qkv = _bf(Bn, T, W)
+    ext = gpu_ext()
+    res = {}
+    for v in ("1", "3"):
+        monkeypatch.setenv("RTDC_FA_FWD", v)
+        o = torch.empty((Bn, T, H * Dh), dtype=torch.bfloat16, device="cuda")
+        lse = torch.empty((Bn * H, T), dtype=torch.float32, device="cuda")
+        ext.flash_fwd(qkv, o, lse, Bn, T, H, Hkv, Dh, Dh ** -0.5)
+        torch.cuda.synchronize()
+        res[v] = (o, lse)
+    assert torch.equal(res["1"][0], res["3"][0])
+    assert torch.equal(res["1"][1], res["3"][1])
+    ref = causal_attention_ref(qkv.float(), Bn, T, H, Hkv, Dh)
+    _close(res["3"][0].float(), ref.view_as(res["3"][0]).float(), 3e-2)
