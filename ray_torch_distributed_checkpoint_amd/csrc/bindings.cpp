@@ -1019,10 +1019,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_status", &grad_status, "per-parameter gradient placement: 0 none, 1 flat slice, 2 elsewhere");
   m.def("have_gpu", &rtdc_ckpt::g_have_gpu);
   m.def("plan_layout", &plan_layout, "file layout of a list of (raw, records) archives");
-  m.def("crc32", [](py::bytes b) {
-    std::string s = b;
-    return (uint32_t)crc32(0L, (const Bytef*)s.data(), (uInt)s.size());
-  });
+  // the checkpoint writers' CRC-32 (PCLMUL folding, zlib-compatible; runtime/crc32_fast.h)
+  m.def(
+      "crc32",
+      [](py::bytes b, uint32_t init) {
+        std::string s = b;
+        return rtdc::crc::crc32_fast(init, s.data(), s.size());
+      },
+      py::arg("data"), py::arg("init") = 0u);
   m.def(
       "read_ranges",
       [](const std::string& path, std::vector<uint64_t> offs, std::vector<uint64_t> lens, std::vector<uintptr_t> dsts,

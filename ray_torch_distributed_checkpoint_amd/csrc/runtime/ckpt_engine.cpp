@@ -23,6 +23,8 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <zlib.h>
+
+#include "runtime/crc32_fast.h"
 #include <fcntl.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
@@ -845,7 +847,7 @@ class Engine {
             src = ring_.ptr(w.slot);
           }
           uint32_t c = 0;
-          if (f.crc_on) c = (uint32_t)crc32(0L, (const Bytef*)src, (uInt)w.len);
+          if (f.crc_on) c = rtdc::crc::crc32_fast(0u, src, w.len);  // PCLMUL folding: ~5 GB/s per writer from DRAM
           write_piece(f, src, w.len, w.off);
           if (w.slot >= 0) ring_.release(w.slot);
           w.slot = -1;
@@ -910,7 +912,7 @@ class Engine {
           }
           r.crc = c;
         } else {
-          r.crc = f.crc_on ? (uint32_t)crc32(0L, (const Bytef*)r.inline_data.data(), (uInt)r.inline_data.size()) : 0;
+          r.crc = f.crc_on ? rtdc::crc::crc32_fast(0u, r.inline_data.data(), r.inline_data.size()) : 0;
         }
       }
       for (auto& r : a.recs) {

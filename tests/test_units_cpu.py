@@ -190,3 +190,23 @@ def test_wgrad_round_split_rows():
     assert G._round_split_rows(128256, 4096, 16384, "fake") == 496 * 256
     # the tail must stay a split-K candidate (< 200 tiles)
     assert G._round_split_rows(16 * 256, 257 * 256, 16384, "fake") == 0
+
+
+def test_crc32_fast_matches_zlib():
+    """The checkpoint writers' CRC-32 (carry-less-multiply folding + table tail,
+    csrc/runtime/crc32_fast.h) equals zlib.crc32 for every length class (< 64 B table path,
+    folds of 64 / 16 B with tails), unaligned starts and chained initial values."""
+    import random
+    import zlib
+
+    from ray_torch_distributed_checkpoint_amd.ops import _ext
+
+    ext = _ext.ext()
+    rng = random.Random(7)
+    buf = bytes(rng.getrandbits(8) for _ in range(300_000))
+    lens = list(range(0, 200)) + [rng.randrange(200, 250_000) for _ in range(200)] + [250_000]
+    for n in lens:
+        off = rng.randrange(0, 64)
+        init = 0 if n % 3 == 0 else rng.getrandbits(32)
+        data = buf[off:off + n]
+        assert ext.crc32(data, init) == zlib.crc32(data, init), (n, off, init)
