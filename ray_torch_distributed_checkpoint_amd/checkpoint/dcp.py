@@ -517,6 +517,34 @@ def _zip_data_record(path: str, base: int, length: int, f=None) -> tuple[int, in
     raise IOError(f"{path}@{base}: no tensor data record")
 
 
+def _data_records(items, threads: int = 8) -> list[tuple[int, int]]:
+    """(data offset, size) of the tensor record of each (path, base, length) zip slice, in
+    order: one native call per file (csrc/runtime/ckpt_engine.cpp zip_data_records - parallel
+    preads, no per-item Python I/O).  RTDC_ZIP_PARSE=py keeps the Python parser (A/B)."""
+    out: list = [None] * len(items)
+    if os.environ.get("RTDC_ZIP_PARSE", "native") == "py":
+        handles: dict = {}
+        try:
+            for i, (path, base, length) in enumerate(items):
+                fh = handles.get(path)
+                if fh is None:
+                    fh = handles[path] = open(path, "rb", buffering=0)
+                out[i] = _zip_data_record(path, base, length, fh)
+        finally:
+            for fh in handles.values():
+                fh.close()
+        return out
+    by_path: dict[str, list[int]] = {}
+    for i, (path, _b, _l) in enumerate(items):
+        by_path.setdefault(path, []).append(i)
+    ext = _ext.ext()
+    for path, ids in by_path.items():
+        res = ext.zip_data_records(path, [items[i][1] for i in ids], [items[i][2] for i in ids], threads)
+        for i, r in zip(ids, res):
+            out[i] = (int(r[0]), int(r[1]))
+    return out
+
+
 def _pinned(n: int) -> torch.Tensor:
     t = torch.empty(n, dtype=torch.uint8)
     if torch.cuda.is_available():
@@ -572,25 +600,23 @@ def load(state_dict: dict, checkpoint_id: str, process_group=None, *, broadcast:
     my = [k for k in tensor_fqns if reader[k] == rank]
     # ---- read my items: (dest tensor, chunk offsets, chunk sizes, file, data offset, nbytes)
     reqs = []
-    handles: dict = {}
+    need = []
     for k in my:
         dest = flat[k]
         mdt = md.state_dict_metadata[k]
         if tuple(mdt.size) != tuple(dest.shape):
             raise ValueError(f"{k}: checkpoint shape {tuple(mdt.size)} != destination {tuple(dest.shape)}")
         for idx, info in chunks_of[k]:
-            path = os.path.join(checkpoint_id, info.relative_path)
-            fh = handles.get(path)
-            if fh is None:
-                fh = handles[path] = open(path, "rb", buffering=0)
-            off, n = _zip_data_record(path, info.offset, info.length, fh)
-            csizes = None
-            for c in mdt.chunks:
-                if tuple(c.offsets) == tuple(idx.offset):
-                    csizes = tuple(c.sizes)
-            reqs.append((dest, tuple(idx.offset), csizes or tuple(dest.shape), path, off, n, mdt.properties.dtype))
-    for fh in handles.values():
-        fh.close()
+            need.append((k, idx, info, os.path.join(checkpoint_id, info.relative_path)))
+    recs = _data_records([(path, info.offset, info.length) for _k, _i, info, path in need], threads)
+    for (k, idx, info, path), (off, n) in zip(need, recs):
+        dest = flat[k]
+        mdt = md.state_dict_metadata[k]
+        csizes = None
+        for c in mdt.chunks:
+            if tuple(c.offsets) == tuple(idx.offset):
+                csizes = tuple(c.sizes)
+        reqs.append((dest, tuple(idx.offset), csizes or tuple(dest.shape), path, off, n, mdt.properties.dtype))
     # device destinations whose region is one contiguous run of the same dtype stream straight
     # from the file: native pread -> pinned ring -> H2D on the engine's copy stream, pipelined
     # (torchsave.get_engine().read_to_device); anything else (host destinations, resharded
@@ -687,47 +713,43 @@ def _load_sharded(flat, fqns, md, chunks_of, checkpoint_id, ext, threads) -> Non
 
     dev_reads: dict[str, tuple[list, list, list]] = {}
     host_reads: dict[str, tuple[list, list, list]] = {}
-    handles: dict = {}
-    try:
-        for k in fqns:
-            v = flat[k]
-            mdt = md.state_dict_metadata[k]
-            if tuple(mdt.size) != tuple(v.shape):
-                raise ValueError(f"{k}: checkpoint shape {tuple(mdt.size)} != destination {tuple(v.shape)}")
-            if mdt.properties.dtype != v.dtype:
-                raise ValueError(f"{k}: checkpoint dtype {mdt.properties.dtype} != destination {v.dtype}")
-            esz = torch.empty((), dtype=v.dtype).element_size()
-            sizes_of = {tuple(c.offsets): tuple(c.sizes) for c in mdt.chunks}
-            covered = 0
-            for idx, info in chunks_of[k]:
-                fr = chunk_flat_range(idx.offset, sizes_of[tuple(idx.offset)], v.shape)
-                if fr is None:
-                    raise ValueError(f"{k}: chunk at {tuple(idx.offset)} is not contiguous in row-major order; a "
-                                     f"flat-sharded destination cannot read it")
-                cs, cn = fr
-                rec = None
-                for s0, t in v.local:
-                    lo, hi = max(s0, cs), min(s0 + t.numel(), cs + cn)
-                    if lo >= hi:
-                        continue
-                    path = os.path.join(checkpoint_id, info.relative_path)
-                    if rec is None:
-                        fh = handles.get(path)
-                        if fh is None:
-                            fh = handles[path] = open(path, "rb", buffering=0)
-                        rec = _zip_data_record(path, info.offset, info.length, fh)
-                    dst = t[lo - s0:hi - s0]
-                    group = dev_reads if (dst.is_cuda and torch.cuda.is_available()) else host_reads
-                    o, l_, d = group.setdefault(path, ([], [], []))
-                    o.append(rec[0] + (lo - cs) * esz)
-                    l_.append((hi - lo) * esz)
-                    d.append(dst.data_ptr())
-                    covered += hi - lo
-            if covered != v.local_numel():
-                raise ValueError(f"{k}: checkpoint chunks cover {covered} of this rank's {v.local_numel()} elements")
-    finally:
-        for fh in handles.values():
-            fh.close()
+    # pass 1: the (chunk, local slice) intersections; pass 2 reads the data records they need
+    hits = []  # (path, info, [(dst tensor, byte offset in the record, bytes)])
+    for k in fqns:
+        v = flat[k]
+        mdt = md.state_dict_metadata[k]
+        if tuple(mdt.size) != tuple(v.shape):
+            raise ValueError(f"{k}: checkpoint shape {tuple(mdt.size)} != destination {tuple(v.shape)}")
+        if mdt.properties.dtype != v.dtype:
+            raise ValueError(f"{k}: checkpoint dtype {mdt.properties.dtype} != destination {v.dtype}")
+        esz = torch.empty((), dtype=v.dtype).element_size()
+        sizes_of = {tuple(c.offsets): tuple(c.sizes) for c in mdt.chunks}
+        covered = 0
+        for idx, info in chunks_of[k]:
+            fr = chunk_flat_range(idx.offset, sizes_of[tuple(idx.offset)], v.shape)
+            if fr is None:
+                raise ValueError(f"{k}: chunk at {tuple(idx.offset)} is not contiguous in row-major order; a "
+                                 f"flat-sharded destination cannot read it")
+            cs, cn = fr
+            parts = []
+            for s0, t in v.local:
+                lo, hi = max(s0, cs), min(s0 + t.numel(), cs + cn)
+                if lo >= hi:
+                    continue
+                parts.append((t[lo - s0:hi - s0], (lo - cs) * esz, (hi - lo) * esz))
+                covered += hi - lo
+            if parts:
+                hits.append((os.path.join(checkpoint_id, info.relative_path), info, parts))
+        if covered != v.local_numel():
+            raise ValueError(f"{k}: checkpoint chunks cover {covered} of this rank's {v.local_numel()} elements")
+    recs = _data_records([(path, info.offset, info.length) for path, info, _p in hits], threads)
+    for (path, _info, parts), rec in zip(hits, recs):
+        for dst, at, nb in parts:
+            group = dev_reads if (dst.is_cuda and torch.cuda.is_available()) else host_reads
+            o, l_, d = group.setdefault(path, ([], [], []))
+            o.append(rec[0] + at)
+            l_.append(nb)
+            d.append(dst.data_ptr())
     if dev_reads:
         from . import torchsave
 

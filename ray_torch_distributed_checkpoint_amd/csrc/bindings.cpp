@@ -1035,6 +1035,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         rtdc_ckpt::read_ranges(path, offs, lens, dsts, nthreads);
       },
       "parallel pread of (offset, len) ranges into raw destination pointers");
+  m.def(
+      "zip_data_records",
+      [](const std::string& path, std::vector<uint64_t> bases, std::vector<uint64_t> lens, int nthreads) {
+        py::gil_scoped_release nogil;
+        return rtdc_ckpt::zip_data_records(path, bases, lens, nthreads);
+      },
+      py::arg("path"), py::arg("bases"), py::arg("lengths"), py::arg("nthreads") = 8,
+      "(data offset, size) of the '*/data/0' record of each zip archive slice [base, base + length)");
 
   py::class_<Engine>(m, "CkptEngine")
       .def(py::init<size_t, size_t, int, int, bool, uintptr_t>(), py::arg("nslots"), py::arg("slot_bytes"),

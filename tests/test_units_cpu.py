@@ -210,3 +210,32 @@ def test_crc32_fast_matches_zlib():
         init = 0 if n % 3 == 0 else rng.getrandbits(32)
         data = buf[off:off + n]
         assert ext.crc32(data, init) == zlib.crc32(data, init), (n, off, init)
+
+
+def test_zip_data_records_native_matches_python(tmp_path):
+    """The native batch locator of tensor data records (dcp._data_records ->
+    ext.zip_data_records) returns what the Python parser returns for torch.save archives
+    concatenated in one file (DCP's .distcp layout), written by torch itself."""
+    import io
+    import os
+
+    import torch
+
+    from ray_torch_distributed_checkpoint_amd.checkpoint import dcp
+
+    path = os.path.join(tmp_path, "f.distcp")
+    items = []
+    with open(path, "wb") as f:
+        for i, shape in enumerate([(3,), (17, 5), (0,), (1000,), (2, 3, 4)]):
+            b = io.BytesIO()
+            torch.save(torch.arange(int(torch.Size(shape).numel()), dtype=torch.float32).reshape(shape) + i, b)
+            raw = b.getvalue()
+            items.append((path, f.tell(), len(raw)))
+            f.write(raw)
+    py = [dcp._zip_data_record(p, base, ln) for p, base, ln in items]
+    nat = dcp._data_records(items, threads=4)
+    assert nat == [(int(o), int(n)) for o, n in py]
+    with open(path, "rb") as f:
+        for (o, n), (_p, base, ln) in zip(nat, items):
+            f.seek(o)
+            assert len(f.read(n)) == n and base <= o and o + n <= base + ln
