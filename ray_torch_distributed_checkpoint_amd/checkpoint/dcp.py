@@ -356,6 +356,10 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
         ready = torch.cuda.Event()
         ready.record()
     ext = _ext.ext()
+    # this rank's records, built once: the engine writes them and - the layout depends on record
+    # names and sizes only - they also plan this rank's file for the metadata and the verify pass
+    arcs_mine = _archives_for(mine, with_ptrs=True) if mine else []
+    lay_mine = None
     metadata = None
     if rank == 0 or not replicated or sim:
         sd_md = {}
@@ -363,8 +367,10 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
         ranks = range(world) if replicated else [rank]
         for r in ranks:
             fname = f"__{r}_0.distcp"
-            arcs = _archives_for(per_rank[r], with_ptrs=False)
-            _, lay = ext.plan_layout(arcs)
+            if r == rank:
+                _, lay = lay_mine = ext.plan_layout(arcs_mine)
+            else:
+                _, lay = ext.plan_layout(_archives_for(per_rank[r], with_ptrs=False))
             for it, (base, size, _recs) in zip(per_rank[r], lay):
                 if it.kind == "tensor" and it.chunk is not None:
                     offs, sizes, gshape = it.chunk
@@ -402,12 +408,11 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     nbytes = sum(it.nbytes for it in mine)
     verify = []
     if mine:
-        arcs = _archives_for(mine, with_ptrs=True)
         path = os.path.join(checkpoint_id, f"__{rank}_0.distcp")
-        handle = torchsave.submit_files([(path, fsync, crc, arcs)],
+        handle = torchsave.submit_files([(path, fsync, crc, arcs_mine)],
                                         [lease] + [it.tensor for it in mine if it.tensor is not None], nbytes, ready)
         if os.environ.get("RTDC_CKPT_VERIFY", "0") == "1":
-            _, lay = ext.plan_layout(_archives_for(mine, with_ptrs=False))
+            _, lay = lay_mine or ext.plan_layout(arcs_mine)
             verify = [(path, base, size, it.tensor) for it, (base, size, _r) in zip(mine, lay) if it.kind == "tensor"]
     h = AsyncSave(checkpoint_id, handle, metadata, rank, t0, time.perf_counter() - t0, nbytes, process_group)
     h._verify = verify
