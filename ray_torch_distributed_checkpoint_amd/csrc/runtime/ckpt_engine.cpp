@@ -1074,11 +1074,18 @@ static std::pair<uint64_t, uint64_t> zip_data_record(int fd, uint64_t base, uint
         const char* ex = &cd[pos + 46 + nlen];
         while (e + 4 <= elen) {
           const uint16_t tag = rd16(ex + e), sz = rd16(ex + e + 2);
+          if (e + 4 + sz > elen) throw std::runtime_error("corrupt zip64 extra field");
           if (tag == 1) {
             size_t v = e + 4;
-            if (usize == kZ32) { usize = rd64(ex + v); v += 8; }
-            if (csize == kZ32) { csize = rd64(ex + v); v += 8; }
-            if (lho == kZ32) { lho = rd64(ex + v); v += 8; }
+            const size_t end = e + 4 + sz;
+            auto next64 = [&](uint64_t& x) {
+              if (v + 8 > end) throw std::runtime_error("short zip64 extra field");
+              x = rd64(ex + v);
+              v += 8;
+            };
+            if (usize == kZ32) next64(usize);
+            if (csize == kZ32) next64(csize);
+            if (lho == kZ32) next64(lho);
             break;
           }
           e += 4 + sz;

@@ -175,6 +175,8 @@ def test_zip64_record_over_4gib_is_torch_loadable(tmp_path):
     # the DCP record locator (used by dcp.load) on the same archive
     off, size = dcp._zip_data_record(path, 0, os.path.getsize(path))
     assert size == n
+    # ... and its native batch form (ZIP64 end record + extra-field sizes)
+    assert dcp._data_records([(path, 0, os.path.getsize(path))]) == [(off, size)]
     with open(path, "rb") as f:
         f.seek(off + n - 77)
         assert f.read(77) == bytes([201]) * 77
