@@ -218,7 +218,10 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
                                                        const float* __restrict__ gamma = nullptr,
                                                        const float* __restrict__ beta = nullptr) {
   const bool mx = gamma != nullptr;  // relu mask from x
-  __shared__ float red[2][256][8];
+  // channel-major partials: red[k][e][thread] - consecutive threads hit consecutive banks on both
+  // the stores and the reduction's reads (a [thread][8] layout made the reads 8-way conflicted:
+  // 4.3 conflict cycles per LDS instruction, round-5 ResNet PMC)
+  __shared__ float red[2][8][256];
   const long long r0 = (long long)blockIdx.x * R;
   const long long r1 = min(N, r0 + R);
   const int n = (int)max(0LL, r1 - r0);
@@ -324,27 +327,28 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[0][t][e] = s1[e];
-      red[1][t][e] = s2[e];
+      red[0][e][t] = s1[e];
+      red[1][e][t] = s2[e];
     }
     __syncthreads();
-    if (t < chunk) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float A = 0.f, Bq = 0.f;
-        for (int l = 0; l < rl; ++l) {
-          A += red[0][l * chunk + t][e];
-          Bq += red[1][l * chunk + t][e];
-        }
-        float o0 = A, o1 = Bq;
-        if (mode == 0) {
-          const float p = n > 0 ? bf2f(a[r0 * C + c + e]) : 0.f;
-          o0 = n > 0 ? p + A / n : 0.f;
-          o1 = n > 0 ? fmaxf(Bq - A * A / n, 0.f) : 0.f;
-        }
-        out0[(long long)blockIdx.x * C + c + e] = o0;
-        out1[(long long)blockIdx.x * C + c + e] = o1;
+    // one thread per output channel (8 x chunk of them, not one thread per 8-channel group):
+    // each sums its rl row-lane partials in lane order, the order of the loop it replaces
+    for (int o = t; o < 8 * chunk; o += 256) {
+      const int e = o / chunk, go = o - e * chunk;
+      float A = 0.f, Bq = 0.f;
+      for (int l = 0; l < rl; ++l) {
+        A += red[0][e][l * chunk + go];
+        Bq += red[1][e][l * chunk + go];
       }
+      const int ce = (gbase + go) * 8 + e;
+      float o0 = A, o1 = Bq;
+      if (mode == 0) {
+        const float p = n > 0 ? bf2f(a[r0 * C + ce]) : 0.f;
+        o0 = n > 0 ? p + A / n : 0.f;
+        o1 = n > 0 ? fmaxf(Bq - A * A / n, 0.f) : 0.f;
+      }
+      out0[(long long)blockIdx.x * C + ce] = o0;
+      out1[(long long)blockIdx.x * C + ce] = o1;
     }
     __syncthreads();
   }
@@ -829,7 +833,7 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_reduce_kernel(const bf16_t* _
                                                                 int Ho, int Wo, float* __restrict__ out0,
                                                                 float* __restrict__ out1) {
   constexpr int CG = C / 8;
-  __shared__ float red[2][256][8];
+  __shared__ float red[2][8][256];  // channel-major (conflict-free, as bn_reduce_kernel)
   const int total = B * H * W * CG;
   const int i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
   const int c = (i0 % CG) * 8;
@@ -860,21 +864,21 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_reduce_kernel(const bf16_t* _
   const int t = threadIdx.x;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    red[0][t][e] = s1[e];
-    red[1][t][e] = s2[e];
+    red[0][e][t] = s1[e];
+    red[1][e][t] = s2[e];
   }
   __syncthreads();
-  if (t < CG) {  // threads t, t + CG, t + 2 CG, ... of this block share channel group t (fixed order)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float A = 0.f, Bq = 0.f;
-      for (int l = t; l < 256; l += CG) {
-        A += red[0][l][e];
-        Bq += red[1][l][e];
-      }
-      out0[(long long)blockIdx.x * C + t * 8 + e] = A;
-      out1[(long long)blockIdx.x * C + t * 8 + e] = Bq;
+  // one thread per output channel: threads go, go + CG, go + 2 CG, ... of this block share channel
+  // group go (summed in that fixed order)
+  for (int o = t; o < 8 * CG; o += 256) {
+    const int e = o / CG, go = o - e * CG;
+    float A = 0.f, Bq = 0.f;
+    for (int l = go; l < 256; l += CG) {
+      A += red[0][e][l];
+      Bq += red[1][e][l];
     }
+    out0[(long long)blockIdx.x * C + go * 8 + e] = A;
+    out1[(long long)blockIdx.x * C + go * 8 + e] = Bq;
   }
 }
 
