@@ -95,14 +95,14 @@ __device__ __forceinline__ void grid_pos(const Args& a, int& x, int& y) {
 }
 
 // [64 rows][DH] bf16 LDS image, 16-B chunks XOR-swizzled per row by (row & 7) at Dh 64,
-// (row & 15) at Dh 128: bank-conflict-free for both readers - the ds_read_b128 row reads
-// (frag_rows) and the 32-lane ds_read_b64_tr_b16 halves (frag_cols).  The round-4 (row >> 1) & 7
-// swizzle left every transposing read 2-way (two rows of a lane pair on one bank; round-5 PMC:
-// 1.0-1.3 conflict cycles per LDS instruction in the three flash kernels).
+// 2 (row & 7) at Dh 128: bank-conflict-free for both readers - the ds_read_b128 row reads
+// (frag_rows) and the 32-lane ds_read_b64_tr_b16 halves (frag_cols).  Round 4's (row >> 1) & 7
+// (Dh 64) and (row & 15) (Dh 128) left every transposing read 2-way (two rows of a 32-lane half
+// on one bank; round-5 PMC: 1.0-1.3 conflict cycles per LDS instruction in the flash kernels).
 template <int DH>
 __device__ __forceinline__ int toff(int row, int chunk) {
   if constexpr (DH == 64) return row * 128 + ((chunk ^ (row & 7)) << 4);
-  else return row * 256 + ((chunk ^ (row & 15)) << 4);
+  else return row * 256 + ((chunk ^ ((row & 7) << 1)) << 4);
 }
 
 // global -> LDS copy of rows [r0, r0+64) (row stride ld elements, column offset col0) by all
@@ -125,7 +125,7 @@ __device__ __forceinline__ void stage(const bf16_t* base, long long ld, int r0, 
     const int pch = lane % CPR;
     int lch;
     if constexpr (DH == 64) lch = pch ^ (row & 7);
-    else lch = pch ^ (row & 15);
+    else lch = pch ^ ((row & 7) << 1);
     const bf16_t* src = HOIST ? tb + (row * (int)ld + lch * 8) : base + (long long)(r0 + row) * ld + col0 + lch * 8;
     __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(tile + piece * 1024), 16, 0, 0);
   }
@@ -150,7 +150,7 @@ __device__ __forceinline__ void tr_lane_offsets(uint32_t (&off)[DH / 16], int la
   constexpr int RB = DH * 2;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int lr = 4 * g + q, pb = p >> 1;
-  const int f = DH == 64 ? (lr & 7) : (lr & 15);
+  const int f = DH == 64 ? (lr & 7) : ((lr & 7) << 1);
 #pragma unroll
   for (int d = 0; d < DH / 16; ++d) off[d] = lr * RB + ((((2 * d) + pb) ^ f) << 4) + ((p & 1) << 3);
 }
