@@ -43,14 +43,19 @@ class CapturedStep:
                 fn()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        self.philox.enter_graph_mode(dev)
+        # several captured steps (e.g. one per input batch) share the device counter base: the
+        # first capture enters graph mode, the others reuse it (each ends with base += consumed)
+        self._owns_philox = self.philox._base is None
+        if self._owns_philox:
+            self.philox.enter_graph_mode(dev)
         self.graph = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(self.graph, pool=pool):
                 self.out = fn()
                 self.philox.end_graph_step()
         except Exception:
-            self.philox.exit_graph_mode()
+            if self._owns_philox:
+                self.philox.exit_graph_mode()
             raise
         self.replays = 0
 
@@ -60,6 +65,8 @@ class CapturedStep:
         return self.out
 
     def close(self) -> None:
-        """Leave graph mode: the host Philox counter resumes where the replays left it."""
+        """Leave graph mode (the capture that entered it): the host Philox counter resumes where
+        the replays left it."""
         torch.cuda.synchronize()
-        self.philox.exit_graph_mode()
+        if self._owns_philox:
+            self.philox.exit_graph_mode()

@@ -202,3 +202,53 @@ def test_toy_mlp_hipgraph_step_matches_eager():
     assert torch.equal(le, lg), (le, lg)
     assert all(torch.equal(a, b) for a, b in zip(pe, pg))
     assert se == sg
+
+
+def test_resnet18_two_captured_steps_replay_equals_eager():
+    """bench.py --graph for ResNet-18: one captured step per synthetic batch (shared memory
+    pool, replayed alternately in capture order) trains exactly as the eager steps do - loss,
+    parameters and BatchNorm running statistics bitwise equal after the same step sequence."""
+    from ray_torch_distributed_checkpoint_amd import ops
+    from ray_torch_distributed_checkpoint_amd.models import ResNet18
+    from ray_torch_distributed_checkpoint_amd.optim import FusedSGD
+    from ray_torch_distributed_checkpoint_amd.utils.graphs import CapturedStep
+
+    torch.manual_seed(0)
+    base = ResNet18(num_classes=10)
+    pool = [(torch.randn(8, 3, 64, 64, device="cuda"), torch.randint(0, 10, (8,), device="cuda")) for _ in range(2)]
+    seed = torch.ones((), device="cuda")
+
+    def run(graph):
+        m = copy.deepcopy(base).cuda()
+        opt = FusedSGD(m.parameters(), lr=1e-2, momentum=0.9, weight_decay=5e-5)
+
+        def step(i):
+            x, y = pool[i % 2]
+            loss = ops.cross_entropy(m(x), y)
+            loss.backward(seed)
+            opt.step()
+            opt.zero_grad()
+            return loss.detach()
+
+        losses = [step(0).clone(), step(1).clone()]  # eager warm-up (the bench's warmup steps)
+        if graph:
+            gp = torch.cuda.graph_pool_handle()
+            caps = [CapturedStep(lambda k=k: step(k), warmup=1, pool=gp) for k in range(2)]  # 2 more steps
+            for i in range(2, 8):
+                losses.append(caps[i % 2].replay().clone())
+            caps[0].close()
+        else:
+            for i in range(2):  # what the two captures' warm-ups ran
+                losses.append(step(i).clone())
+            for i in range(2, 8):
+                losses.append(step(i).clone())
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+    le, se = run(False)
+    lg, sg = run(True)
+    assert len(le) == 10 and len(lg) == 8  # the two captures' warm-up steps return no loss here
+    for a, b in zip(le[-6:], lg[-6:]):
+        assert torch.equal(a, b)
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
