@@ -19,6 +19,8 @@
 // writes the int64 outputs.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace rtdc {
 
 constexpr int SORT_WAVES = 16;
@@ -34,6 +36,131 @@ __device__ __forceinline__ uint64_t peers_of(uint32_t d, bool valid) {
     m &= bit ? bal : ~bal;
   }
   return m;
+}
+
+// Segments of at most SORT_REG_CHUNKS 64-element chunks per wave (n <= 16 x 16 x 64 = 16384, the
+// GPT-2 step's token count) are held in registers for a whole pass: every load of the pass is
+// issued at once, where the chunk loop below waits for one global load per chunk and phase (the
+// kernel ran 230-320 us per step that way, latency-bound, on the side stream under the LM head).
+constexpr int SORT_REG_CHUNKS = 16;
+
+__global__ __launch_bounds__(1024) void sort_ids_reg_kernel(const int64_t* __restrict__ ids, int n, int passes,
+                                                            uint32_t* __restrict__ k0, uint32_t* __restrict__ v0,
+                                                            uint32_t* __restrict__ k1, uint32_t* __restrict__ v1,
+                                                            int64_t* __restrict__ sorted, int64_t* __restrict__ perm) {
+  __shared__ uint32_t hist[SORT_WAVES][SORT_RADIX];
+  __shared__ uint32_t dsum[SORT_RADIX];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int chunks = (n + 63) >> 6;
+  const int cper = (chunks + SORT_WAVES - 1) / SORT_WAVES;  // <= SORT_REG_CHUNKS (host-checked)
+  const int beg = min(n, w * cper * 64), end = min(n, (w + 1) * cper * 64);
+  const int nch = (end - beg + 63) >> 6;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    const uint32_t* sk = (p & 1) ? k0 : k1;
+    const uint32_t* sv = (p & 1) ? v0 : v1;
+    uint32_t* dk = (p & 1) ? k1 : k0;
+    uint32_t* dv = (p & 1) ? v1 : v0;
+    const bool last = (p == passes - 1);
+#pragma unroll
+    for (int j = 0; j < SORT_RADIX / 64; ++j) hist[w][lane + 64 * j] = 0u;
+    // the wave's whole segment, all loads in flight together
+    uint32_t kr[SORT_REG_CHUNKS], vr[SORT_REG_CHUNKS];
+#pragma unroll
+    for (int j = 0; j < SORT_REG_CHUNKS; ++j) {
+      const int i = beg + 64 * j + lane;
+      kr[j] = 0u;
+      vr[j] = 0u;
+      if (j < nch && i < end) {
+        if (p == 0) {
+          kr[j] = (uint32_t)ids[i];
+          vr[j] = (uint32_t)i;
+        } else {
+          kr[j] = sk[i];
+          vr[j] = sv[i];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // 1. per-wave digit counts
+#pragma unroll
+    for (int j = 0; j < SORT_REG_CHUNKS; ++j) {
+      if (j < nch) {
+        const bool valid = beg + 64 * j + lane < end;
+        const uint32_t d = (kr[j] >> shift) & 0xffu;
+        const uint64_t m = peers_of(d, valid);
+        if (valid && (m & below) == 0) hist[w][d] += (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();
+    // 2. exclusive scan in (digit-major, wave-minor) order
+    if (threadIdx.x < SORT_RADIX) {
+      const int d = threadIdx.x;
+      uint32_t run = 0;
+#pragma unroll
+      for (int ww = 0; ww < SORT_WAVES; ++ww) {
+        const uint32_t c = hist[ww][d];
+        hist[ww][d] = run;
+        run += c;
+      }
+      dsum[d] = run;
+    }
+    __syncthreads();
+    if (w == 0) {
+      uint32_t v[4], s = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = dsum[lane * 4 + j];
+        s += v[j];
+      }
+      uint32_t inc = s;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += o;
+      }
+      uint32_t ex = inc - s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dsum[lane * 4 + j] = ex;
+        ex += v[j];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < SORT_RADIX) {
+      const int d = threadIdx.x;
+      const uint32_t b = dsum[d];
+#pragma unroll
+      for (int ww = 0; ww < SORT_WAVES; ++ww) hist[ww][d] += b;
+    }
+    __syncthreads();
+    // 3. stable scatter (segment order, then lane order)
+#pragma unroll
+    for (int j = 0; j < SORT_REG_CHUNKS; ++j) {
+      if (j < nch) {
+        const bool valid = beg + 64 * j + lane < end;
+        const uint32_t d = (kr[j] >> shift) & 0xffu;
+        const uint64_t m = peers_of(d, valid);
+        const uint32_t at = hist[w][d] + (uint32_t)__popcll(m & below);
+        __builtin_amdgcn_wave_barrier();
+        if (valid) {
+          if (last) {
+            sorted[at] = (int64_t)kr[j];
+            perm[at] = (int64_t)vr[j];
+          } else {
+            dk[at] = kr[j];
+            dv[at] = vr[j];
+          }
+          if ((m & below) == 0) hist[w][d] += (uint32_t)__popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(1024) void sort_ids_kernel(const int64_t* __restrict__ ids, int n, int passes,
@@ -184,8 +311,13 @@ extern "C" int rtdc_sort_ids(const int64_t* ids, int n, int nbits, uint32_t* ws,
   uint32_t* v0 = ws + n;
   uint32_t* k1 = ws + 2LL * n;
   uint32_t* v1 = ws + 3LL * n;
-  hipLaunchKernelGGL(sort_ids_kernel, dim3(1), dim3(SORT_WAVES * 64), 0, st, ids, n, passes, k0, v0, k1, v1, sorted,
-                     perm);
+  const int chunks = (n + 63) / 64, cper = (chunks + SORT_WAVES - 1) / SORT_WAVES;
+  if (cper <= SORT_REG_CHUNKS && !(getenv("RTDC_SORT_REG") && getenv("RTDC_SORT_REG")[0] == '0'))
+    hipLaunchKernelGGL(sort_ids_reg_kernel, dim3(1), dim3(SORT_WAVES * 64), 0, st, ids, n, passes, k0, v0, k1, v1,
+                       sorted, perm);
+  else
+    hipLaunchKernelGGL(sort_ids_kernel, dim3(1), dim3(SORT_WAVES * 64), 0, st, ids, n, passes, k0, v0, k1, v1,
+                       sorted, perm);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -921,9 +921,11 @@ def test_fp32_linear_fused_dropout_equals_separate_kernel(M, K, N, p):
     assert (a[0] == 0).float().mean().item() > p * 0.5  # really dropped
 
 
-@pytest.mark.parametrize("n,V", [(1, 10), (63, 50257), (1000, 7), (16384, 50257), (2048, 128256), (5000, 1 << 24)])
+@pytest.mark.parametrize("n,V", [(1, 10), (63, 50257), (1000, 7), (16384, 50257), (2048, 128256), (5000, 1 << 24),
+                                 (16385, 50257), (32768, 128256)])
 def test_sort_ids_matches_stable_sort(n, V):
-    """Native one-workgroup radix sort == torch's stable sort (ids and original positions)."""
+    """Native one-workgroup radix sort == torch's stable sort (ids and original positions); up to
+    16384 ids the register-resident kernel, above it the chunk-loop kernel."""
     from ray_torch_distributed_checkpoint_amd.ops.embedding import sort_ids
 
     g = torch.Generator(device=DEV).manual_seed(n)
