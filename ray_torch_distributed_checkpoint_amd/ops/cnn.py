@@ -522,7 +522,9 @@ def batch_norm(x: torch.Tensor, weight, bias, running_mean, running_var, trainin
 # stem backward without the full-resolution pool gradient (RTDC_POOL_BN_FUSED=0: maxpool backward
 # + BatchNorm reduce + apply); partial rows of the statistics pass
 _POOL_BN_FUSED = os.environ.get("RTDC_POOL_BN_FUSED", "1") != "0"
-_POOL_BN_BLOCKS = 1024
+# statistics-pass blocks of the fused stem pool + BatchNorm backward (RTDC_POOL_BN_BLOCKS: A/B;
+# round 5, ResNet-18 step: 512 / 1024 / 2048 / 4096 blocks = 8.17 / 8.09 / 8.10 / 8.10 ms)
+_POOL_BN_BLOCKS = int(os.environ.get("RTDC_POOL_BN_BLOCKS", "1024"))
 
 
 class _BNReluMaxPool(torch.autograd.Function):
