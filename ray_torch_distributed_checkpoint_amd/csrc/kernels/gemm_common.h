@@ -44,23 +44,34 @@ __device__ __forceinline__ int mnmaj_swz(int kr) {
 }
 
 // Per-lane global sources of one operand tile, computed once per block.
+#ifndef RTDC_STAGER32
+#define RTDC_STAGER32 0
+#endif
 template <bool KMAJOR, int ROWS, int NW>
 struct Stager {
   static constexpr int PIECES = ROWS / 8;  // 1 KiB pieces per 64-deep k tile
   static constexpr int PPW = PIECES / NW;
+#if RTDC_STAGER32
+  // A/B build (-DRTDC_STAGER32=1): a wave-uniform base + 32-bit per-lane element offsets (half
+  // the VGPRs of 64-bit per-lane pointers; the launcher keeps operands under 2^31 elements)
+  const bf16_t* base;
+  uint32_t off[PPW];
+#else
   const bf16_t* src[PPW];
+#endif
   long long kmul;  // element stride per unit of k
 
   __device__ __forceinline__ void init(const bf16_t* X, int ld, int rows, int r0, int wave, int lane) {
 #pragma unroll
     for (int ii = 0; ii < PPW; ++ii) {
       const int piece = wave * PPW + ii;
+      long long o;
       if constexpr (KMAJOR) {
         const int row = piece * 8 + (lane >> 3);
         const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
         int gr = r0 + row;
         gr = gr < rows ? gr : rows - 1;
-        src[ii] = X + (long long)gr * ld + lchunk * 8;
+        o = (long long)gr * ld + lchunk * 8;
       } else {
         constexpr int CPR = ROWS / 8;     // 16-B chunks per k-row
         constexpr int KRP = 1024 / (ROWS * 2);  // k-rows per piece
@@ -68,10 +79,26 @@ struct Stager {
         const int lchunk = (lane % CPR) ^ mnmaj_swz<ROWS>(kr);
         int gc = r0 + lchunk * 8;
         gc = gc < rows ? gc : rows - 8;
-        src[ii] = X + (long long)kr * ld + gc;
+        o = (long long)kr * ld + gc;
       }
+#if RTDC_STAGER32
+      off[ii] = (uint32_t)o;
+#else
+      src[ii] = X + o;
+#endif
     }
+#if RTDC_STAGER32
+    base = X;
+#endif
     kmul = KMAJOR ? 1 : ld;
+  }
+
+  __device__ __forceinline__ const bf16_t* addr(int ii, long long koff) const {
+#if RTDC_STAGER32
+    return base + (koff + off[ii]);
+#else
+    return src[ii] + koff;
+#endif
   }
 
   __device__ __forceinline__ void issue(int k0, char* lds_tile, int wave) const {
@@ -79,14 +106,14 @@ struct Stager {
 #pragma unroll
     for (int ii = 0; ii < PPW; ++ii) {
       const int piece = wave * PPW + ii;
-      __builtin_amdgcn_global_load_lds((const void*)(src[ii] + koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)addr(ii, koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
     }
   }
   // one piece (1 KiB per wave) of issue(): lets a schedule interleave the DMA with MFMAs
   __device__ __forceinline__ void issue_one(int k0, char* lds_tile, int wave, int ii) const {
     const long long koff = (long long)k0 * kmul;
     const int piece = wave * PPW + ii;
-    __builtin_amdgcn_global_load_lds((const void*)(src[ii] + koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)addr(ii, koff), LDS_PTR(lds_tile + piece * 1024), 16, 0, 0);
   }
 };
 
