@@ -458,7 +458,7 @@ class Engine {
   // already owns (PyTorch's pool).  0 creates a private one.  Every stream a process creates can
   // cost a hardware queue: with two ranks time-sharing one GPU, ONE extra idle stream per process
   // made the training step 10-15x slower (hardware-queue oversubscription; measured with a bare
-  // hipStreamCreate, scripts/diag_postckpt.py, profiles/ckpt_engine_stream_r5.txt).
+  // hipStreamCreate, scripts/ab_r5/diag_postckpt.py, profiles/ckpt_engine_stream_r5.txt).
   Engine(size_t nslots, size_t slot_bytes, int nwriters, int device, bool direct_io = true, uintptr_t stream = 0)
       : ring_(nslots, slot_bytes), device_(device), direct_io_(direct_io) {
     if (g_have_gpu()) {

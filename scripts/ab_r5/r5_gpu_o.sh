@@ -4,8 +4,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 120 python scripts/attn_dump.py gpurun_out/attn_new.pt > gpurun_out/o_dump1.log 2>&1 || { echo dump1 failed; tail gpurun_out/o_dump1.log; exit 1; }
-RTDC_EXT_SO=abv/_C_oldswz.so timeout -k 10 120 python scripts/attn_dump.py gpurun_out/attn_old.pt > gpurun_out/o_dump2.log 2>&1 || { echo dump2 failed; exit 1; }
+timeout -k 10 120 python scripts/ab_r5/attn_dump.py gpurun_out/attn_new.pt > gpurun_out/o_dump1.log 2>&1 || { echo dump1 failed; tail gpurun_out/o_dump1.log; exit 1; }
+RTDC_EXT_SO=abv/_C_oldswz.so timeout -k 10 120 python scripts/ab_r5/attn_dump.py gpurun_out/attn_old.pt > gpurun_out/o_dump2.log 2>&1 || { echo dump2 failed; exit 1; }
 python3 -c "
 import torch
 a=torch.load('gpurun_out/attn_new.pt', weights_only=True); b=torch.load('gpurun_out/attn_old.pt', weights_only=True)

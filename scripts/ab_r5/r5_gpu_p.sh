@@ -4,8 +4,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out /tmp/dump
-timeout -k 10 180 python scripts/resnet_dump.py /tmp/dump/new.pt > gpurun_out/p_dump1.log 2>&1 || { echo dump1 failed; tail gpurun_out/p_dump1.log; exit 1; }
-RTDC_EXT_SO=abv/_C_oldbn.so timeout -k 10 180 python scripts/resnet_dump.py /tmp/dump/old.pt > gpurun_out/p_dump2.log 2>&1 || { echo dump2 failed; exit 1; }
+timeout -k 10 180 python scripts/ab_r5/resnet_dump.py /tmp/dump/new.pt > gpurun_out/p_dump1.log 2>&1 || { echo dump1 failed; tail gpurun_out/p_dump1.log; exit 1; }
+RTDC_EXT_SO=abv/_C_oldbn.so timeout -k 10 180 python scripts/ab_r5/resnet_dump.py /tmp/dump/old.pt > gpurun_out/p_dump2.log 2>&1 || { echo dump2 failed; exit 1; }
 python3 -c "
 import torch
 a=torch.load('/tmp/dump/new.pt', weights_only=True); b=torch.load('/tmp/dump/old.pt', weights_only=True)

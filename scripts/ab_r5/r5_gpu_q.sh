@@ -4,8 +4,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out /tmp/dump
-timeout -k 10 120 python scripts/attn_dump.py /tmp/dump/attn_new.pt > gpurun_out/q_dump1.log 2>&1 || { echo dump1 failed; tail gpurun_out/q_dump1.log; exit 1; }
-RTDC_EXT_SO=abv/_C_old128.so timeout -k 10 120 python scripts/attn_dump.py /tmp/dump/attn_old.pt > gpurun_out/q_dump2.log 2>&1 || { echo dump2 failed; exit 1; }
+timeout -k 10 120 python scripts/ab_r5/attn_dump.py /tmp/dump/attn_new.pt > gpurun_out/q_dump1.log 2>&1 || { echo dump1 failed; tail gpurun_out/q_dump1.log; exit 1; }
+RTDC_EXT_SO=abv/_C_old128.so timeout -k 10 120 python scripts/ab_r5/attn_dump.py /tmp/dump/attn_old.pt > gpurun_out/q_dump2.log 2>&1 || { echo dump2 failed; exit 1; }
 python3 -c "
 import torch
 a=torch.load('/tmp/dump/attn_new.pt', weights_only=True); b=torch.load('/tmp/dump/attn_old.pt', weights_only=True)

@@ -5,7 +5,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from ray_torch_distributed_checkpoint_amd import ops  # noqa: E402
 from ray_torch_distributed_checkpoint_amd.models import ResNet18  # noqa: E402
 
