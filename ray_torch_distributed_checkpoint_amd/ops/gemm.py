@@ -64,11 +64,20 @@ def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, 
     return C
 
 
+# RTDC_FWD_BLASLT=1: plain forward products (no bias, no activation; the residual add as the
+# library GEMM's beta * C input) on hipBLASLt instead of the hand-written kernel (A/B switch).
+_FWD_BLASLT = os.environ.get("RTDC_FWD_BLASLT", "0") == "1"
+
+
 def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None, aux_out=None,
                out_dtype=torch.bfloat16):
     """y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual)."""
     M, K = x2d.shape
     N = w.shape[0]
+    if (_FWD_BLASLT and act == ACT_NONE and bias is None and aux_out is None and out_dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16
+            and (residual is None or residual.dtype == torch.bfloat16)):
+        return torch.matmul(x2d, w.t()) if residual is None else torch.addmm(residual, x2d, w.t())
     y = torch.empty((M, N), dtype=out_dtype, device=x2d.device)
     gemm_bf16(x2d, w, y, M, N, K, K, K, N, True, True, Cin=residual, bias=bias, aux_out=aux_out,
               beta=1.0 if residual is not None else 0.0, act=act)
