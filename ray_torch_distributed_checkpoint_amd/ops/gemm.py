@@ -64,9 +64,19 @@ def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, 
     return C
 
 
-# RTDC_FWD_BLASLT=1: plain forward products (no bias, no activation; the residual add as the
-# library GEMM's beta * C input) on hipBLASLt instead of the hand-written kernel (A/B switch).
-_FWD_BLASLT = os.environ.get("RTDC_FWD_BLASLT", "0") == "1"
+# Plain products (no bias, no activation, no column sums; a residual add rides as the library
+# GEMM's beta * C input) go to hipBLASLt where it beats the hand-written kernels: few-row
+# products with wide K and N - Llama-3-8B's qkv / o / gate|up / down at 2048 tokens, where the
+# 8-wave kernels trail it by 5-20 % (round-5 gemm_bench) and the step gains 3 ms (137.3 ->
+# 134.4 ms, profiles/llama_blaslt_plain_ab_r5.txt).  GPT-2 / ResNet products (16k+ rows, or
+# fused epilogues) keep the native kernels.  RTDC_FWD_BLASLT / RTDC_DGRAD_BLASLT: auto | 1 | 0.
+_FWD_BLASLT = os.environ.get("RTDC_FWD_BLASLT", "auto")
+
+
+def _blaslt_plain(mode: str, M: int, N: int, K: int) -> bool:
+    if mode == "1":
+        return True
+    return mode == "auto" and 1024 <= M <= 4096 and N >= 1024 and K >= 1024
 
 
 def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None, aux_out=None,
@@ -74,7 +84,8 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     """y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual)."""
     M, K = x2d.shape
     N = w.shape[0]
-    if (_FWD_BLASLT and act == ACT_NONE and bias is None and aux_out is None and out_dtype == torch.bfloat16
+    if (_blaslt_plain(_FWD_BLASLT, M, N, K) and act == ACT_NONE and bias is None and aux_out is None
+            and out_dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16
             and (residual is None or residual.dtype == torch.bfloat16)):
         return torch.matmul(x2d, w.t()) if residual is None else torch.addmm(residual, x2d, w.t())
@@ -84,9 +95,9 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     return y
 
 
-# RTDC_DGRAD_BLASLT=1: plain input-gradient products (no activation / column-sum epilogue) on
-# hipBLASLt - a plain library GEMM - instead of the hand-written kernel (A/B switch).
-_DGRAD_BLASLT = os.environ.get("RTDC_DGRAD_BLASLT", "0") == "1"
+# plain input-gradient products (no activation / column-sum epilogue): same rule as the forwards
+# (GPT-2's 16k-row dgrads measured neutral on hipBLASLt, profiles/dgrad_blaslt_ab_r5.txt)
+_DGRAD_BLASLT = os.environ.get("RTDC_DGRAD_BLASLT", "auto")
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None,
@@ -96,8 +107,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=Non
     the activation), reduced by the GEMM epilogue instead of a second pass over dx."""
     M, N = dy.shape
     K = w.shape[1]
-    if (_DGRAD_BLASLT and act_bwd == ACT_NONE and aux_in is None and alpha == 1.0 and alpha_dev is None
-            and colsum_out is None and w.dtype == torch.bfloat16):
+    if (_blaslt_plain(_DGRAD_BLASLT, M, K, N) and act_bwd == ACT_NONE and aux_in is None and alpha == 1.0
+            and alpha_dev is None and colsum_out is None and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16):
         return torch.matmul(dy, w)
     dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev,
