@@ -684,11 +684,31 @@ def test_gemm_auto_long_k_forward_routes_to_one_barrier(M, N, K):
 
     torch.manual_seed(M + N + K)
     x, w = _bf(M, K), _bf(N, K, scale=0.05)
-    y = G.linear_fwd(x, w)
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=DEV)
+    G.gemm_bf16(x, w, y, M, N, K, K, K, N, True, True)  # the native dispatcher's own choice
     y12 = torch.empty_like(y)
     G.gemm_bf16(x, w, y12, M, N, K, K, K, N, True, True, tile_cfg=12)
     assert torch.equal(y, y12)
     _close(y, x.float() @ w.float().t(), 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K,res", [(2048, 4096, 4096, True), (2048, 6144, 4096, False), (16384, 768, 768, True)])
+def test_linear_plain_products_blaslt_rule(M, N, K, res):
+    """ops.gemm routes plain few-row products (Llama's qkv / o / gate|up / down at 2048 tokens) to
+    hipBLASLt with the residual as beta * C, and keeps GPT-2-sized ones (16k rows) on the native
+    kernels: both forms match the fp32 reference, forward and input gradient."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(M + N)
+    x, w = _bf(M, K), _bf(N, K, scale=0.05)
+    r = _bf(M, N) if res else None
+    assert G._blaslt_plain(G._FWD_BLASLT, M, N, K) == (M <= 4096)
+    y = G.linear_fwd(x, w, residual=r)
+    ref = x.float() @ w.float().t() + (r.float() if res else 0.0)
+    _close(y, ref, 1e-2)
+    dy = _bf(M, N)
+    dx = G.linear_dgrad(dy, w)
+    _close(dx, dy.float() @ w.float(), 1e-2)
 
 
 def test_gemm_4wave_one_barrier_dgrad_gelu():
