@@ -7,7 +7,7 @@ cd /root/repo/ray_torch_distributed_checkpoint_amd
 NAME=$1; DEFS=$2
 mkdir -p ../abv /tmp/variant_$NAME
 TDIR=$(python -c "import torch,os; print(os.path.dirname(torch.__file__))")
-VAR="gemm_8ph gemm_bf16 gemm4b gemm8b"
+VAR=${VAR:-"gemm_8ph gemm_bf16 gemm4b gemm8b"}  # VAR="attn_flash" etc. to vary other kernel files
 OBJS=""
 for o in build/*.o; do
   b=$(basename $o .hip.o); skip=0
