@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the RTDC_ADAMW variant kernel was removed after this A/B: profiles/adamw_two_group_ab_r5.txt)
 # AdamW: one 4-element group per lane (RTDC_ADAMW=1) vs two groups (2) vs two groups with
 # non-temporal stores (3) - isolated on the GPT-2 parameter count, then the GPT-2 step
 set -o pipefail
