@@ -358,8 +358,13 @@ def headline(args, wl, model, world, B, T, ms_per_step, samples_per_s, final_los
         "samples_per_sec_per_gpu": round(samples_per_s / world, 3),
         "model_tflops_per_gpu": round(wl["flops_per_sample"] * samples_per_s / world / 1e12, 2),
         "model_tflops_note": wl.get("flops_note", ""),
+        # the attention FLOP convention is explicit, and the full-square figure of
+        # rounds 1-4 is reported beside it so records stay comparable across rounds
+        "flops_convention": "causal" if wl.get("flops_per_sample_full") else "dense",
         "final_loss": round(final_loss, 4),
     }
+    if wl.get("flops_per_sample_full"):
+        out["model_tflops_per_gpu_full_attn"] = round(wl["flops_per_sample_full"] * samples_per_s / world / 1e12, 2)
     if wl.get("tokens_per_sample"):
         out["tokens_per_sec"] = round(samples_per_s * wl["tokens_per_sample"], 1)
     # self-description of the communication setup (what ran, on how many ranks)
@@ -560,6 +565,7 @@ def build_workload(args, dev, rank):
                 unit=f"samples/s (sequences of {T} tokens, all GPUs)", optim_name="fused AdamW (fp32 master)",
                 data="synthetic (random tokens), random-init weights",
                 flops_per_sample=model.flops_per_token(T, causal=True) * T,
+                flops_per_sample_full=model.flops_per_token(T, causal=False) * T,
                 flops_note="6N + 6·L·d·T per token (N without the position/input embedding; causal attention: "
                            "the lower triangle only - rounds 1-4 counted the full square, ~7 % more on GPT-2)")
 

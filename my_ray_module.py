@@ -154,7 +154,9 @@ def train_func_per_worker(config: Dict):
     use_graph = (device.type == "cuda" and config.get("hipgraph", True) and n_train > 0
                  and n_train % batch_size == 0 and (world == 1 or _all_buckets_p2p(model)))
     if use_graph:
-        side = torch.cuda.Stream()
+        from ray_torch_distributed_checkpoint_amd.ops.streams import side_stream
+
+        side = side_stream(device, "capture")
         sx = torch.zeros((batch_size, 1, 28, 28), device=device)
         sy = torch.zeros((batch_size,), dtype=torch.int64, device=device)
 

@@ -177,10 +177,12 @@ class AsyncSave:
             if self._error is None and self.write_s is None:
                 try:
                     if self._h is not None:
-                        self._h.wait()
+                        self._h.wait()  # raises CommPoisonedError from the words captured at the snapshot
                     from ..parallel import health
 
-                    health.assert_healthy("checkpoint commit", sync=False)
+                    if health.poisoned(getattr(self, "_words", None)):  # (also when this rank wrote nothing)
+                        raise health.CommPoisonedError(
+                            "refusing checkpoint commit: a P2P gradient all-reduce timed out before the snapshot")
                     if getattr(self, "_verify", None):
                         _verify_written(self._verify)
                         self._verify = None
@@ -337,9 +339,9 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     from ..parallel import health
 
     # a timed-out P2P collective left NaN gradients behind: never snapshot that state.  No
-    # device sync here (that would drain the compute stream on the non-blocking path): the word
-    # is checked again in wait(), after the drain - the snapshot is stream-ordered after every
-    # collective the optimizer consumed, so by then any timeout among them is visible
+    # device sync here (that would drain the compute stream on the non-blocking path): the
+    # communicators' words are also captured right after the snapshot copies, in stream order,
+    # and wait() decides commit-or-refuse from that captured value (not the live sticky word)
     health.assert_healthy("checkpoint save", sync=False)
     sim = _simulated(simulate)
     world, rank, items, mapping, per_rank = _plan_save(state_dict, process_group, replicated, sim)
@@ -351,6 +353,7 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     lease, snaps = snapshot.take([it.tensor for it in owned_t])
     for it, t in zip(owned_t, snaps):
         it.tensor = t
+    words = health.capture_error_words()
     ready = None
     if any(it.kind == "tensor" and it.tensor.is_cuda for it in mine):
         ready = torch.cuda.Event()
@@ -410,12 +413,14 @@ def async_save(state_dict: dict, checkpoint_id: str, process_group=None, *, fsyn
     if mine:
         path = os.path.join(checkpoint_id, f"__{rank}_0.distcp")
         handle = torchsave.submit_files([(path, fsync, crc, arcs_mine)],
-                                        [lease] + [it.tensor for it in mine if it.tensor is not None], nbytes, ready)
+                                        [lease] + [it.tensor for it in mine if it.tensor is not None], nbytes, ready,
+                                        words)
         if os.environ.get("RTDC_CKPT_VERIFY", "0") == "1":
             _, lay = lay_mine or ext.plan_layout(arcs_mine)
             verify = [(path, base, size, it.tensor) for it, (base, size, _r) in zip(mine, lay) if it.kind == "tensor"]
     h = AsyncSave(checkpoint_id, handle, metadata, rank, t0, time.perf_counter() - t0, nbytes, process_group)
     h._verify = verify
+    h._words = words
     h._lease = lease if verify else None  # the verify pass reads the snapshot after the drain
     return h
 

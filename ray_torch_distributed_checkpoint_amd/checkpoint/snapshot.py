@@ -65,7 +65,15 @@ def _acquire(nbytes: int, device) -> torch.Tensor:
         # a buffer too small for this save is dropped (the state grew): keep one per save size
         for b in list(free):
             free.remove(b)
-    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+    try:
+        return torch.empty(nbytes, dtype=torch.uint8, device=device)
+    except torch.cuda.OutOfMemoryError:
+        # pooled arenas of other sizes (e.g. a larger plan of an earlier save) are what the
+        # caching allocator cannot reclaim: drop every free one and retry once
+        with _lock:
+            _pool.clear()
+        torch.cuda.empty_cache()
+        return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
 def _bytes_view(t: torch.Tensor, lo: int, n: int) -> torch.Tensor:

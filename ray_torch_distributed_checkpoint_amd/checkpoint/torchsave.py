@@ -150,9 +150,15 @@ def get_engine():
             if _engine is None:
                 nslots, slot_bytes, writers = engine_config()
                 dev = torch.cuda.current_device() if torch.cuda.is_available() else 0
-                # the copy stream comes from PyTorch's pool: a private stream would add a
-                # hardware queue to the process (see the Engine constructor)
-                stream = torch.cuda.Stream(device=dev).cuda_stream if torch.cuda.is_available() else 0
+                # the copy stream comes from PyTorch's pool (a private stream would add a
+                # hardware queue to the process, see the Engine constructor), reserved for the
+                # engine: the Stream object lives in ops/streams.py for the process lifetime and
+                # every framework stream user draws its own pool entry there
+                stream = 0
+                if torch.cuda.is_available():
+                    from ..ops.streams import side_stream
+
+                    stream = side_stream(dev, "ckpt").cuda_stream
                 _engine = _ext.ext().CkptEngine(nslots, slot_bytes, writers, dev, stream=stream)
     return _engine
 
@@ -160,8 +166,11 @@ def get_engine():
 class SaveHandle:
     """A submitted (possibly still running) native save.  `wait()` -> seconds to durable."""
 
-    def __init__(self, job_id: int, keepalive, t0: float, nbytes: int):
+    def __init__(self, job_id: int, keepalive, t0: float, nbytes: int, error_words=None):
         self.job_id, self._keep, self.t0, self.nbytes = job_id, keepalive, t0, nbytes
+        # communicator error words captured right after the snapshot (parallel/health.py):
+        # commit-or-refuse is decided from them, not from the live sticky word
+        self._words = error_words
         self._result = None
         self._error: str | None = None
         self._lock = threading.Lock()  # waited on by the training thread AND the committer thread
@@ -186,9 +195,10 @@ class SaveHandle:
                 self._keep = None  # the snapshot (arena lease / clones) is drained: release it
                 from ..parallel import health
 
-                if not err and health.error():
+                if not err and health.poisoned(self._words):
                     # a collective the snapshot depends on timed out (its NaN-poisoned state
-                    # was staged): the write is never committed
+                    # was staged): the write is never committed.  A timeout of a later step
+                    # (after the snapshot) does not void this clean checkpoint
                     self._poisoned = True
                     err = "a P2P gradient all-reduce timed out before the snapshot (state poisoned)"
                 if err:
@@ -213,14 +223,15 @@ def snapshot_tensors(tensors: list, stream=None) -> list:
     return out
 
 
-def submit_files(files: list, keepalive, nbytes: int, ready_event=None) -> SaveHandle:
-    """files: [(path, fsync, crc, [(raw, records), ...])] -> SaveHandle (non-blocking)."""
+def submit_files(files: list, keepalive, nbytes: int, ready_event=None, error_words=None) -> SaveHandle:
+    """files: [(path, fsync, crc, [(raw, records), ...])] -> SaveHandle (non-blocking).
+    error_words: parallel/health.py capture_error_words() taken at the snapshot."""
     t0 = time.perf_counter()
     ev = 0
     if ready_event is not None:
         ev = ready_event.cuda_event
     jid = get_engine().submit(files, ev)
-    return SaveHandle(jid, (keepalive, ready_event), t0, nbytes)
+    return SaveHandle(jid, (keepalive, ready_event), t0, nbytes, error_words)
 
 
 def _storages_of(tensors):
@@ -240,7 +251,7 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
     """
     from ..parallel import health
 
-    health.assert_healthy("checkpoint save", sync=False)  # re-checked after the drain (SaveHandle.wait)
+    health.assert_healthy("checkpoint save", sync=False)  # decided again from the words captured at the snapshot
     pkl, tensors = pickle_state(obj)
     if snapshot is None:
         snapshot = async_
@@ -252,6 +263,7 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
     else:
         contig = [t.detach() if t.is_contiguous() else t.detach().clone(memory_format=torch.contiguous_format)
                   for t in tensors]
+    words = health.capture_error_words()  # stream-ordered after the snapshot copies
     ready = None
     if any(t.is_cuda for t in contig):
         ready = torch.cuda.Event()
@@ -259,7 +271,7 @@ def save(obj, path: str, *, async_: bool = False, fsync: bool = True, crc: bool 
     stor = _storages_of(contig)
     nbytes = sum(s[1] for s in stor)
     recs = build_records(pkl, stor, prefix=os.path.splitext(os.path.basename(path))[0] or "archive")
-    h = submit_files([(path, fsync, crc, [(False, recs)])], [lease] + contig, nbytes, ready)
+    h = submit_files([(path, fsync, crc, [(False, recs)])], [lease] + contig, nbytes, ready, words)
     if async_:
         return h
     h.wait()

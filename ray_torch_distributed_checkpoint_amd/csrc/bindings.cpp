@@ -950,6 +950,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("allreduce_", &rtdc_p2p::P2PComm::allreduce_, py::arg("tensor"), py::arg("average") = true)
       .def("error", &rtdc_p2p::P2PComm::error)
       .def("error_ptr", &rtdc_p2p::P2PComm::error_ptr)
+      .def("snapshot_error", &rtdc_p2p::P2PComm::snapshot_error)
       .def("capacity", &rtdc_p2p::P2PComm::capacity)
       .def("epoch", &rtdc_p2p::P2PComm::epoch)
       .def_property_readonly("world", &rtdc_p2p::P2PComm::world)

@@ -502,6 +502,14 @@ class Engine {
     for (auto& sg : sig_) hsa_signal_destroy(sg);
   }
 
+  // The copy stream is a PyTorch pool stream the Python side reserves for the engine
+  // (ops/streams.py side_stream(dev, "ckpt")); should another user ever capture a hipGraph on the
+  // same handle, enqueueing here would join (or invalidate) that capture: fail the job loudly.
+  void check_stream_free() const {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream_ && hipStreamIsCapturing(stream_, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("checkpoint engine: its copy stream is being captured into a hipGraph");
+  }
   // "sdma" (hsa_amd_memory_async_copy) or "hip" (hipMemcpyAsync on the copy stream)
   std::string d2h_mode() const { return sdma_ ? "sdma" : (stream_ ? "hip" : "host"); }
 
@@ -717,6 +725,7 @@ class Engine {
         hipError_t e = wait_event_sleepy(job->ready);
         if (e != hipSuccess) throw std::runtime_error(std::string("snapshot event: ") + hipGetErrorString(e));
       } else if (stream_) {
+        check_stream_free();
         hipStreamWaitEvent(stream_, job->ready, 0);
       }
     }
@@ -767,6 +776,7 @@ class Engine {
                 }
               }
               if (!w.wait_signal) {
+                check_stream_free();
                 hipError_t e = hipMemcpyAsync(ring_.ptr(s), r.src + o, len, hipMemcpyDeviceToHost, stream_);
                 if (e != hipSuccess) {
                   ring_.release(s);

@@ -95,6 +95,15 @@ class P2PComm {
   // device-readable address of the error word (host-coherent): the fused optimizer kernels
   // skip their update when it is set (kernels/optim.hip comm_poisoned)
   int64_t error_ptr() const { return (int64_t)(uintptr_t)err_; }
+  // stream-ordered copy of the error word into dst[idx] (pinned host int32) on the current
+  // stream: a checkpoint snapshot records the outcome of exactly the collectives enqueued
+  // before it, not the live sticky word (parallel/health.py capture_error_words)
+  void snapshot_error(at::Tensor dst, int64_t idx) const {
+    TORCH_CHECK(dst.scalar_type() == at::kInt && dst.is_contiguous() && idx >= 0 && idx < dst.numel(),
+                "P2PComm.snapshot_error: contiguous int32 destination");
+    hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_).stream();
+    check(hipMemcpyAsync(dst.data_ptr<int>() + idx, err_, sizeof(int), hipMemcpyDefault, st), "hipMemcpyAsync");
+  }
   long long capacity() const { return cap_; }
   int world() const { return world_; }
   int rank() const { return rank_; }

@@ -99,7 +99,9 @@ class Dataset:
         with torch.cuda.device(dev):
             stage = [torch.empty((B,) + col.shape[1:], dtype=dtype).pin_memory() for _ in range(2)]
             views = [st.numpy() for st in stage]
-            h2d = torch.cuda.Stream(dev)
+            from ..ops.streams import side_stream
+
+            h2d = side_stream(dev, "dataset_h2d")
             landed = [None, None]
             compute = torch.cuda.current_stream(dev)
             for i, s in enumerate(range(lo, hi, B)):

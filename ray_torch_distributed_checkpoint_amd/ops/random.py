@@ -21,6 +21,7 @@ class PhiloxStream:
         self.offset = int(offset)
         self._lock = threading.Lock()
         self._base = None  # device counter base in graph mode
+        self._graph_users = 0  # live captured steps sharing _base (acquire/release_graph_mode)
 
     def device_base(self):
         return self._base
@@ -40,6 +41,23 @@ class PhiloxStream:
         if self._base is not None:
             self.offset = int(self._base.item()) + self.offset
             self._base = None
+        self._graph_users = 0
+
+    def acquire_graph_mode(self, device) -> None:
+        """A captured step starts using the device base: the first user enters graph mode, the
+        others share it (each of their graphs ends with base += consumed)."""
+        if self._base is None:
+            self.enter_graph_mode(device)
+            self._graph_users = 0
+        self._graph_users += 1
+
+    def release_graph_mode(self) -> None:
+        """A captured step is closed: graph mode ends with the LAST user, so no live graph ever
+        replays against a freed device base (or a host offset that overlaps its counter)."""
+        if self._graph_users > 0:
+            self._graph_users -= 1
+            if self._graph_users == 0:
+                self.exit_graph_mode()
 
     def reserve(self, numel: int) -> tuple[int, int]:
         """Reserve counters for `numel` elements; returns (seed, offset)."""

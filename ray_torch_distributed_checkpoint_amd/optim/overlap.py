@@ -59,7 +59,9 @@ class BackwardOverlap:
         self.groups = [[p for p in g if id(p) in mine] for g in self.groups]
         self.group_of = {id(p): gi for gi, g in enumerate(self.groups) for p in g}
         self.pgroup_of = {id(p): k for k, grp in enumerate(opt.param_groups) for p in grp["params"]}
-        self.stream = torch.cuda.Stream(device=sp.device, priority=0)
+        from ..ops.streams import side_stream
+
+        self.stream = side_stream(sp.device, "overlap")
         self._reset()
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook)
                        for g in self.groups for p in g]

@@ -11,10 +11,17 @@ source of truth for "this rank's gradients are poisoned", and three places consu
   collective and the step;
 * **the host, per step**: `DistributedDataParallel._finalize` and the captured-step replay in
   my_ray_module raise as soon as the word is visible;
-* **every checkpoint write**: `assert_healthy()` synchronises the device and raises before any
-  snapshot is taken (checkpoint/dcp.py save/async_save, checkpoint/torchsave.py save), so a
-  poisoned state is never staged, let alone committed.  A supervisor restart then resumes from
-  the last committed (clean) checkpoint (train/launcher.py).
+* **every checkpoint write**: a save refuses up front when the word is already set
+  (`assert_healthy(sync=False)`: no device sync on the non-blocking path), and it records the
+  word AT ITS SNAPSHOT (`capture_error_words()`: a stream-ordered copy of each communicator's
+  word into pinned host memory, enqueued right after the snapshot copies).  Commit-or-refuse is
+  decided from that captured value once the drain is done (`poisoned(words)`), not from the live
+  sticky word: a timeout of a LATER step that happens while this snapshot drains does not void
+  this clean checkpoint, and a timeout among the collectives the snapshot depends on always
+  does.  A supervisor restart then resumes from the last committed (clean) checkpoint
+  (train/launcher.py);
+* **report()** without a checkpoint synchronises (`assert_healthy(sync=True)`) before the
+  commit barrier, so a poisoned rank fails there even when it saves nothing.
 
 The reference has none of this (R/my_ray_module.py:155-160 relies on NCCL's own watchdog).
 """
@@ -49,6 +56,48 @@ def error() -> int:
     """Non-zero when any registered communicator recorded a timeout (reads host-coherent words;
     a collective still running on the device may set one later)."""
     return next((e for e in (c.error() for c in list(_comms)) if e), 0)
+
+
+class CapturedErrorWords:
+    """Every registered communicator's error word as it stood at a point of the current stream
+    (capture_error_words).  `value()` waits for the stream to pass that point (its own event) and
+    returns the first non-zero word, else 0."""
+
+    def __init__(self, words: torch.Tensor, event):
+        self.words, self.event = words, event
+
+    def value(self) -> int:
+        if self.event is not None:
+            self.event.synchronize()
+        return next((int(w) for w in self.words.tolist() if w), 0)
+
+
+def capture_error_words():
+    """Enqueue, on the current stream, a copy of every registered communicator's error word into
+    pinned host memory; returns a CapturedErrorWords (None when no communicator is registered).
+    A save calls it right after its snapshot copies: the words then record the outcome of exactly
+    the collectives the snapshot depends on."""
+    comms = list(_comms)
+    if not comms:
+        return None
+    on_dev = torch.cuda.is_available() and torch.cuda.is_initialized()
+    words = torch.zeros(len(comms), dtype=torch.int32, pin_memory=on_dev)
+    event = None
+    for i, c in enumerate(comms):
+        snap = getattr(c, "snapshot_error", None)
+        if snap is not None and on_dev:
+            snap(words, i)
+        else:  # no stream-ordered copy available: the host-visible value now
+            words[i] = int(c.error())
+    if on_dev:
+        event = torch.cuda.Event()
+        event.record()
+    return CapturedErrorWords(words, event)
+
+
+def poisoned(captured) -> int:
+    """Non-zero when a CapturedErrorWords recorded a timeout (None: nothing was registered)."""
+    return 0 if captured is None else captured.value()
 
 
 def assert_healthy(what: str = "checkpoint", sync: bool = True) -> None:

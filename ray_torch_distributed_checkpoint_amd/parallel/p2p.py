@@ -55,3 +55,7 @@ class P2PAllReduce:
     def error_ptr(self) -> int:
         """Device-readable address of the error word (the fused optimizers' `skip_ptr`)."""
         return self.comm.error_ptr()
+
+    def snapshot_error(self, dst: torch.Tensor, idx: int) -> None:
+        """Copy the error word into dst[idx] (pinned int32), ordered on the current stream."""
+        self.comm.snapshot_error(dst, int(idx))

@@ -196,8 +196,11 @@ class _Session:
         from ..parallel import health
 
         # a rank whose gradient collective timed out (NaN-poisoned, update skipped) fails here,
-        # before the commit barrier: the attempt dies and nothing of this report is committed
-        health.assert_healthy("report", sync=False)  # the save's wait() re-checks after its drain
+        # before the commit barrier: the attempt dies and nothing of this report is committed.
+        # With a checkpoint attached, its save decides from the words captured at its snapshot
+        # (no device sync on the async path); without one, synchronise so every collective
+        # enqueued so far has completed or recorded its timeout
+        health.assert_healthy("report", sync=checkpoint is None)
         rank = self.ctx.world_rank
         n = self.n_reports
         key = f"s{self.ctx.attempt}/r{n}"

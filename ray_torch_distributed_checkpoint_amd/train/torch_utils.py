@@ -119,7 +119,9 @@ class DeviceLoader:
         if self.device.type != "cuda":
             yield from self.loader
             return
-        stream = torch.cuda.Stream()
+        from ..ops.streams import side_stream
+
+        stream = side_stream(self.device, "h2d")
         it = iter(self.loader)
         nxt = None
 

@@ -36,7 +36,9 @@ class CapturedStep:
         self.fn = fn
         self.philox = philox or default_stream()
         dev = torch.cuda.current_device()
-        side = torch.cuda.Stream()
+        from ..ops.streams import side_stream
+
+        side = side_stream(dev, "capture")
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up: lazy allocations, optimizer state, workspaces
             for _ in range(warmup):
@@ -44,18 +46,20 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         # several captured steps (e.g. one per input batch) share the device counter base: the
-        # first capture enters graph mode, the others reuse it (each ends with base += consumed)
-        self._owns_philox = self.philox._base is None
-        if self._owns_philox:
-            self.philox.enter_graph_mode(dev)
+        # first capture enters graph mode, the others reuse it (each ends with base += consumed);
+        # graph mode is reference-counted and ends when the last of them is closed
+        self.philox.acquire_graph_mode(dev)
+        self._holds_philox = True
         self.graph = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(self.graph, pool=pool):
+            # capture on the reserved stream, not torch.cuda.graph's own pool stream (which
+            # may alias another user's handle, e.g. the checkpoint engine's copy stream)
+            with torch.cuda.graph(self.graph, pool=pool, stream=side):
                 self.out = fn()
                 self.philox.end_graph_step()
         except Exception:
-            if self._owns_philox:
-                self.philox.exit_graph_mode()
+            self._holds_philox = False
+            self.philox.release_graph_mode()
             raise
         self.replays = 0
 
@@ -65,8 +69,10 @@ class CapturedStep:
         return self.out
 
     def close(self) -> None:
-        """Leave graph mode (the capture that entered it): the host Philox counter resumes where
-        the replays left it."""
+        """Release this capture's share of Philox graph mode; when the last live capture closes,
+        the host counter resumes where the replays left it (an owner closing first no
+        longer frees the device base other captures still replay against)."""
         torch.cuda.synchronize()
-        if self._owns_philox:
-            self.philox.exit_graph_mode()
+        if getattr(self, "_holds_philox", False):
+            self._holds_philox = False
+            self.philox.release_graph_mode()

@@ -1,7 +1,7 @@
 """Step time after each part of the bench's checkpoint phase (2 gloo ranks sharing one GPU):
 which part leaves the training step slower.
 
-    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 scripts/ab_r5/diag_postckpt.py
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 scripts/diag_postckpt.py
 """
 import os
 import sys
@@ -11,7 +11,7 @@ import time
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():

@@ -142,3 +142,68 @@ def test_writer_budget_is_per_node_and_quota_aware(monkeypatch):
     assert torchsave.default_writer_threads() == 4  # 64 // (2 * 8): the node's budget, split
     monkeypatch.setattr(hostinfo, "available_cpus", lambda: 16)
     assert torchsave.default_writer_threads() == 2
+
+
+class _FakeComm:
+    """A registered communicator whose error word the test flips (parallel/health.py)."""
+
+    def __init__(self):
+        self.err = 0
+
+    def error(self):
+        return self.err
+
+
+def _with_fake_comm(fn):
+    from ray_torch_distributed_checkpoint_amd.parallel import health
+
+    c = _FakeComm()
+    health.register(c)
+    try:
+        return fn(c)
+    finally:
+        health.unregister(c)
+
+
+def test_later_timeout_does_not_void_clean_checkpoint(tmp_path):
+    """commit-or-refuse is decided from the error words captured AT the snapshot, so a
+    timeout of a later step while this snapshot drains does not refuse the clean checkpoint."""
+    from ray_torch_distributed_checkpoint_amd.checkpoint import dcp, torchsave
+
+    def body(c):
+        h = torchsave.save({"w": torch.randn(1000)}, str(tmp_path / "a.pt"), async_=True)
+        a = dcp.async_save({"w": torch.randn(64)}, str(tmp_path / "ck"))
+        c.err = 1  # a later collective times out while the saves drain
+        assert h.wait() >= 0
+        assert a.wait() >= 0
+        # a save that starts now refuses up front
+        from ray_torch_distributed_checkpoint_amd.parallel.health import CommPoisonedError
+
+        with pytest.raises(CommPoisonedError):
+            torchsave.save({"w": torch.randn(10)}, str(tmp_path / "b.pt"), async_=True)
+
+    _with_fake_comm(body)
+
+
+def test_timeout_before_snapshot_refuses_commit(tmp_path):
+    """The words captured at the snapshot are what wait() checks: a poisoned capture refuses."""
+    from ray_torch_distributed_checkpoint_amd.checkpoint import torchsave
+    from ray_torch_distributed_checkpoint_amd.parallel import health
+
+    def body(c):
+        real = health.capture_error_words
+
+        def poisoned_capture():
+            c.err = 7  # the timeout lands between the up-front check and the snapshot
+            return real()
+
+        health.capture_error_words = poisoned_capture
+        try:
+            h = torchsave.save({"w": torch.randn(100)}, str(tmp_path / "p.pt"), async_=True)
+        finally:
+            health.capture_error_words = real
+        c.err = 0  # the live word no longer matters
+        with pytest.raises(health.CommPoisonedError):
+            h.wait()
+
+    _with_fake_comm(body)

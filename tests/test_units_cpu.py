@@ -239,3 +239,23 @@ def test_zip_data_records_native_matches_python(tmp_path):
         for (o, n), (_p, base, ln) in zip(nat, items):
             f.seek(o)
             assert len(f.read(n)) == n and base <= o and o + n <= base + ln
+
+
+def test_philox_graph_mode_is_reference_counted():
+    """Two captured steps share the device counter base; closing the first must not drop it
+    while the second still replays (utils/graphs.py CapturedStep)."""
+    from ray_torch_distributed_checkpoint_amd.ops.random import PhiloxStream
+
+    ph = PhiloxStream(seed=1, offset=100)
+    ph.acquire_graph_mode("cpu")
+    base = ph.device_base()
+    ph.acquire_graph_mode("cpu")
+    assert ph.device_base() is base
+    ph.offset = 7
+    ph.end_graph_step()  # a replayed step consumed 7
+    ph.release_graph_mode()
+    assert ph.device_base() is base and int(base.item()) == 107  # still live for the other capture
+    ph.release_graph_mode()
+    assert ph.device_base() is None and ph.offset == 107  # folded back once, by the last user
+    ph.release_graph_mode()  # extra release is a no-op
+    assert ph.offset == 107
