@@ -30,18 +30,6 @@
 namespace rtdc {
 namespace g8 {
 
-__device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
-  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-}
-// ds_read_b64_tr_b16 with an immediate byte offset (common.h ds_tr16 protocol: retire with an
-// lgkmcnt wait, then tr_use)
-template <int OFF>
-__device__ __forceinline__ bf16x4 ds_tr16_imm(uint32_t addr) {
-  bf16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
-  return r;
-}
-
 template <bool AK, bool BKM, typename OutT>
 __global__ __launch_bounds__(256, 1) void gemm4b_kernel(GemmArgs a) {
   // MN-major operands read through the asm transposing read (TrPair): retired by an explicit

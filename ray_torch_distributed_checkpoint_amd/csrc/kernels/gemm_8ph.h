@@ -1002,6 +1002,18 @@ __device__ __forceinline__ void mfma4_agpr(f32x4 (&c)[4], const bf16x8& a, const
 // serialised them with the MFMAs).  vmcnt / expcnt fields at their maxima (no wait).
 __device__ __forceinline__ void lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
+__device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+// ds_read_b64_tr_b16 with an immediate byte offset (common.h ds_tr16 protocol: retire with an
+// lgkmcnt wait, then tr_use)
+template <int OFF>
+__device__ __forceinline__ bf16x4 ds_tr16_imm(uint32_t addr) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+  return r;
+}
+
 template <bool AK, bool BKM, typename OutT>
 __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs a) {
   constexpr int BN = 256, BH = 128, SA = 64, SB = 64, TMQ = 4, TNQ = 4;

@@ -64,19 +64,10 @@ def gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, *, 
     return C
 
 
-# Plain products (no bias, no activation, no column sums; a residual add rides as the library
-# GEMM's beta * C input) go to hipBLASLt where it beats the hand-written kernels: few-row
-# products with wide K and N - Llama-3-8B's qkv / o / gate|up / down at 2048 tokens, where the
-# 8-wave kernels trail it by 5-20 % (round-5 gemm_bench) and the step gains 3 ms (137.3 ->
-# 134.4 ms, profiles/llama_blaslt_plain_ab_r5.txt).  GPT-2 / ResNet products (16k+ rows, or
-# fused epilogues) keep the native kernels.  RTDC_FWD_BLASLT / RTDC_DGRAD_BLASLT: auto | 1 | 0.
-_FWD_BLASLT = os.environ.get("RTDC_FWD_BLASLT", "auto")
-
-
-def _blaslt_plain(mode: str, M: int, N: int, K: int) -> bool:
-    if mode == "1":
-        return True
-    return mode == "auto" and 1024 <= M <= 4096 and N >= 1024 and K >= 1024
+# Every product of the models runs on the hand-written gfx950 kernels (csrc/kernels/gemm_*):
+# round 5 routed Llama-3-8B's few-row plain forwards / input gradients and GPT-2's LM-head
+# logits to hipBLASLt where it measured faster; that vendor route was removed in round 6
+# (benchmarks/gemm_bench.py keeps torch.matmul as the comparison oracle only).
 
 
 def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None, aux_out=None,
@@ -84,20 +75,10 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     """y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual)."""
     M, K = x2d.shape
     N = w.shape[0]
-    if (_blaslt_plain(_FWD_BLASLT, M, N, K) and act == ACT_NONE and bias is None and aux_out is None
-            and out_dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16
-            and (residual is None or residual.dtype == torch.bfloat16)):
-        return torch.matmul(x2d, w.t()) if residual is None else torch.addmm(residual, x2d, w.t())
     y = torch.empty((M, N), dtype=out_dtype, device=x2d.device)
     gemm_bf16(x2d, w, y, M, N, K, K, K, N, True, True, Cin=residual, bias=bias, aux_out=aux_out,
               beta=1.0 if residual is not None else 0.0, act=act)
     return y
-
-
-# plain input-gradient products (no activation / column-sum epilogue): same rule as the forwards
-# (GPT-2's 16k-row dgrads measured neutral on hipBLASLt, profiles/dgrad_blaslt_ab_r5.txt)
-_DGRAD_BLASLT = os.environ.get("RTDC_DGRAD_BLASLT", "auto")
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None,
@@ -107,9 +88,6 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=Non
     the activation), reduced by the GEMM epilogue instead of a second pass over dx."""
     M, N = dy.shape
     K = w.shape[1]
-    if (_blaslt_plain(_DGRAD_BLASLT, M, K, N) and act_bwd == ACT_NONE and aux_in is None and alpha == 1.0
-            and alpha_dev is None and colsum_out is None and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16):
-        return torch.matmul(dy, w)
     dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev,
               colsum_out=colsum_out)

@@ -70,12 +70,8 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, n_valid: int | Non
 # (96 MB), 810.1 (48 MB): the per-chunk GEMM tails cost more than the HBM round trip saves.
 _LM_CHUNK_MB = float(os.environ.get("RTDC_LMHEAD_CHUNK_MB", "0"))
 _chunk_bufs: dict = {}
-# The logits product is a plain GEMM (no epilogue: the fused work is the cross-entropy kernel
-# after it), so it may run as a library GEMM: hipBLASLt leads the persistent 8-wave kernel on
-# this shape (1174 vs 997 TF isolated, profiles/gemm_pingpong_ab_r4.txt) and the GPT-2 step
-# measured 16.88 / 16.87 vs 17.08 / 17.09 ms (alternating runs, profiles/lmhead_blaslt_ab_r5.txt),
-# so it is the default.  RTDC_LMHEAD_BLASLT=0 keeps it on the native kernel.
-_LM_BLASLT = os.environ.get("RTDC_LMHEAD_BLASLT", "1") == "1"
+# The logits product runs on the hand-written kernels like every other GEMM of the step (no
+# vendor-library route: round 5's hipBLASLt default for this product was removed in round 6).
 
 
 def _lm_chunk_rows(M: int, Vp: int) -> int:
@@ -111,9 +107,9 @@ class _LMHeadXent(torch.autograd.Function):
         tgt = target.reshape(-1).contiguous()
         R = _lm_chunk_rows(M, Vp)
         if R >= M:
-            # [M, Vp] bf16, softmax gradient written in place; the plain logits product on
-            # hipBLASLt (or the persistent 8-wave kernel, RTDC_LMHEAD_BLASLT=0)
-            logits = torch.matmul(x2, ws.t()) if _LM_BLASLT else G.linear_fwd(x2, ws)
+            # [M, Vp] bf16, softmax gradient written in place (the logits product on the
+            # persistent native GEMM: ops/gemm.py linear_fwd)
+            logits = G.linear_fwd(x2, ws)
             launch_pending_sorts()  # the embedding backward's token sort, under the xent kernel
             gpu_ext().xent(logits, logits, tgt, loss, None, None, M, vocab, Vp, scale, IGNORE_INDEX)
         else:

@@ -47,7 +47,9 @@ def test_take_matches_clones_bitwise(monkeypatch, arena):
         for r, o in zip(ref, out):
             assert o.dtype == r.dtype and o.shape == r.shape and o.is_contiguous(), name
             assert o.device == r.device, name
-            assert torch.equal(o.view(torch.uint8) if o.dim() else o, r.view(torch.uint8) if r.dim() else r), name
+            ob = o.contiguous().reshape(-1).view(torch.uint8)
+            rb = r.contiguous().reshape(-1).view(torch.uint8)
+            assert torch.equal(ob, rb), name
         if lease is not None:
             lease.release()
 
