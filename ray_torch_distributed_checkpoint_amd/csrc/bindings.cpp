@@ -21,7 +21,6 @@ int rtdc_gemm_bf16(const rtdc::GemmArgs* args, int a_kmajor, int b_kmajor, int o
 int rtdc_gemm_f32(const rtdc::GemmF32Args* args, hipStream_t st);
 int rtdc_gemm8_grouped(const rtdc::GemmArgs* args, int n, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 int rtdc_gemm4b_set(int v);
-int rtdc_gemm4s_set(int v);
 int rtdc_conv_gemm(const rtdc::GemmArgs* args, int mode, hipStream_t stream);
 int rtdc_layernorm_fwd(const void* x, const void* g, const void* b, void* y, float* mean, float* rstd,
                        int M, int D, float eps, hipStream_t st);
@@ -962,8 +961,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_bf16_grouped", &gemm_bf16_grouped);
   m.def("gemm4b", &rtdc_gemm4b_set, py::arg("v") = -1,
         "route K-major x K-major 256x256 products to the one-barrier 4-wave kernel (1/0), or query (-1); returns the previous setting");
-  m.def("gemm4s", &rtdc_gemm4s_set, py::arg("v") = -1,
-        "route the 256-wide-tile bf16-output products to the persistent stream-K 4-wave kernel (1/0), or query (-1)");
   m.def("gemm_f32", &gemm_f32);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);

@@ -612,23 +612,6 @@ extern "C" int rtdc_gemm8p_launch(const GemmArgs* args, int a_kmajor, int b_kmaj
 extern "C" int rtdc_gemm4_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 extern "C" int rtdc_gemm4b_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
 extern "C" int rtdc_gemm8b_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, int out_fp32, hipStream_t st);
-extern "C" int rtdc_gemm4s_launch(const GemmArgs* args, int a_kmajor, int b_kmajor, hipStream_t st);
-
-// cfg 14: the persistent stream-K 4-wave kernel (gemm4s.hip; bf16 outputs, any operand layout).
-// RTDC_GEMM4S: 0 off, 1 every eligible 256-wide-tile product (A/B and the default rule below).
-static int g_gemm4s = -1;
-static int gemm4s_mode() {
-  if (g_gemm4s < 0) {
-    const char* e = getenv("RTDC_GEMM4S");
-    g_gemm4s = e ? atoi(e) : 0;
-  }
-  return g_gemm4s;
-}
-extern "C" int rtdc_gemm4s_set(int v) {
-  const int old = gemm4s_mode();
-  if (v >= 0) g_gemm4s = v;
-  return old;
-}
 
 // cfg 12 / 13: the one-barrier-per-K-tile kernels (gemm4b.hip: 4 waves, any operand layout;
 // gemm8b.hip: 8 waves, forward layout).  RTDC_GEMM4B_AUTO: 2 (default) cfg 12 for K-major x
@@ -793,10 +776,6 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
     cfg = 13;
   if ((cfg == 6 || cfg == 8) && a.tile_cfg < 0 && gemm4b_mode() == 2 && a_kmajor && b_kmajor && a.K >= 2048) cfg = 12;
   if (cfg == 13 && !(a_kmajor && b_kmajor)) cfg = 6;  // the 8-wave one-barrier kernel: forward layout only
-  if (a.tile_cfg < 0 && gemm4s_mode() == 1 && cfg >= 6 && cfg <= 13 && cfg != 10 && !out_fp32 && batch == 1 &&
-      a.causal == 0 && !a.stats_mean && !a.bnb_x)
-    cfg = 14;
-  if (cfg == 14 && (out_fp32 || batch != 1 || a.causal != 0 || a.stats_mean || a.bnb_x)) cfg = 6;
   // Tail split: a forward-layout product on 256x256 tiles whose last round of tiles fills at
   // most half the 256 CUs (Llama-3-8B gate|up at 2048 tokens: 8 x 112 = 896 tiles = 3.5 rounds)
   // runs its whole rounds as one launch and the remaining column tiles on 256x128 tiles - twice
@@ -834,7 +813,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   // offsets (gemm_8ph.hip tile_epilogue)
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
                        (uintptr_t)a.bias;
-  if (cfg >= 6 && cfg <= 14 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
+  if (cfg >= 6 && cfg <= 13 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
@@ -843,7 +822,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
                   : cfg == 5 ? ntiles<Cfg64x256>(a) : ntiles<Cfg128x128>(a);
   // cfg 11: the 8-wave kernel on 256x128 tiles (bf16 output, K-major A)
   if (cfg == 11 && (out_fp32 || !a_kmajor)) cfg = 6;
-  const bool big = cfg >= 6 && cfg <= 14;  // counted-vmcnt pipelines (gemm_8ph.hip, gemm4b/4s.hip, gemm8b.hip)
+  const bool big = cfg >= 6 && cfg <= 13;  // counted-vmcnt pipelines (gemm_8ph.hip, gemm4b.hip, gemm8b.hip)
   const int bn = (cfg == 7 || cfg == 9) ? 192 : cfg == 11 ? 128 : 256;
   if (big) {
     if (batch != 1 || a.causal != 0) return 1;
@@ -853,12 +832,7 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   if (plain && (cfg <= 7 || (cfg >= 10 && cfg <= 13)))
     a.splitk = cfg >= 6 ? pick_splitk(a, tiles, 256, cfg == 7 ? 1.35 : cfg == 11 ? 1.0 : cfg == 12 ? 1.52 : cfg == 13 ? 1.45 : 1.8)
                         : pick_splitk(a, tiles);
-  if (cfg == 14) {
-    int rc = rtdc_gemm4s_launch(&a, a_kmajor, b_kmajor, stream);
-    // 1: not eligible (epilogue / layout / size), 3: no workspace while capturing
-    if (rc == 1 || rc == 3) rc = rtdc_gemm4b_launch(&a, a_kmajor, b_kmajor, 0, stream);
-    if (rc) return rc;
-  } else if (cfg == 10) {
+  if (cfg == 10) {
     const int rc = rtdc_gemm4_launch(&a, a_kmajor, b_kmajor, out_fp32, stream);
     if (rc) return rc;
   } else if (cfg == 12) {

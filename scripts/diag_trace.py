@@ -2,7 +2,10 @@
 call count and total / max host time in the baseline window vs the window after DIAG_MODE's
 ingredient (the windows are cut at the largest gap-free change of step rate: the script prints
 its step timings; here the split is the first hipStreamCreate* call after the warm-up, or the
-midpoint).  Usage: python scripts/diag_trace.py <rocprof dir> [<rank log>]"""
+midpoint).  With a peer rank's trace directory as well, the kernel side: dispatches that ran far
+longer than their kernel's median, and how much of each one the peer's kernels covered on the
+same device (profiles/multiproc_slowdown_r6.md).
+Usage: python scripts/diag_trace.py <rocprof dir> [<rank log>] [<peer rocprof dir>]"""
 import csv
 import glob
 import os
@@ -55,6 +58,33 @@ def main():
         for line in open(sys.argv[2]):
             if "ms/step" in line or "rc=" in line:
                 print(line.rstrip())
+    if len(sys.argv) > 3:
+        kernel_side(kernels(sys.argv[1]), kernels(sys.argv[3]))
+
+
+def kernels(d):
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    out = []
+    for path in f:
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                out.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60], r["Queue_Id"]))
+    return sorted(out)
+
+
+def kernel_side(mine, peer, top=12):
+    med = defaultdict(list)
+    for s, e, n, _q in mine:
+        med[n].append(e - s)
+    med = {n: sorted(v)[len(v) // 2] for n, v in med.items()}
+    slow = [k for k in mine if k[1] - k[0] > 50 * max(med[k[2]], 1000) and k[1] - k[0] > 5e6]
+    print(f"\n== KERNELS: {len(slow)} of {len(mine)} dispatches ran > 50x their kernel's median (and > 5 ms); "
+          f"{sum(k[1] - k[0] for k in slow) / 1e6:.0f} ms of dispatch time in all")
+    print(f"{'ms':>8s} {'median us':>9s}  {'kernel':60s} peer-busy-share peer-queues")
+    for s, e, n, q in sorted(slow, key=lambda k: k[0] - k[1])[:top]:
+        ov = [k for k in peer if k[1] > s and k[0] < e]
+        busy = sum(min(e, k[1]) - max(s, k[0]) for k in ov)
+        print(f"{(e - s) / 1e6:8.1f} {med[n] / 1e3:9.1f}  {n:60s} {busy / (e - s):5.2f} {sorted(set(k[3] for k in ov))}")
 
 
 if __name__ == "__main__":

@@ -105,14 +105,17 @@ for task in ${TASKS//,/ }; do
       mr() { local name=$1 port=$2; shift 2
         TAILN=1 run "mr_$name" 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port "$port" bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo "$@"; }
-      # two sweep cells: gloo's host-staged all-reduce of CUDA tensors with two processes on one
-      # device runs 10-40x slower once the checkpoint engine exists (profiles/ckpt_engine_stream_r5.txt)
+      # one HIP hardware queue per process: two processes on one device with gloo's priority
+      # streams plus the checkpoint engine's stream oversubscribe the device's queue slots and the
+      # scheduler time-slices them (kernels 1000x their length; profiles/multiproc_slowdown_r6.md)
+      export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-1}
       export RTDC_SWEEP_CELLS=fp32:32,bf16:64
       mr gpt2 29533 --batch 4 --sweep-budget-s 420 || exit $?
       mr resnet 29534 --model resnet18 --batch 32 --sweep-budget-s 420 || exit $?
       unset RTDC_SWEEP_CELLS
       mr gpt2_zero 29535 --batch 4 --zero 1 --grad-comm-dtype bf16 || exit $?
-      mr gpt2_p2p 29536 --batch 4 --p2p-kb 4096 --no-ckpt || exit $? ;;
+      mr gpt2_p2p 29536 --batch 4 --p2p-kb 4096 --no-ckpt || exit $?
+      unset GPU_MAX_HW_QUEUES ;;
     roundend)
       bash "$0" tests,smoke,bench,multirank || exit $? ;;
     py)

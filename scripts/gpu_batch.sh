@@ -9,11 +9,9 @@ step() {  # step <name> <timeout> <cmd...>
   local name=$1 to=$2; shift 2
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log"
+  echo "[$name] EXIT $rc"; tail -n 3 "gpurun_out/$name.log"
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step snap_tests 200 python -u -m pytest tests/test_snapshot_gpu.py -x -v -s --timeout 150 --timeout-method thread
-GPU_MAX_HW_QUEUES=2 DIAG_TIMEOUT=250 step diag_trace_q2 300 bash scripts/diag_trace.sh
-cp gpurun_out/diag_trace_summary.txt gpurun_out/diag_trace_summary_q2.txt 2>/dev/null
-step gpu_tests 900 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread
-step bench_gpt2 400 python bench.py --steps 20 --warmup 5
+step resume_test 300 python -u -m pytest tests/test_resume_fullsize_gpu.py -v -s --timeout 240 --timeout-method thread
+step gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
+step multirank 900 bash scripts/gpu.sh multirank

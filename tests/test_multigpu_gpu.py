@@ -277,8 +277,22 @@ def _matrix(backend, tmp_path_factory):
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_worker, args=(r, world, port, backend, path, q)) for r in range(world)]
-    for p in ps:
-        p.start()
+    # ranks sharing one device (the gloo stand-in): one HIP hardware queue each, or gloo's priority
+    # streams oversubscribe the device's queue slots and the scheduler time-slices the two
+    # processes (profiles/multiproc_slowdown_r6.md).  Set in the parent: a spawned child
+    # initialises HIP when it imports this module.
+    old_q = os.environ.get("GPU_MAX_HW_QUEUES")
+    if backend == "gloo":
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
+    try:
+        for p in ps:
+            p.start()
+    finally:
+        if backend == "gloo":
+            if old_q is None:
+                os.environ.pop("GPU_MAX_HW_QUEUES", None)
+            else:
+                os.environ["GPU_MAX_HW_QUEUES"] = old_q
     out = {}
     try:
         for _ in range(world):
