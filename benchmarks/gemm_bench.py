@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--set", default="gpt2", choices=["gpt2", "llama", "all"])
     ap.add_argument("--sweep", action="store_true", help="also time forced tile configurations (all layouts)")
     ap.add_argument("--cfgs", default="0,6,7", help="tile configurations for --sweep")
+    ap.add_argument("--layouts", default=None, help="comma list of the rows to time (e.g. fwd,dgrad,dgrad_kmaj)")
     ap.add_argument("--wgrad-group", default=None, choices=["llama", "gpt2"],
                     help="time one layer's grouped weight-gradient launch (gemm_bf16_grouped) against the "
                          "same products on hipBLASLt with fp32 output")
@@ -116,10 +117,14 @@ def main():
             ("dgrad_gelu_cs_kmaj", lambda: G.gemm_bf16(dy, wt, dxk, M, K, N, N, N, K, True, True, aux_in=x,
                                                        act=G.ACT_GELU_BWD, colsum_out=cs_out), lambda: dy @ w),
             ("dgrad", lambda: G.linear_dgrad(dy, w), lambda: dy @ w),
+            # the same product on a K-major (transposed) bf16 image of w
+            ("dgrad_kmaj", lambda: G.gemm_bf16(dy, wt, dxk, M, K, N, N, N, K, True, True), lambda: dy @ w),
             ("wgrad", lambda: G.linear_wgrad(dy, x), lambda: (dy.t() @ x)),
             # same product, hipBLASLt writing fp32 like our kernel does
             ("wgrad_f32out", lambda: G.linear_wgrad(dy, x), lambda: _mm_f32(dy.t(), x)),
         ]:
+            if args.layouts and lay not in args.layouts.split(","):
+                continue
             # interleaved rounds, best of each: neither side is always timed first
             t_o = t_r = float("inf")
             for _ in range(3):

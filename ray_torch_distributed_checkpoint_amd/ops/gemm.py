@@ -82,15 +82,21 @@ def linear_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, resi
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, act_bwd=ACT_NONE, aux_in=None, alpha=1.0, alpha_dev=None,
-                 colsum_out=None):
+                 colsum_out=None, w_kmajor=None):
     """dx[M,K] = alpha (* alpha_dev[0]) * dy[M,N] @ w[N,K]  (optionally * act'(aux_in)).
     colsum_out (fp32 [K]): also sum_m dx[m, :] (the bias gradient of the layer that produced
-    the activation), reduced by the GEMM epilogue instead of a second pass over dx."""
+    the activation), reduced by the GEMM epilogue instead of a second pass over dx.
+    w_kmajor: the same weight as a K-major [K, N] bf16 image (ops/shadow.py kmajor_image): both
+    operands then stream K-major (ds_read_b128 fragments instead of the transposing reads)."""
     M, N = dy.shape
     K = w.shape[1]
     dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
-    gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha, alpha_dev=alpha_dev,
-              colsum_out=colsum_out)
+    if w_kmajor is not None:
+        gemm_bf16(dy, w_kmajor, dx, M, K, N, N, N, K, True, True, aux_in=aux_in, act=act_bwd, alpha=alpha,
+                  alpha_dev=alpha_dev, colsum_out=colsum_out)
+    else:
+        gemm_bf16(dy, w, dx, M, K, N, N, K, K, True, False, aux_in=aux_in, act=act_bwd, alpha=alpha,
+                  alpha_dev=alpha_dev, colsum_out=colsum_out)
     return dx
 
 

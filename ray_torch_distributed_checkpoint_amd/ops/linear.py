@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from . import gemm as G
 from ._ext import gpu_ext
 from .gradbuf import grad_target
-from .shadow import shadow_of
+from .shadow import kmajor_image, kmajor_prefetch, kmajor_wanted, shadow_of
 
 
 def _relu_mask_bwd(dy: torch.Tensor, y: torch.Tensor, p: float = 0.0) -> torch.Tensor:
@@ -41,6 +41,10 @@ class _LinearBF16(torch.autograd.Function):
         ws = shadow_of(w)
         res2 = residual.reshape(-1, w.shape[0]) if residual is not None else None
         y = G.linear_fwd(x2, ws, bias=b, act=G.ACT_RELU if relu else G.ACT_NONE, residual=res2)
+        # the input gradient's K-major weight image, built on a side stream under the forward
+        ctx.kimg = ctx.needs_input_grad[0] and kmajor_wanted(w, x2.shape[0])
+        if ctx.kimg:
+            kmajor_prefetch(w)
         ctx.save_for_backward(x2, ws, y if relu else None)
         ctx.relu = relu
         ctx.has_b = b is not None
@@ -58,7 +62,8 @@ class _LinearBF16(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dpre = _relu_mask_bwd(dy2, y) if ctx.relu else dy2
         w, b = ctx.params
-        dx = G.linear_dgrad(dpre, ws).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dx = (G.linear_dgrad(dpre, ws, w_kmajor=kmajor_image(w) if ctx.kimg else None).view(ctx.in_shape)
+              if ctx.needs_input_grad[0] else None)
         dw = G.linear_wgrad(dpre, x2, out=grad_target(w)) if ctx.needs_input_grad[1] else None
         db = G.colsum(dpre, out=grad_target(b)) if ctx.has_b and ctx.needs_input_grad[2] else None
         dres = dy if ctx.has_res else None
@@ -147,25 +152,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, relu
 # Measured neutral on GPT-2-small (profiles/gelu_save_grad_ab.txt): the dgrad epilogue is not
 # bound by its two transcendentals, so the numerics stay on the original pair.
 _GELU_SAVE_GRAD = os.environ.get("RTDC_GELU_SAVE_GRAD", "0") == "1"
-# c_proj's dgrad (dpre = dy . W_proj, M x 4C outputs over K = C) reads W_proj N-major; only the
-# K-major x K-major form has the persistent 8-wave kernel (gemm_8ph.hip gemm8p_kernel, whose
-# next-tile loads and epilogue stores overlap MFMA work - 3 tile rounds at GPT-2 shapes).  The
-# forward writes a K-major bf16 image of W_proj (one transposing conversion from the fp32 master,
-# C x 4C) and the backward runs the dgrad on it.  Measured neutral on GPT-2-small (17.62 vs
-# 17.56 ms/step, alternating runs on one MI355X, profiles/colsum_defer_pool_bn_ab_r3.txt):
-# opt-in, RTDC_DGRAD_KMAJOR=1.
-_DGRAD_KMAJOR = os.environ.get("RTDC_DGRAD_KMAJOR", "0") == "1"
-
-
-def _kmajor_image(w: torch.Tensor):
-    """bf16 [in, out] image of an fp32 [out, in] master weight (None when not applicable)."""
-    if not (_DGRAD_KMAJOR and w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.is_contiguous()):
-        return None
-    t = torch.empty((w.shape[1], w.shape[0]), dtype=torch.bfloat16, device=w.device)
-    gpu_ext().f32_to_bf16_t(w.detach(), t)
-    return t
-
-
 class _FusedMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_fc, b_fc, w_proj, b_proj, residual):
@@ -182,7 +168,13 @@ class _FusedMLP(torch.autograd.Function):
                          aux_out=pre)
         res2 = residual.reshape(-1, C) if residual is not None else None
         y = G.linear_fwd(g, wps, bias=b_proj, residual=res2)
-        ctx.wp_t = _kmajor_image(w_proj) if ctx.needs_input_grad[0] or ctx.needs_input_grad[1] else None
+        # both input gradients on K-major weight images (ops/shadow.py), built under the forward:
+        # c_proj's (dpre = dy . W_proj with GELU' and the c_fc bias column sums) and c_fc's
+        ctx.kimg = (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) and kmajor_wanted(w_proj, M)
+        if ctx.kimg:
+            kmajor_prefetch(w_proj)
+            if ctx.needs_input_grad[0]:
+                kmajor_prefetch(w_fc)
         ctx.save_for_backward(x2, wfs, wps, pre, g)
         ctx.has_res = residual is not None
         ctx.in_shape = x.shape
@@ -204,15 +196,10 @@ class _FusedMLP(torch.autograd.Function):
         if db_fc is None and b_fc is not None:
             db_fc = torch.empty(b_fc.shape, dtype=torch.float32, device=dy2.device)
         act = G.ACT_MUL if _GELU_SAVE_GRAD else G.ACT_GELU_BWD
-        wp_t, ctx.wp_t = ctx.wp_t, None
-        if wp_t is not None:
-            M, H = pre.shape
-            dpre = torch.empty((M, H), dtype=torch.bfloat16, device=dy2.device)
-            G.gemm_bf16(dy2, wp_t, dpre, M, H, C, C, C, H, True, True, aux_in=pre, act=act, colsum_out=db_fc)
-        else:
-            dpre = G.linear_dgrad(dy2, wps, act_bwd=act, aux_in=pre, colsum_out=db_fc)
+        dpre = G.linear_dgrad(dy2, wps, act_bwd=act, aux_in=pre, colsum_out=db_fc,
+                              w_kmajor=kmajor_image(w_proj) if ctx.kimg else None)
         dw_fc = G.linear_wgrad(dpre, x2, out=grad_target(w_fc))
-        dx = G.linear_dgrad(dpre, wfs).view(ctx.in_shape)
+        dx = G.linear_dgrad(dpre, wfs, w_kmajor=kmajor_image(w_fc) if ctx.kimg else None).view(ctx.in_shape)
         return dx, dw_fc, db_fc, dw_proj, db_proj, (dy if ctx.has_res else None)
 
 

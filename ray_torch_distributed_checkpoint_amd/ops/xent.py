@@ -19,7 +19,7 @@ from . import gemm as G
 from ._ext import gpu_ext
 from .embedding import launch_pending_sorts
 from .gradbuf import grad_target
-from .shadow import shadow_of
+from .shadow import kmajor_image, kmajor_prefetch, kmajor_wanted, shadow_of
 
 IGNORE_INDEX = -100
 
@@ -105,6 +105,11 @@ class _LMHeadXent(torch.autograd.Function):
         loss = torch.empty(M, dtype=torch.float32, device=x.device)
         scale = 1.0 / n_valid if n_valid is not None else 1.0
         tgt = target.reshape(-1).contiguous()
+        # the logits' input gradient on a K-major image of the (tied) vocabulary matrix, built
+        # on a side stream under the logits GEMM and the loss kernel (ops/shadow.py)
+        ctx.kimg = ctx.needs_input_grad[0] and kmajor_wanted(w, M)
+        if ctx.kimg:
+            kmajor_prefetch(w)
         R = _lm_chunk_rows(M, Vp)
         if R >= M:
             # [M, Vp] bf16, softmax gradient written in place (the logits product on the
@@ -144,7 +149,7 @@ class _LMHeadXent(torch.autograd.Function):
             a = torch.empty(1, dtype=torch.float32, device=gs.device)
             gpu_ext().xent_alpha(gs, cnt, a)
             gs = a
-        dx = G.linear_dgrad(dlogits, ws, alpha_dev=gs)
+        dx = G.linear_dgrad(dlogits, ws, alpha_dev=gs, w_kmajor=kmajor_image(ctx.w) if ctx.kimg else None)
         dw = G.linear_wgrad(dlogits, x2, out=grad_target(ctx.w), alpha_dev=gs)
         return dx.view(ctx.in_shape), dw, None, None, None
 

@@ -21,6 +21,7 @@ import math
 import torch
 
 from ..ops._ext import gpu_ext
+from ..ops.shadow import bump_generation
 from .flat import FlatParamSpace, space_of
 
 
@@ -296,6 +297,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         if ov is not None:
             ov.end_step()  # the compute stream waits for the updates that ran during backward
         sp.after_step()  # ZeRO-1: gather the updated shards
+        bump_generation()  # masters / shadows changed in place: K-major weight images are stale
 
     @staticmethod
     def _rows(chunks, n):

@@ -81,7 +81,7 @@ for task in ${TASKS//,/ }; do
     norm)
       TAILN=40 run "norm_$TAG" 300 python3 benchmarks/norm_bench.py $ARGS || exit $? ;;
     ab)
-      OLD=$PWD/ab/_C_old.so
+      OLD=$PWD/abv/_C_old.so
       for r in $(seq "$ROUNDS"); do
         for arm in old new; do
           if [ $arm = old ]; then export RTDC_EXT_SO=$OLD; else unset RTDC_EXT_SO; fi

@@ -257,7 +257,7 @@ def test_fused_mlp_kmajor_dgrad_matches(monkeypatch):
 
     from ray_torch_distributed_checkpoint_amd.ops import fused_mlp
 
-    L = importlib.import_module("ray_torch_distributed_checkpoint_amd.ops.linear")
+    S = importlib.import_module("ray_torch_distributed_checkpoint_amd.ops.shadow")
     torch.manual_seed(5)
     M, C = 16384, 768
     x0 = _bf(M, C)
@@ -268,7 +268,7 @@ def test_fused_mlp_kmajor_dgrad_matches(monkeypatch):
     g = _bf(M, C)
     grads = []
     for on in (True, False):
-        monkeypatch.setattr(L, "_DGRAD_KMAJOR", on)
+        monkeypatch.setattr(S, "_KMAJOR", "1" if on else "0")
         x = x0.clone().requires_grad_(True)
         for p in (wf, bfc, wp, bp):
             p.grad = None

@@ -21,17 +21,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 pytestmark = pytest.mark.gpu
 
 
+def _sha(t):
+    return hashlib.sha1(t.detach().reshape(-1).contiguous().cpu().view(torch.uint8).numpy().tobytes()).hexdigest()
+
+
 def _digests(model, opt):
-    out = {}
-    for n, p in model.named_parameters():
-        out["p." + n] = hashlib.sha1(p.detach().contiguous().view(torch.uint8).cpu().numpy().tobytes()).hexdigest()
+    out = {"p." + n: _sha(p) for n, p in model.named_parameters()}
     for k, st in opt.state_dict()["state"].items():
         for n, v in st.items():
-            if torch.is_tensor(v):
-                out[f"o.{k}.{n}"] = hashlib.sha1(v.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes()
-                                                 ).hexdigest()
-            else:
-                out[f"o.{k}.{n}"] = repr(v)
+            out[f"o.{k}.{n}"] = _sha(v) if torch.is_tensor(v) else repr(v)
     return out
 
 
@@ -43,12 +41,21 @@ def _setup(W, dev, B):
     return wl, stream
 
 
-def _step(wl, stream):
+def _step(wl, stream, probe=None):
     x, y = stream.next()
     loss = wl.loss_fn(wl.model, x, y)
     loss.backward()
+    if probe is not None:  # the gradients this step's update reads
+        from ray_torch_distributed_checkpoint_amd.ops.gemm import flush_wgrads
+
+        flush_wgrads()
+        torch.cuda.synchronize()
+        probe["grad"] = {n: _sha(p.grad) for n, p in wl.model.named_parameters() if p.grad is not None}
     wl.optimizer.step()
     wl.optimizer.zero_grad(set_to_none=True)
+    if probe is not None:
+        torch.cuda.synchronize()
+        probe["after"] = _digests(wl.model, wl.optimizer)
     return loss.detach()
 
 
@@ -68,13 +75,15 @@ def test_gpt2_small_exact_resume_bitwise(tmp_path, mode):
     saved_pos = (stream.epoch, stream.pos)
     state = W._train_state(wl.model, wl.optimizer, stream, 3, W._rng_blob(dev))
     path = str(tmp_path / "ck")
+    live = {}
     if mode == "async":
         h = dcp.async_save(state, path)
-        ref = [_step(wl, stream) for _ in range(3)]  # training continues while the engine drains
-        h.wait()
+        # training continues while the engine drains
+        ref = [_step(wl, stream, live)] + [_step(wl, stream) for _ in range(2)]
+        h.result()  # durable + .metadata committed
     else:
         dcp.save(state, path)
-        ref = [_step(wl, stream) for _ in range(3)]
+        ref = [_step(wl, stream, live)] + [_step(wl, stream) for _ in range(2)]
     ref = [float(v) for v in ref]
 
     wl2, stream2 = _setup(W, dev, B)
@@ -84,5 +93,10 @@ def test_gpt2_small_exact_resume_bitwise(tmp_path, mode):
     got = _digests(wl2.model, wl2.optimizer)
     bad = sorted(k for k in saved if got.get(k) != saved[k])
     assert not bad, f"{len(bad)} of {len(saved)} restored entries differ, e.g. {bad[:6]}"
-    out = [float(_step(wl2, stream2)) for _ in range(3)]
+    res = {}
+    out = [float(_step(wl2, stream2, res))] + [float(_step(wl2, stream2)) for _ in range(2)]
+    gbad = sorted(k for k in live["grad"] if res["grad"].get(k) != live["grad"][k])
+    assert not gbad, f"first step after the restore: {len(gbad)} gradients differ, e.g. {gbad[:6]}"
+    abad = sorted(k for k in live["after"] if res["after"].get(k) != live["after"][k])
+    assert not abad, f"first update after the restore: {len(abad)} of {len(live['after'])} entries differ, e.g. {abad[:8]}"
     assert out == ref, (out, ref)
