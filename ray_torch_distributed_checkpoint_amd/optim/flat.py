@@ -107,6 +107,7 @@ class FlatParamSpace:
                 seen.add(id(p))
                 uniq.append(p)
         self.params = uniq
+        had_grad = any(p.grad is not None for p in uniq)
         self.device = torch.device(device) if device is not None else uniq[0].device
         self.segments: list[Segment] = []
         # "fresh" gradient mode (zero_grad(set_to_none=True)): p.grad is None until the first
@@ -139,8 +140,18 @@ class FlatParamSpace:
         if grads:
             self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
             self.grad._rtdc_flat_grad = True  # (ops/gemm.py _deferrable: a gradient slot autograd adopts)
-            for p, s in zip(uniq, self.segments):
-                p.grad = self.view(self.grad, s)
+            if had_grad:
+                for p, s in zip(uniq, self.segments):
+                    p.grad = self.view(self.grad, s)
+            else:
+                # no gradient yet (a space built before the first backward: a restore's
+                # init_state, a DDP wrap): start in the per-step mode zero_grad(set_to_none=True)
+                # leaves, so the first backward takes the same kernels (grouped weight gradients
+                # written into the slices) as every later one - a run restarted from a
+                # checkpoint then reproduces the uninterrupted run's gradients bit for bit
+                for p in uniq:
+                    p.grad = None
+                self.fresh = True
         self.shadow = None
         if shadow_dtype is not None and self.device.type == "cuda":
             self.shadow = torch.empty(off, dtype=shadow_dtype, device=self.device)

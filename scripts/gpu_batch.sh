@@ -13,5 +13,5 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
 step resume_test 300 python -u -m pytest tests/test_resume_fullsize_gpu.py -v -s --timeout 240 --timeout-method thread
-step new_tests 400 python -u -m pytest tests/test_kmajor_gpu.py tests/test_kernels_gpu.py -m gpu -k "kmajor" -v --timeout 200 --timeout-method thread
-RTDC_DGRAD_KMAJOR=auto step prof_kmaj 700 bash scripts/gpu.sh prof STEPS=10 TAG=gpt2_kmaj
+step gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
+step product 1100 python3 scripts/product_path.py gpurun_out/product
