@@ -48,6 +48,9 @@ int rtdc_sgd(const void* chunks, int nchunks, float* p, const float* g, float* b
              const int* skip, hipStream_t st);
 int rtdc_f32_to_bf16(const float* x, void* y, long long n, hipStream_t st);
 int rtdc_f32_to_bf16_t(const float* x, void* y, int R, int C, hipStream_t st);
+int rtdc_bf16_transpose_multi(const void* const* src, void* const* dst, const int* R, const int* C, int n,
+                              void* jobs_dev, hipStream_t st);
+int rtdc_bf16_transpose_jobs_bytes();
 int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float* partial, hipStream_t st);
 int rtdc_softmax_fwd(const void* S, void* P, float* lse, long long rows, int T, int causal, hipStream_t st);
 int rtdc_softmax_bwd(const void* P, const void* dP, void* dS, long long rows, int T, int causal,
@@ -389,6 +392,33 @@ static void sgd(Tensor chunks, int64_t nchunks, Tensor p, Tensor g, c10::optiona
 }
 static void f32_to_bf16(Tensor x, Tensor y) {
   check_rc(rtdc_f32_to_bf16(x.data_ptr<float>(), y.data_ptr(), (long long)x.numel(), cur_stream()), "f32_to_bf16");
+}
+// dst[i] = src[i]^T for bf16 [R, C] -> [C, R] matrices in one launch; `jobs` is a uint8 device
+// buffer of >= bf16_transpose_jobs_bytes() (the job table, uploaded on the current stream)
+static void bf16_transpose_multi(std::vector<Tensor> src, std::vector<Tensor> dst, Tensor jobs) {
+  TORCH_CHECK(src.size() == dst.size(), "bf16_transpose_multi: src/dst count");
+  TORCH_CHECK(jobs.is_cuda() && jobs.numel() >= rtdc_bf16_transpose_jobs_bytes(), "bf16_transpose_multi: jobs buffer");
+  std::vector<const void*> s;
+  std::vector<void*> d;
+  std::vector<int> R, C;
+  for (size_t i = 0; i < src.size(); ++i) {
+    const Tensor& x = src[i];
+    const Tensor& y = dst[i];
+    TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
+                "bf16_transpose_multi: contiguous bf16 [R, C] sources");
+    TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.scalar_type() == at::kBFloat16 && y.is_contiguous() &&
+                    y.size(0) == x.size(1) && y.size(1) == x.size(0),
+                "bf16_transpose_multi: contiguous bf16 [C, R] destinations");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(y.data_ptr()) & 15) == 0,
+                "bf16_transpose_multi: 16-B aligned operands");
+    s.push_back(x.data_ptr());
+    d.push_back(y.data_ptr());
+    R.push_back((int)x.size(0));
+    C.push_back((int)x.size(1));
+  }
+  check_rc(rtdc_bf16_transpose_multi(s.data(), d.data(), R.data(), C.data(), (int)s.size(), jobs.data_ptr(),
+                                     cur_stream()),
+           "bf16_transpose_multi");
 }
 static void f32_to_bf16_t(Tensor x, Tensor y) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.scalar_type() == at::kFloat && x.is_contiguous(),
@@ -978,6 +1008,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("nesterov"), py::arg("first"), py::arg("grad_scale"), py::arg("skip_ptr") = 0);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("f32_to_bf16_t", &f32_to_bf16_t);
+  m.def("bf16_transpose_multi", &bf16_transpose_multi);
+  m.def("bf16_transpose_jobs_bytes", &rtdc_bf16_transpose_jobs_bytes);
   m.def("sumsq", &sumsq);
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);

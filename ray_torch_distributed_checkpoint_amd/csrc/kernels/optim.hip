@@ -260,6 +260,84 @@ extern "C" int rtdc_f32_to_bf16_t(const float* x, void* y, int R, int C, hipStre
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// ---- batched bf16 transpose: dst[c][r] = src[r][c] for up to kTMaxJobs row-major [R][C]
+// matrices in one launch (the K-major images of a model's weights, ops/shadow.py
+// kmajor_refresh).  Block = one 64x64 tile of one job: 16-B loads of 8 rows x 8 columns per
+// pass into an LDS tile padded by one 16-B chunk per row, 16-B stores of 8 consecutive output
+// columns gathered from one LDS column.  Requires R % 8 == 0 and C % 8 == 0.
+typedef __attribute__((ext_vector_type(4))) unsigned int tu32x4;
+constexpr int kTMaxJobs = 96;
+struct TJobs {
+  const bf16_t* src[kTMaxJobs];
+  bf16_t* dst[kTMaxJobs];
+  int R[kTMaxJobs], C[kTMaxJobs];
+  int start[kTMaxJobs + 1];  // first tile of each job (prefix sums)
+  int n;
+};
+
+__global__ __launch_bounds__(256) void bf16_transpose_multi_kernel(const TJobs* __restrict__ jobs) {
+  __shared__ __attribute__((aligned(16))) bf16_t t[64][72];
+  const int b = blockIdx.x;
+  int j = 0;
+  {  // job of this tile: the last job whose start <= b (n <= 96: a short scalar scan)
+    const int n = jobs->n;
+    for (int i = 1; i < n; ++i) j = jobs->start[i] <= b ? i : j;
+  }
+  const int R = jobs->R[j], C = jobs->C[j];
+  const int tiles_c = (C + 63) / 64;
+  const int tile = b - jobs->start[j];
+  const int r0 = (tile / tiles_c) * 64, c0 = (tile % tiles_c) * 64;
+  const bf16_t* src = jobs->src[j];
+  bf16_t* dst = jobs->dst[j];
+  const int tid = threadIdx.x;
+  // load: thread -> (row tid / 8 + 32 p, 8 columns at 8 * (tid % 8))
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int rr = tid / 8 + 32 * p, cc = 8 * (tid % 8);
+    tu32x4 v = {0u, 0u, 0u, 0u};
+    if (r0 + rr < R && c0 + cc < C) v = *(const tu32x4*)(src + (long long)(r0 + rr) * C + c0 + cc);
+    *(tu32x4*)&t[rr][cc] = v;
+  }
+  __syncthreads();
+  // store: thread -> (output row = input column tid / 8 + 32 p, 8 output columns = input rows)
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int oc = tid / 8 + 32 * p, orr = 8 * (tid % 8);
+    if (c0 + oc >= C || r0 + orr >= R) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] = (uint32_t)t[orr + 2 * e][oc] | ((uint32_t)t[orr + 2 * e + 1][oc] << 16);
+    *(tu32x4*)(dst + (long long)(c0 + oc) * R + r0 + orr) = tu32x4{w[0], w[1], w[2], w[3]};
+  }
+}
+
+extern "C" int rtdc_bf16_transpose_multi(const void* const* src, void* const* dst, const int* R, const int* C, int n,
+                                         void* jobs_dev, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > kTMaxJobs) return 1;
+  TJobs h{};
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    if (R[i] % 8 || C[i] % 8) return 1;
+    h.src[i] = (const bf16_t*)src[i];
+    h.dst[i] = (bf16_t*)dst[i];
+    h.R[i] = R[i];
+    h.C[i] = C[i];
+    h.start[i] = tiles;
+    tiles += ((R[i] + 63) / 64) * ((C[i] + 63) / 64);
+  }
+  h.start[n] = tiles;
+  h.n = n;
+  // the table goes to device memory ahead of the kernel on the same stream (larger than the
+  // kernel-argument segment)
+  if (hipMemcpyAsync(jobs_dev, &h, sizeof(TJobs), hipMemcpyHostToDevice, st) != hipSuccess) return 2;
+  hipLaunchKernelGGL(bf16_transpose_multi_kernel, dim3((unsigned)tiles), dim3(256), 0, st, (const TJobs*)jobs_dev);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int rtdc_bf16_transpose_jobs_bytes() { return (int)sizeof(TJobs); }
+
 extern "C" int rtdc_sumsq(const void* chunks, int nchunks, const float* g, float* partial, hipStream_t st) {
   if (nchunks <= 0) return 0;
   hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(nchunks)), dim3(256), 0, st, (const Chunk*)chunks,
