@@ -50,8 +50,9 @@ def bind_shadow(p: torch.Tensor, s: torch.Tensor) -> None:
 # it) and waited for by the backward GEMM that consumes it.  Worth its transposition
 # (6 B/element) only when the product is long in M: RTDC_DGRAD_KMAJOR = auto (token rows >=
 # 8192: GPT-2's 16k-row steps, not Llama-3-8B's 2k) | 1 | 0 (default).  Isolated, the K-major
-# dgrads run 3-11 % faster (at hipBLASLt's times); in the GPT-2 step the side-stream images cost
-# more than that (18.19 / 18.10 vs 17.85 / 17.79 ms, profiles/r6/dgrad_kmajor_ab_r6.txt).
+# dgrads run 3-11 % faster (at hipBLASLt's times); in the GPT-2 step they save ~190 us against a
+# 124 us batched transpose of the shadows - neutral within the run-to-run spread (17.02 vs
+# 16.99 ms, profiles/r6/dgrad_kmajor_ab_r6.txt).
 _KMAJOR = os.environ.get("RTDC_DGRAD_KMAJOR", "0")
 _GEN = [0]
 
@@ -69,24 +70,49 @@ def kmajor_wanted(w: torch.Tensor, rows: int) -> bool:
     return not torch.cuda.is_current_stream_capturing()
 
 
+_registry: list = []   # weakrefs of the parameters that have a K-major image
+_jobs: dict = {}       # device -> uint8 job-table buffer of the batched transpose
+
+
+def _stale(p) -> bool:
+    st = getattr(p, "_rtdc_kimg", None)
+    return st is None or st["gen"] != _GEN[0] or st["ver"] != p._version
+
+
 def kmajor_prefetch(w: torch.Tensor) -> None:
-    """Start building this step's [in, out] bf16 image of the fp32 master `w` on a side stream
-    (after everything the compute stream has queued, i.e. the last optimizer update)."""
-    st = getattr(w, "_rtdc_kimg", None)
-    if st is not None and st["gen"] == _GEN[0] and st["ver"] == w._version:
-        return
+    """Start building this step's [in, out] bf16 image of `w` on a side stream, after
+    everything the compute stream has queued (i.e. the last optimizer update).  Every other
+    registered weight whose image is stale is transposed in the same launch (one batched
+    transpose of the bf16 shadows per step, not one conversion per weight)."""
+    import weakref
+
     from .streams import side_stream
 
+    st = getattr(w, "_rtdc_kimg", None)
+    if st is not None and not _stale(w):
+        return
     if st is None:
-        st = {"img": torch.empty((w.shape[1], w.shape[0]), dtype=torch.bfloat16, device=w.device),
-              "ev": torch.cuda.Event()}
-        w._rtdc_kimg = st
+        w._rtdc_kimg = {"img": torch.empty((w.shape[1], w.shape[0]), dtype=torch.bfloat16, device=w.device),
+                        "gen": -1, "ver": -1, "ev": None}
+        _registry.append(weakref.ref(w))
+    live = [r() for r in _registry]
+    _registry[:] = [r for r, p in zip(_registry, live) if p is not None]
+    todo = [p for p in live if p is not None and p.device == w.device and _stale(p)]
+    srcs = [shadow_of(p) for p in todo]  # (on the compute stream: refreshed there if stale)
+    cur = torch.cuda.current_stream(w.device)
     side = side_stream(w.device, "wgrad")
-    side.wait_stream(torch.cuda.current_stream(w.device))
+    side.wait_stream(cur)
+    jb = _jobs.get(w.device)
+    if jb is None:
+        jb = _jobs[w.device] = torch.empty(gpu_ext().bf16_transpose_jobs_bytes(), dtype=torch.uint8, device=w.device)
+    ev = torch.cuda.Event()
     with torch.cuda.stream(side):
-        gpu_ext().f32_to_bf16_t(w.detach(), st["img"])
-        st["ev"].record(side)
-    st["gen"], st["ver"] = _GEN[0], w._version
+        for i in range(0, len(todo), 96):
+            gpu_ext().bf16_transpose_multi(srcs[i:i + 96], [p._rtdc_kimg["img"] for p in todo[i:i + 96]], jb)
+        ev.record(side)
+    for p, s_ in zip(todo, srcs):
+        s_.record_stream(side)
+        p._rtdc_kimg.update(gen=_GEN[0], ver=p._version, ev=ev)
 
 
 def kmajor_image(w: torch.Tensor) -> torch.Tensor:

@@ -91,3 +91,19 @@ def test_gpt2_backward_with_kmajor_images_matches(kmajor):
         g1 = grads["1"][n]
         err = (g1 - g0).norm() / max(g0.norm().item(), 1e-12)
         assert err < 2e-2, (n, float(err))
+
+
+def test_bf16_transpose_multi_matches_torch():
+    """The batched transpose behind the K-major images: several matrices (ragged edges, R and C
+    multiples of 8) in one launch, bitwise torch's transpose."""
+    from ray_torch_distributed_checkpoint_amd.ops._ext import gpu_ext
+
+    torch.manual_seed(7)
+    shapes = [(2304, 768), (768, 3072), (50304, 768), (72, 136), (8, 8), (1000, 24)]
+    src = [torch.randn(r, c, device="cuda").bfloat16() for r, c in shapes]
+    dst = [torch.empty(c, r, device="cuda", dtype=torch.bfloat16) for r, c in shapes]
+    jobs = torch.empty(gpu_ext().bf16_transpose_jobs_bytes(), dtype=torch.uint8, device="cuda")
+    gpu_ext().bf16_transpose_multi(src, dst, jobs)
+    torch.cuda.synchronize()
+    for s, d in zip(src, dst):
+        assert torch.equal(d, s.t().contiguous())
