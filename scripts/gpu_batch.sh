@@ -12,6 +12,6 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 3 "gpurun_out/$name.log"
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step resume_test 300 python -u -m pytest tests/test_resume_fullsize_gpu.py -v -s --timeout 240 --timeout-method thread
-step gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
-step product 1100 python3 scripts/product_path.py gpurun_out/product
+step kmaj_tests 300 python -u -m pytest tests/test_kmajor_gpu.py tests/test_kernels_gpu.py -m gpu -k "kmajor or transpose" -v --timeout 200 --timeout-method thread
+bash scripts/gpu.sh envab ENVA="RTDC_DGRAD_KMAJOR=0" ENVB="RTDC_DGRAD_KMAJOR=auto" ROUNDS=3 TAG=kmajor2
+RTDC_DGRAD_KMAJOR=auto step prof_kmaj2 700 bash scripts/gpu.sh prof STEPS=10 TAG=gpt2_kmaj2
