@@ -82,10 +82,19 @@ def test_flat_param_space_views():
     ps = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(70))]
     vals = [p.detach().clone() for p in ps]
     sp = FlatParamSpace(ps)
+    # a space built while a parameter holds a gradient keeps the accumulate views
+    q = [torch.nn.Parameter(torch.randn(4)), torch.nn.Parameter(torch.randn(6))]
+    q[0].grad = torch.ones(4)
+    sq = FlatParamSpace(q)
+    assert not sq.fresh and all(p.grad is not None and p.grad.data_ptr() == sq.grad.data_ptr() + 4 * s.offset
+                                for p, s in zip(q, sq.segments))
     assert sp.numel == 128 + 64  # 64-element aligned segments
     for p, v, s in zip(ps, vals, sp.segments):
         assert torch.equal(p, v) and p.data_ptr() == sp.data.data_ptr() + 4 * s.offset
-        assert p.grad is not None and p.grad.data_ptr() == sp.grad.data_ptr() + 4 * s.offset
+        # built before any backward: the per-step fresh-gradient mode (p.grad None; the first
+        # contribution lands in the slice), as after zero_grad(set_to_none=True)
+        assert p.grad is None and sp.fresh
+        assert sp.grad_view(p).data_ptr() == sp.grad.data_ptr() + 4 * s.offset
     rows, n = sp.chunk_table(ps, [True, False])
     assert n == 2 and int(rows[0, 1]) >> 32 == 1 and int(rows[1, 1]) >> 32 == 0
 
