@@ -45,6 +45,9 @@ def main():
     r["ours_fwd_us"] = round(timeit(ours_fwd), 1)
     r["ours_fwd_TBps"] = round(2 * nb / r["ours_fwd_us"] / 1e6, 2)
     r["aten_fwd_us"] = round(timeit(aten_fwd), 1)
+    ref = F.layer_norm(x.float(), (D,), w, b)
+    r["ours_fwd_max_err"] = float((ours_fwd().float() - ref).abs().max())
+    r["RTDC_NORM_FWD2R"] = os.environ.get("RTDC_NORM_FWD2R", "0")
     print(json.dumps(r), flush=True)
 
     # backward at the GPT-2 form (residual-stream gradient added in the kernel, column sums of

@@ -94,6 +94,83 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
+// Two rows per wave with full 16-B lanes where one row's D / 8 chunks are 64k + 32 (GPT-2's
+// D = 768: 96 chunks, so the one-row form leaves half the lanes idle on its second load): the
+// 2 (64k + 32) chunks of a row pair are NPL = 2k + 1 per lane, chunk q = lane + 64 i of the pair
+// belongs to row q / nch.  Same per-row math as norm_fwd_kernel; the second row's chunks sit
+// on other lanes, so its wave reductions add the partials in another order (last-bit
+// differences in mean / rstd).
+template <int NPL, bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd2r_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
+                                                         const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                         int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2;  // rows r0, r0 + 1
+  if (r0 >= M) return;
+  const int nch = D >> 3;
+  const bool two = r0 + 1 < M;
+  const bf16_t* xr = x + (long long)r0 * D;  // the pair is contiguous: chunk q at xr + 8 q
+  float v[NPL][8];
+  float s[2] = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int q = lane + 64 * i;
+    const int rr = q >= nch ? 1 : 0;
+    if (rr == 0 || two) {
+      ld8(xr + q * 8, v[i]);
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t += v[i][e];
+      s[rr] += t;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    }
+  }
+  float mean[2] = {0.f, 0.f};
+  if (!RMS) {
+    mean[0] = wave_sum(s[0]) / D;
+    mean[1] = wave_sum(s[1]) / D;
+  }
+  float ss[2] = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int q = lane + 64 * i;
+    const int rr = q >= nch ? 1 : 0;
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[i][e] - mean[rr];
+      t += d * d;
+    }
+    ss[rr] += t;
+  }
+  const float rstd[2] = {rsqrtf(wave_sum(ss[0]) / D + eps), rsqrtf(wave_sum(ss[1]) / D + eps)};
+  if (lane == 0) {
+    if (mean_out) mean_out[r0] = mean[0];
+    rstd_out[r0] = rstd[0];
+    if (two) {
+      if (mean_out) mean_out[r0 + 1] = mean[1];
+      rstd_out[r0 + 1] = rstd[1];
+    }
+  }
+  bf16_t* yr = y + (long long)r0 * D;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int q = lane + 64 * i;
+    const int rr = q >= nch ? 1 : 0;
+    if (rr == 1 && !two) continue;
+    const int c = q - rr * nch;
+    float gg[8], bb[8], o[8];
+    ld8(g + c * 8, gg);
+    if (!RMS) ld8(b + c * 8, bb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean[rr]) * rstd[rr] * gg[e] + (RMS ? 0.f : bb[e]);
+    st8(yr + q * 8, o);
+  }
+}
+
 // dxhat = dy*g ; dx = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat*xhat))   (LayerNorm)
 // dx = rstd * (dxhat - xhat * mean(dxhat*xhat))                                  (RMSNorm)
 // CS: also the column sums of dx itself (the residual-stream gradient this kernel produces is
@@ -694,6 +771,25 @@ static int launch_norm_fwd(const void* x, const void* g, const void* b, void* y,
     else if (cpl4 == 3) L4(3);
     else L4(4);
 #undef L4
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
+  // RTDC_NORM_FWD2R=1: two rows per wave where a row's 16-B chunks are 64k + 32 (A/B)
+  static int fwd2r = -1;
+  if (fwd2r < 0) {
+    const char* e = getenv("RTDC_NORM_FWD2R");
+    fwd2r = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (fwd2r && (D / 8) % 64 == 32 && (D / 8) <= 224) {
+    const int npl = (2 * (D / 8)) / 64;
+    dim3 grid2((M + 7) / 8), block2(256);
+#define L2(C)                                                                                 \
+  hipLaunchKernelGGL((norm_fwd2r_kernel<C, RMS>), grid2, block2, 0, st, (const bf16_t*)x,      \
+                     (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, mean, rstd, M, D, eps)
+    if (npl == 1) L2(1);
+    else if (npl == 3) L2(3);
+    else if (npl == 5) L2(5);
+    else L2(7);
+#undef L2
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
   dim3 grid((M + 3) / 4), block(256);
