@@ -12,11 +12,4 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-RTDC_NORM_FWD2R=1 step ln2r_tests 300 python -u -m pytest tests -m gpu -k "norm or layer" -v --timeout 200 --timeout-method thread
-for r in 1 2; do
-  for v in 0 1; do
-    RTDC_NORM_FWD2R=$v step norm_bench_${v}_$r 200 python -u benchmarks/norm_bench.py
-    grep '"ours_fwd_us"' gpurun_out/norm_bench_${v}_$r.log | cut -c1-200
-  done
-done
-bash scripts/gpu.sh envab ENVA="RTDC_NORM_FWD2R=0" ENVB="RTDC_NORM_FWD2R=1" ROUNDS=3 TAG=ln2r
+step llama_sweep 900 python -u benchmarks/gemm_bench.py --set llama --sweep --cfgs 0,6,7,11,12,13 --layouts fwd,dgrad,wgrad --reps 10
