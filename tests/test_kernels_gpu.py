@@ -810,6 +810,35 @@ def test_gemm_persistent_epilogues():
         _close(y2, pre_ref + res.float(), 1e-2)
 
 
+@pytest.mark.parametrize("cfg", [6, 7, 8, 9, 12])
+def test_gemm_epilogue_input_combinations(cfg):
+    """The 8-wave / 4-wave / persistent epilogues' optional inputs: bias (fp32 or bf16) and
+    residual, each alone and combined, and an input-gradient activation WITH a residual, on
+    partial tiles against fp32 torch."""
+    from ray_torch_distributed_checkpoint_amd.ops import gemm as G
+
+    torch.manual_seed(41 + cfg)
+    M, N, K = 1800, 1152, 768
+    x, w = _bf(M, K), _bf(N, K, scale=0.05)
+    base = x.float() @ w.float().t()
+    res = _bf(M, N)
+    for bias in (None, torch.randn(N, device=DEV), torch.randn(N, device=DEV).bfloat16()):
+        bf = 0.0 if bias is None else bias.float()
+        for r in (None, res):
+            y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+            G.gemm_bf16(x, w, y, M, N, K, K, K, N, True, True, bias=bias, Cin=r, beta=0.0 if r is None else 0.5,
+                        tile_cfg=cfg)
+            _close(y, base + bf + (0.0 if r is None else 0.5 * res.float()), 1e-2)
+    if cfg in (6, 7):  # dgrad layout with GELU' and a residual
+        dy, w2, pre = _bf(M, K), _bf(K, N, scale=0.05), _bf(M, N)
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        G.gemm_bf16(dy, w2, out, M, N, K, K, N, N, True, False, aux_in=pre, act=G.ACT_GELU_BWD, Cin=res, beta=1.0,
+                    tile_cfg=cfg)
+        hf = pre.float().requires_grad_(True)
+        (gd,) = torch.autograd.grad(F.gelu(hf, approximate="tanh").sum(), hf)
+        _close(out, (dy.float() @ w2.float() + res.float()) * gd, 1e-2)
+
+
 def test_gemm_persistent_auto_matches_plain(monkeypatch):
     """The automatic persistent dispatch (RTDC_GEMM_PERSIST, default on) is bitwise identical
     to the per-tile launch: same tiles, same MFMA order, only the schedule differs."""
