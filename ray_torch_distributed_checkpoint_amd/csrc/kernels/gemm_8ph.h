@@ -116,6 +116,14 @@ __device__ __forceinline__ typename Frag<KMAJOR>::T load_frag96(const char* tile
 #define RTDC_EPI_W 2
 #endif
 
+// s_waitcnt vmcnt(0) lgkmcnt(0) as the builtin, which the compiler's wait insertion reads (asm
+// waits it cannot).  hipcc treats a global_load_lds (a FLAT instruction, counted in vmcnt AND
+// lgkmcnt) as pending until a wait it sees clears both counters, and while one is pending every
+// wait it inserts is vmcnt(0): each activation-input read of the epilogue waited for all the
+// stores issued before it (small-kernel check: after a glds, the builtin vmcnt(0) alone keeps
+// later waits at 0; vmcnt(0) lgkmcnt(0) makes them counted; profiles/r6/gemm_epilogue_counted_waits_ab_r6.txt).
+__device__ __forceinline__ void vm_drained() { __builtin_amdgcn_s_waitcnt(0x0070); }
+
 template <int ACT, int TMQ, int TNQ, int SA, int SB, int BH, bool ZERO>
 __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
                                                    int wa, int wb, int lane, float alpha) {
@@ -124,9 +132,10 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
   // 256 rows x ldc x 2 B under 2 GiB)
   const long long tile_off = (long long)m0 * a.ldc * 2, rows_bytes = (long long)(a.M - m0) * a.ldc * 2;
   const auto rC = make_rsrc(a.C, tile_off, rows_bytes);
-  const bool has_cin = a.Cin && a.beta != 0.f;
+  // (an input-gradient activation takes no residual here: the launcher routes that combination
+  // to the general kernel, so the ACT_IN epilogue has no conditional load)
+  const bool has_cin = !ACT_IN && a.Cin && a.beta != 0.f;
   const auto rIn = make_rsrc(ACT_IN ? (const void*)a.aux_in : a.Cin, tile_off, (ACT_IN || has_cin) ? rows_bytes : 0);
-  const auto rCin = make_rsrc(a.Cin, tile_off, (ACT_IN && has_cin) ? rows_bytes : 0);
   const auto rAux = make_rsrc(a.aux_out, tile_off, (ACT == 2 || ACT == 5) ? rows_bytes : 0);
   const int bias_elt = a.bias_type == 2 ? 4 : 2;
   const auto rBias = make_rsrc(a.bias, 0, a.bias_type ? (long long)a.N * bias_elt : 0);
@@ -199,12 +208,6 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
     float x[8];
     if constexpr (ACT_IN) {
       unpack8bf(xin[P], x);
-      if (has_cin) {  // (not produced by the models; kept for the GEMM contract)
-        float c[8];
-        unpack8bf(buf_load16(rCin, off), c);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] += a.beta * c[r];
-      }
     } else if (has_cin) {
       unpack8bf(xin[P], x);
 #pragma unroll
@@ -258,6 +261,10 @@ __device__ __forceinline__ void tile_epilogue_bf16(const GemmArgs& a, f32x4 (&ac
 template <typename OutT, int TMQ, int TNQ, int SA, int SB, int BH, bool ZERO>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& a, f32x4 (&acc)[2][2][TMQ][TNQ], int m0, int n0,
                                               int wa, int wb, int lane, float alpha) {
+  // this block's operand DMA has landed (non-persistent: the last K-tile's asm waits;
+  // persistent: A-lo(g+2) is still in flight and this retires it, as the epilogue's first load
+  // wait would - vmcnt is in order) - said in a wait hipcc sees
+  vm_drained();
   if constexpr (std::is_same_v<OutT, bf16_t>) {
     switch (a.act) {
       case 1: tile_epilogue_bf16<1, TMQ, TNQ, SA, SB, BH, ZERO>(a, acc, m0, n0, wa, wb, lane, alpha); break;

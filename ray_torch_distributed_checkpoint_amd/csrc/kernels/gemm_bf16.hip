@@ -814,6 +814,9 @@ extern "C" int rtdc_gemm_bf16(const GemmArgs* args, int a_kmajor, int b_kmajor, 
   const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.Cin | (uintptr_t)a.aux_in | (uintptr_t)a.aux_out |
                        (uintptr_t)a.bias;
   if (cfg >= 6 && cfg <= 13 && !out_fp32 && ((al & 15) != 0 || (a.ldc & 7) != 0 || a.ldc >= (1 << 22))) cfg = 0;
+  // ... and take no residual with an input-gradient activation (their epilogue then has no
+  // conditional load; the models never ask for this combination)
+  if (cfg >= 6 && cfg <= 13 && (a.act == 3 || a.act == 4 || a.act == 6) && a.Cin && a.beta != 0.f) cfg = 0;
   a.splitk = 1;
   // split-K when the output tiles cannot fill the chip and K is long (weight gradients)
   const bool plain = a.act == 0 && a.bias_type == 0 && a.causal == 0 && batch == 1;
