@@ -718,6 +718,12 @@ static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, doub
 //   256x256  1.74 (1.58 persistent, > 256 tiles)   256x192  1.42 fwd / 1.37 dgrad
 //   256x128  1.10 fwd / 1.16 dgrad
 // Returns the cfg (6 / 7 / 11), or -1 when the product is outside this regime.
+// RTDC_GEMM_FEW_ROWS_X=0 drops pick_cfg_few_rows' measured exceptions (A/B)
+static bool few_rows_exceptions() {
+  const char* e = getenv("RTDC_GEMM_FEW_ROWS_X");
+  return !(e && e[0] == '0');
+}
+
 static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
   const int kt = a.K / gemm::BK, tm = (a.M + 255) / 256;
   const double slab_us = (double)a.M * a.N * 8.0 / 4.0e6;
@@ -733,6 +739,17 @@ static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
     return best;
   };
   const long long t6 = (long long)tm * ((a.N + 255) / 256);
+  // Measured exceptions to the model (Llama-3-8B at 2048 tokens, gemm_bench --sweep,
+  // profiles/r6/llama_few_rows_cfg_r6.txt):
+  //  * one partial round of 256x256 tiles on the forward layout (qkv: 192 tiles, K = 4096): the
+  //    one-barrier 8-wave kernel runs at ~1.25 us per K-tile there - 1287 TF vs 1145 at 256x192;
+  //  * at most half a round (o-proj: 128 tiles, K = 4096, both layouts): 128x128 tiles with two
+  //    blocks per CU - 1052 / 1015 TF vs 958 / 930 at 256x128 (not past K = 4096: the down
+  //    projection's K = 14336 forward loses on them, 1164 vs 1280).
+  if (few_rows_exceptions()) {
+    if (b_kmajor && t6 > 128 && t6 <= 256 && gemm4b_mode() != 0) return 13;
+    if (t6 <= 128 && a.K <= 4096) return 0;
+  }
   const double e6 = est(256, b_kmajor && t6 > 256 ? 1.58 : 1.74);
   const double e7 = (b_kmajor || a.K <= 4096) ? est(192, b_kmajor ? 1.42 : 1.37) : 1e30;
   const double e11 = est(128, b_kmajor ? 1.10 : 1.16);

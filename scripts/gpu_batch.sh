@@ -12,9 +12,7 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-L=fwd,fwd_bias_gelu,dgrad_gelu_cs_kmaj
 step kt 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm or linear or mlp" --timeout 120 --timeout-method thread
-step gemm_new 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_old 400 env RTDC_EXT_SO=$PWD/abv/_C_old.so python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_new2 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-bash scripts/gpu.sh ab TAG=s32 ROUNDS=3 STEPS=30
+step gemm_llama 400 python -u benchmarks/gemm_bench.py --set llama --layouts fwd,dgrad --reps 10
+step gemm_llama_x0 400 env RTDC_GEMM_FEW_ROWS_X=0 python -u benchmarks/gemm_bench.py --set llama --layouts fwd,dgrad --reps 10
+bash scripts/gpu.sh envab MODEL=llama3-8b TAG=fewx STEPS=10 WARMUP=3 ROUNDS=2 ENVA=RTDC_GEMM_FEW_ROWS_X=0 ENVB=RTDC_GEMM_FEW_ROWS_X=1
