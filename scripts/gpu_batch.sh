@@ -12,7 +12,9 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step kt 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm or linear or mlp" --timeout 120 --timeout-method thread
-step gemm_llama 400 python -u benchmarks/gemm_bench.py --set llama --layouts fwd,dgrad --reps 10
-step gemm_llama_x0 400 env RTDC_GEMM_FEW_ROWS_X=0 python -u benchmarks/gemm_bench.py --set llama --layouts fwd,dgrad --reps 10
-bash scripts/gpu.sh envab MODEL=llama3-8b TAG=fewx STEPS=10 WARMUP=3 ROUNDS=2 ENVA=RTDC_GEMM_FEW_ROWS_X=0 ENVB=RTDC_GEMM_FEW_ROWS_X=1
+step final_gpu_tests 600 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread
+step final_smoke 240 python -c 'import __graft_entry__ as g; g.smoke()'
+step final_bench_gpt2_1 500 python bench.py
+step final_bench_gpt2_2 500 python bench.py
+bash scripts/gpu.sh prof TAG=gpt2_final STEPS=10 WARMUP=3
+bash scripts/gpu.sh pmc TAG=gpt2_final
