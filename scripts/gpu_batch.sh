@@ -12,9 +12,5 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step final_gpu_tests 600 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread
-step final_smoke 240 python -c 'import __graft_entry__ as g; g.smoke()'
-step final_bench_gpt2_1 500 python bench.py
-step final_bench_gpt2_2 500 python bench.py
-bash scripts/gpu.sh prof TAG=gpt2_final STEPS=10 WARMUP=3
-bash scripts/gpu.sh pmc TAG=gpt2_final
+step final2_bench_resnet18 500 python bench.py --model resnet18
+step final2_bench_llama 600 python bench.py --model llama3-8b
