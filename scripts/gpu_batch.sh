@@ -12,5 +12,10 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step final2_bench_resnet18 500 python bench.py --model resnet18
-step final2_bench_llama 600 python bench.py --model llama3-8b
+L=fwd,fwd_bias_gelu,dgrad_gelu_cs_kmaj
+step kt 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm or linear or mlp" --timeout 120 --timeout-method thread
+step gemm_new 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+step gemm_old 400 env RTDC_EXT_SO=$PWD/abv/_C_old.so python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+step gemm_new2 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+step gemm_old2 400 env RTDC_EXT_SO=$PWD/abv/_C_old.so python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+bash scripts/gpu.sh ab TAG=pro ROUNDS=3 STEPS=30
