@@ -12,10 +12,12 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-L=fwd,fwd_bias_gelu,dgrad_gelu_cs_kmaj
-step kt 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm or linear or mlp" --timeout 120 --timeout-method thread
-step gemm_new 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_old 400 env RTDC_EXT_SO=$PWD/abv/_C_old.so python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_new2 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_old2 400 env RTDC_EXT_SO=$PWD/abv/_C_old.so python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-bash scripts/gpu.sh ab TAG=pro ROUNDS=3 STEPS=30
+L=fwd_bias_res,fwd_bias_gelu,dgrad_gelu_cs
+W4=$PWD/abv/_C_w4.so
+step kt_w4 600 env RTDC_EXT_SO=$W4 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm or linear or mlp" --timeout 120 --timeout-method thread
+step gemm_w4 400 env RTDC_EXT_SO=$W4 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+step gemm_head 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+step gemm_w4b 400 env RTDC_EXT_SO=$W4 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+step gemm_headb 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
+bash scripts/gpu.sh envab TAG=w4 ROUNDS=3 STEPS=30 ENVA=RTDC_GELU_SAVE_GRAD=0 ENVB=RTDC_EXT_SO=$W4
+bash scripts/gpu.sh envab TAG=gsg ROUNDS=3 STEPS=30 ENVA=RTDC_GELU_SAVE_GRAD=0 ENVB=RTDC_GELU_SAVE_GRAD=1
