@@ -72,6 +72,20 @@ def main():
         t_kf = min(timeit(lambda: ext.flash_fwd(q_, o_, lse, B, T, H, Hkv, Dh, scale), args.reps) for _ in range(3))
         t_kb = min(timeit(lambda: ext.flash_bwd(q_, o_, dyc, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, None), args.reps)
                    for _ in range(3))
+        # the same backward with delta first and the dQ / dK/dV passes on two streams
+        # (ops/attention.py RTDC_FA_CONCURRENT)
+        side = torch.cuda.Stream()
+
+        def conc():
+            ext.flash_delta(o_, dyc, delta, B, T, H, Dh)
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                ext.flash_bwd(q_, o_, dyc, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, None, which=2, delta_ready=True)
+            ext.flash_bwd(q_, o_, dyc, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, None, which=1, delta_ready=True)
+            cur.wait_stream(side)
+
+        t_kc = min(timeit(conc, args.reps) for _ in range(3))
         q = qkv.detach()[..., : H * Dh].view(B, T, H, Dh).transpose(1, 2).contiguous().requires_grad_(True)
         k = qkv.detach()[..., H * Dh:(H + Hkv) * Dh].view(B, T, Hkv, Dh).transpose(1, 2)
         v = qkv.detach()[..., (H + Hkv) * Dh:].view(B, T, Hkv, Dh).transpose(1, 2)
@@ -91,6 +105,7 @@ def main():
                           "kernel_fwd_us": round(t_kf * 1e6, 1), "kernel_fwd_TF": round(flops_f / t_kf / 1e12, 1),
                           "kernel_bwd_us": round(t_kb * 1e6, 1),
                           "kernel_bwd_TF": round(2.5 * flops_f / t_kb / 1e12, 1),
+                          "kernel_bwd_concurrent_us": round(t_kc * 1e6, 1),
                           "sdpa_fwd_us": round(t_sf * 1e6, 1), "sdpa_fwd_TF": round(flops_f / t_sf / 1e12, 1),
                           "sdpa_bwd_us": round((t_sfb - t_sf) * 1e6, 1)}), flush=True)
 

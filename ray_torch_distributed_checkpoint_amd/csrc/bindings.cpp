@@ -105,8 +105,9 @@ int rtdc_maxpool(const void* x, void* y, void* arg, const void* dy, void* dx, in
                  int K, int s, int p, int backward, hipStream_t st);
 int rtdc_avgpool(const void* x, void* y, int B, int HW, int C, int backward, hipStream_t st);
 int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
-                   int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws, float* part, int qs,
-                   hipStream_t st);
+                   int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws, float* part, int qs, int which,
+                   int delta_ready, hipStream_t st);
+int rtdc_flash_delta(const void* out, const void* dout, float* delta, int B, int T, int H, int Dh, hipStream_t st);
 }
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -520,7 +521,7 @@ static void flash_fwd(Tensor qkv, Tensor out, Tensor lse, int64_t B, int64_t T, 
 // cs_ws (optional fp32 [B*T/16][W], W = (H + 2 Hkv) Dh): per 16-row group column sums of dqkv
 static void flash_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor delta, Tensor dqkv, int64_t B, int64_t T,
                       int64_t H, int64_t Hkv, int64_t Dh, double scale, c10::optional<Tensor> cs_ws,
-                      c10::optional<Tensor> part, int64_t qs) {
+                      c10::optional<Tensor> part, int64_t qs, int64_t which, bool delta_ready) {
   TORCH_CHECK(dout.is_contiguous() && dqkv.is_contiguous(), "flash_bwd: contiguous tensors expected");
   TORCH_CHECK(qs >= 1 && (H / Hkv) % qs == 0, "flash_bwd: qs must divide the GQA group size");
   if (qs > 1)
@@ -534,8 +535,18 @@ static void flash_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor de
   check_rc(rtdc_flash_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                           delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)T, (int)H, (int)Hkv, (int)Dh,
                           (float)scale, cs_ws.has_value() ? cs_ws->data_ptr<float>() : nullptr,
-                          qs > 1 ? part->data_ptr<float>() : nullptr, (int)qs, cur_stream()),
+                          qs > 1 ? part->data_ptr<float>() : nullptr, (int)qs, (int)which, delta_ready ? 1 : 0,
+                          cur_stream()),
            "flash_bwd");
+}
+// delta[B*H][T] = rowsum(dO * O) on its own (then flash_bwd(..., which=1|2, delta_ready=True))
+static void flash_delta(Tensor out, Tensor dout, Tensor delta, int64_t B, int64_t T, int64_t H, int64_t Dh) {
+  TORCH_CHECK(out.is_contiguous() && dout.is_contiguous() && delta.is_contiguous() &&
+                  delta.scalar_type() == at::kFloat && delta.numel() >= B * H * T,
+              "flash_delta: contiguous out / dout and fp32 delta [B*H][T] expected");
+  check_rc(rtdc_flash_delta(out.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), (int)B, (int)T, (int)H, (int)Dh,
+                            cur_stream()),
+           "flash_delta");
 }
 
 // ---------------------------------------------------------------------------------- llama ops
@@ -1024,7 +1035,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_bwd", &flash_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("delta"),
         py::arg("dqkv"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("Hkv"), py::arg("Dh"), py::arg("scale"),
-        py::arg("cs_ws") = py::none(), py::arg("part") = py::none(), py::arg("qs") = 1);
+        py::arg("cs_ws") = py::none(), py::arg("part") = py::none(), py::arg("qs") = 1, py::arg("which") = 3,
+        py::arg("delta_ready") = false);
+  m.def("flash_delta", &flash_delta);
   m.def("rope", &rope);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);

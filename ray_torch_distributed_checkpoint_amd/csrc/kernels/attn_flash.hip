@@ -68,6 +68,9 @@ struct Args {
   // part [qs][B*T][Hkv][2*Dh]; dkdv_reduce_kernel sums them in qsub order (deterministic)
   float* part;
   int qs;
+  // delta already in `delta` (delta_kernel ran first): the dQ kernels compute their own copy for
+  // their rows but do not store it - dK/dV may be reading it concurrently (rtdc_flash_bwd `which`)
+  int delta_ready;
 };
 
 // column sums over a wave's 16 rows of its stored fragment values v (lane = row (lane & 15) x
@@ -1132,7 +1135,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(Args a) {
     for (int e = 0; e < 8; ++e)
       dsum = fmaf(bf2f((bf16_t)of[ks][e]), bf2f((bf16_t)ofw[ks][e]), dsum);
   const float del = sum_rows4(dsum);
-  if (g == 0) a.delta[r] = del;
+  if (g == 0 && !a.delta_ready) a.delta[r] = del;
   step_barrier();
 
   f32x4 dq[DT];
@@ -1273,7 +1276,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq2_kernel(Args a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f((bf16_t)of[qg][ks][e]), bf2f((bf16_t)ofw[qg][ks][e]), dsum);
     del[qg] = sum_rows4(dsum);
-    if (g == 0) a.delta[(long long)bh * a.T + myq[qg]] = del[qg];
+    if (g == 0 && !a.delta_ready) a.delta[(long long)bh * a.T + myq[qg]] = del[qg];
   }
   step_barrier();
 
@@ -1437,9 +1440,27 @@ extern "C" int rtdc_flash_fwd(const void* qkv, void* out, float* lse, int B, int
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// delta[b][h][t] = rowsum(dO * O) alone (before dQ and dK/dV run concurrently on two streams)
+extern "C" int rtdc_flash_delta(const void* out, const void* dout, float* delta, int B, int T, int H, int Dh,
+                                hipStream_t st) {
+  if (Dh != 64 && Dh != 128) return 1;
+  const long long threads = (long long)B * T * H * (Dh / 8);
+  dim3 grid((unsigned)((threads + 255) / 256));
+  if (Dh == 64)
+    hipLaunchKernelGGL(fa::delta_kernel<64>, grid, dim3(256), 0, st, (const bf16_t*)out, (const bf16_t*)dout, delta, B,
+                       T, H);
+  else
+    hipLaunchKernelGGL(fa::delta_kernel<128>, grid, dim3(256), 0, st, (const bf16_t*)out, (const bf16_t*)dout, delta,
+                       B, T, H);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// which: bit 0 the dQ pass (it also stores delta unless delta_ready), bit 1 the dK/dV pass (+ the
+// GQA head-split reduction).  Both bits: dQ then dK/dV on `st`.  One bit with delta_ready lets the
+// caller run the two passes on two streams (ops/attention.py).
 extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
                               void* dqkv, int B, int T, int H, int Hkv, int Dh, float scale, float* cs_ws,
-                              float* part, int qs, hipStream_t st) {
+                              float* part, int qs, int which, int delta_ready, hipStream_t st) {
   if (T % 64 != 0 || (Dh != 64 && Dh != 128) || H % Hkv != 0) return 1;
   if (qs < 1 || (H / Hkv) % qs != 0 || (qs > 1 && part == nullptr) || ((Hkv * 2 * Dh) % 4) != 0) return 1;
   // dQ first: it also computes the row terms delta = rowsum(dO * O) that dK/dV read
@@ -1449,7 +1470,9 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   a.dqkv = (bf16_t*)dqkv;
   a.cs_ws = cs_ws;
   a.B = B; a.T = T; a.H = H; a.Hkv = Hkv; a.scale = scale; a.xcd_remap = fa_xcd(); a.diag = fa_diag();
-  a.part = part; a.qs = qs;
+  a.part = part; a.qs = qs; a.delta_ready = delta_ready;
+  if (which < 1 || which > 3 || (which != 3 && !delta_ready)) return 1;
+  const bool run_dq = which & 1, run_dkdv = which & 2;
   dim3 g1(T / 64, B * Hkv * qs), g2(T / 64, B * H);
   const int ns = fa_ns(Dh);
   // dK/dV at Dh = 64: 32 keys per wave (bwd_dkdv2_kernel) unless RTDC_FA_DKDV=1 (16 keys per wave)
@@ -1461,25 +1484,33 @@ extern "C" int rtdc_flash_bwd(const void* qkv, const void* out, const void* dout
   const bool dq2 = (dq_env ? atoi(dq_env) : 2) == 2 && T % 128 == 0;
   const dim3 g2b(T / 128, B * H);
   if (Dh == 64) {
-    if (dq2) FA_DISPATCH(fa::bwd_dq2_kernel, 64, ns, g2b, a);
-    else FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
-    if (dkdv_v == 2 && T % 128 == 0) {
-      dim3 g3(T / 128, B * Hkv * qs);
-      FA_DISPATCH(fa::bwd_dkdv2_kernel, 64, ns, g3, a);
-    } else {
-      FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
+    if (run_dq) {
+      if (dq2) FA_DISPATCH(fa::bwd_dq2_kernel, 64, ns, g2b, a);
+      else FA_DISPATCH(fa::bwd_dq_kernel, 64, ns, g2, a);
+    }
+    if (run_dkdv) {
+      if (dkdv_v == 2 && T % 128 == 0) {
+        dim3 g3(T / 128, B * Hkv * qs);
+        FA_DISPATCH(fa::bwd_dkdv2_kernel, 64, ns, g3, a);
+      } else {
+        FA_DISPATCH(fa::bwd_dkdv_kernel, 64, ns, g1, a);
+      }
     }
   } else {
-    if (dq2) FA_DISPATCH(fa::bwd_dq2_kernel, 128, ns, g2b, a);
-    else FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
-    if (dkdv_env && dkdv_v == 2 && T % 128 == 0) {  // opt-in at Dh = 128 (occupancy 1)
-      dim3 g3(T / 128, B * Hkv * qs);
-      FA_DISPATCH(fa::bwd_dkdv2_kernel, 128, ns, g3, a);
-    } else {
-      FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
+    if (run_dq) {
+      if (dq2) FA_DISPATCH(fa::bwd_dq2_kernel, 128, ns, g2b, a);
+      else FA_DISPATCH(fa::bwd_dq_kernel, 128, ns, g2, a);
+    }
+    if (run_dkdv) {
+      if (dkdv_env && dkdv_v == 2 && T % 128 == 0) {  // opt-in at Dh = 128 (occupancy 1)
+        dim3 g3(T / 128, B * Hkv * qs);
+        FA_DISPATCH(fa::bwd_dkdv2_kernel, 128, ns, g3, a);
+      } else {
+        FA_DISPATCH(fa::bwd_dkdv_kernel, 128, ns, g1, a);
+      }
     }
   }
-  if (qs > 1) {
+  if (qs > 1 && run_dkdv) {
     const int KV = Hkv * 2 * Dh;
     dim3 gr((unsigned)((long long)B * T / 16), (unsigned)((KV / 4 + 255) / 256));
     if (Dh == 64) hipLaunchKernelGGL(fa::dkdv_reduce_kernel<64>, gr, dim3(256), 0, st, a);

@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from ._ext import gpu_ext, require_dtype
+from .streams import side_stream
 
 
 def _qkv_layout(B, T, H, Hkv, Dh):
@@ -109,6 +110,11 @@ class _CausalAttention(torch.autograd.Function):
         return dqkv, None, None, None, None, None
 
 
+# RTDC_FA_CONCURRENT=1: the flash backward's dQ and dK/dV passes on two streams (delta computed
+# by its own kernel first); 0: both on the compute stream, dQ first (it stores delta)
+_FA_CONCURRENT = os.environ.get("RTDC_FA_CONCURRENT", "0") == "1"
+
+
 class _FlashAttention(torch.autograd.Function):
     """Fused causal flash attention (csrc/kernels/attn_flash.hip): no T x T matrix in HBM."""
 
@@ -135,7 +141,25 @@ class _FlashAttention(torch.autograd.Function):
         cs = torch.empty((B * T // 16, Wd), dtype=torch.float32, device=qkv.device) if G.partials_wanted() else None
         qs = _dkdv_head_split(B, T, H, Hkv, qkv.device)
         part = torch.empty(qs * B * T * Hkv * 2 * Dh, dtype=torch.float32, device=qkv.device) if qs > 1 else None
-        gpu_ext().flash_bwd(qkv, out, dout.contiguous(), lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs, part, qs)
+        dout = dout.contiguous()
+        if _FA_CONCURRENT:
+            # delta alone first, then the dQ pass here and the dK/dV pass on a side stream: the two
+            # latency-bound kernels share the CUs and fill each other's causal tails
+            gpu_ext().flash_delta(out, dout, delta, B, T, H, Dh)
+            cur = torch.cuda.current_stream(qkv.device)
+            side = side_stream(qkv.device, "sort")  # (idle in the backward: the token sort runs under the LM head)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                gpu_ext().flash_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs, part, qs,
+                                    which=2, delta_ready=True)
+            gpu_ext().flash_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs, part, qs,
+                                which=1, delta_ready=True)
+            cur.wait_stream(side)
+            for t in (qkv, out, dout, lse, delta, dqkv, cs, part):
+                if t is not None:
+                    t.record_stream(side)
+        else:
+            gpu_ext().flash_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, Hkv, Dh, scale, cs, part, qs)
         if cs is not None:
             G.offer_colsum_partials(dqkv, cs)
         return dqkv, None, None, None, None, None

@@ -12,12 +12,7 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-L=fwd_bias_res,fwd_bias_gelu,dgrad_gelu_cs
-W4=$PWD/abv/_C_w4.so
-step kt_w4 600 env RTDC_EXT_SO=$W4 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm or linear or mlp" --timeout 120 --timeout-method thread
-step gemm_w4 400 env RTDC_EXT_SO=$W4 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_head 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_w4b 400 env RTDC_EXT_SO=$W4 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-step gemm_headb 400 python -u benchmarks/gemm_bench.py --set gpt2 --layouts $L --reps 20
-bash scripts/gpu.sh envab TAG=w4 ROUNDS=3 STEPS=30 ENVA=RTDC_GELU_SAVE_GRAD=0 ENVB=RTDC_EXT_SO=$W4
-bash scripts/gpu.sh envab TAG=gsg ROUNDS=3 STEPS=30 ENVA=RTDC_GELU_SAVE_GRAD=0 ENVB=RTDC_GELU_SAVE_GRAD=1
+step kt 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "flash or attention" --timeout 120 --timeout-method thread
+step attn 400 python -u benchmarks/attn_bench.py
+step attn2 400 python -u benchmarks/attn_bench.py
+bash scripts/gpu.sh envab TAG=fac ROUNDS=3 STEPS=30 ENVA=RTDC_FA_CONCURRENT=0 ENVB=RTDC_FA_CONCURRENT=1

@@ -940,6 +940,28 @@ def test_flash_attention_deterministic():
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("H,Hkv,Dh", [(12, 12, 64), (8, 2, 128)])
+def test_flash_bwd_concurrent_passes_match(monkeypatch, H, Hkv, Dh):
+    """RTDC_FA_CONCURRENT: delta by its own kernel, then the dQ and dK/dV passes on two streams -
+    bitwise deterministic, and equal to the sequential pass up to delta's summation order."""
+    from ray_torch_distributed_checkpoint_amd.ops import attention as A
+
+    torch.manual_seed(23)
+    B, T = 2, 512
+    qkv = _bf(B, T, (H + 2 * Hkv) * Dh)
+    g = _bf(B, T, H * Dh)
+    grads = {}
+    for mode in (False, True, True):
+        monkeypatch.setattr(A, "_FA_CONCURRENT", mode)
+        x = qkv.clone().requires_grad_(True)
+        A.causal_attention(x, H, Hkv).backward(g)
+        torch.cuda.synchronize()
+        grads.setdefault(mode, []).append(x.grad.float())
+    seq, (c1, c2) = grads[False][0], grads[True]
+    assert torch.equal(c1, c2)
+    assert (c1 - seq).abs().max() / seq.abs().max() < 1e-2
+
+
 @pytest.mark.parametrize("M,K,N,p", [(16, 784, 512, 0.25), (16, 512, 512, 0.25), (37, 100, 130, 0.5)])
 def test_fp32_linear_fused_dropout_equals_separate_kernel(M, K, N, p):
     """Linear + ReLU + Dropout as one fp32 GEMM (Philox mask in the epilogue) == the GEMM with
