@@ -12,7 +12,6 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step kt 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "flash or attention" --timeout 120 --timeout-method thread
-step attn 400 python -u benchmarks/attn_bench.py
-step attn2 400 python -u benchmarks/attn_bench.py
-bash scripts/gpu.sh envab TAG=fac ROUNDS=3 STEPS=30 ENVA=RTDC_FA_CONCURRENT=0 ENVB=RTDC_FA_CONCURRENT=1
+step final3_gpu_tests 700 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread
+step final3_smoke 240 python -c 'import __graft_entry__ as g; g.smoke()'
+step final3_bench_gpt2 500 python bench.py
