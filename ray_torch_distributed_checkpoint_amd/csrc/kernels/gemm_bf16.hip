@@ -709,6 +709,12 @@ static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, doub
   return best;
 }
 
+// RTDC_GEMM_FEW_ROWS_X=0 drops pick_cfg_few_rows' measured exceptions (A/B)
+static bool few_rows_exceptions() {
+  const char* e = getenv("RTDC_GEMM_FEW_ROWS_X");
+  return !(e && e[0] == '0');
+}
+
 // Few-row-tile products (M <= 4096: Llama-3-8B at 2048 tokens per GPU) with a K-major A and a
 // bf16 output: choose among the 8-wave tiles by a wave-quantised time model instead of the
 // M = 16384 rules of pick_cfg.  At M = 2048 an N = 4096 output is only 128 tiles of 256x256 -
@@ -717,13 +723,7 @@ static int pick_splitk(const GemmArgs& a, long long tiles, int slots = 512, doub
 // benchmarks/gemm_bench.py --set llama --sweep (profiles/gemm_llama_sweep_r4.jsonl):
 //   256x256  1.74 (1.58 persistent, > 256 tiles)   256x192  1.42 fwd / 1.37 dgrad
 //   256x128  1.10 fwd / 1.16 dgrad
-// Returns the cfg (6 / 7 / 11), or -1 when the product is outside this regime.
-// RTDC_GEMM_FEW_ROWS_X=0 drops pick_cfg_few_rows' measured exceptions (A/B)
-static bool few_rows_exceptions() {
-  const char* e = getenv("RTDC_GEMM_FEW_ROWS_X");
-  return !(e && e[0] == '0');
-}
-
+// Returns the cfg (6 / 7 / 11 / 12 / 13, or 0 under the measured exceptions below).
 static int pick_cfg_few_rows(const GemmArgs& a, bool b_kmajor, bool can_split) {
   const int kt = a.K / gemm::BK, tm = (a.M + 255) / 256;
   const double slab_us = (double)a.M * a.N * 8.0 / 4.0e6;
