@@ -12,6 +12,10 @@ step() {  # step <name> <timeout> <cmd...>
   echo "[$name] EXIT $rc"; tail -n 2 "gpurun_out/$name.log" | cut -c1-300
   if [ $rc -gt 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step final3_gpu_tests 700 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread
-step final3_smoke 240 python -c 'import __graft_entry__ as g; g.smoke()'
-step final3_bench_gpt2 500 python bench.py
+step attn_def 300 python -u benchmarks/attn_bench.py --only gpt2
+step attn_fwd2 300 env RTDC_FA_FWD=2 python -u benchmarks/attn_bench.py --only gpt2
+step attn_fwd3 300 env RTDC_FA_FWD=3 python -u benchmarks/attn_bench.py --only gpt2
+step attn_dq1 300 env RTDC_FA_DQ=1 python -u benchmarks/attn_bench.py --only gpt2
+step attn_dkdv1 300 env RTDC_FA_DKDV=1 python -u benchmarks/attn_bench.py --only gpt2
+step attn_ns3 300 env RTDC_FA_NS=3 python -u benchmarks/attn_bench.py --only gpt2
+step attn_def2 300 python -u benchmarks/attn_bench.py --only gpt2
